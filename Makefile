@@ -1,0 +1,53 @@
+# Builds (all in-tree so the .so files travel to the GPU box with the snapshot):
+#   intent-mpc_amd/lib/libimpc_qp.so      product: HIP kernels (gfx950) + C-ABI + host symbolic
+#                                         analysis + MPC->QP builder
+#   oracle/build/libosqp_oracle.so        test oracle: C restatement of OSQP 0.6.2 (gcc)
+#   tests/native/build/libimpc_core_cpu.so test-only CPU build of admm_core.hpp (debug harness)
+HIPCC   ?= /opt/rocm/bin/hipcc
+ARCH    ?= gfx950
+CC      ?= gcc
+ROOT    := $(abspath $(dir $(lastword $(MAKEFILE_LIST))))
+CSRC    := $(ROOT)/intent-mpc_amd/csrc
+LIBDIR  := $(ROOT)/intent-mpc_amd/lib
+ORADIR  := $(ROOT)/oracle/build
+HARNDIR := $(ROOT)/tests/native/build
+
+HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
+HOSTFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -Wall
+
+LIB     := $(LIBDIR)/libimpc_qp.so
+ORACLE  := $(ORADIR)/libosqp_oracle.so
+HARNESS := $(HARNDIR)/libimpc_core_cpu.so
+
+.PHONY: all lib oracle harness clean
+all: lib oracle harness
+lib: $(LIB)
+oracle: $(ORACLE)
+harness: $(HARNESS)
+
+$(LIBDIR)/impc_qp.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symbolic.hpp $(ROOT)/include/impc_qp.h
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/symbolic.o: $(CSRC)/symbolic.cpp $(CSRC)/symbolic.hpp
+	@mkdir -p $(LIBDIR)
+	$(CXX) $(HOSTFLAGS) -c $< -o $@
+
+$(LIBDIR)/mpc_qp.o: $(CSRC)/mpc_qp.cpp $(ROOT)/include/impc_mpc.h
+	@mkdir -p $(LIBDIR)
+	$(CXX) $(HOSTFLAGS) -c $< -o $@
+
+$(LIB): $(LIBDIR)/impc_qp.o $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ -o $@
+
+$(ORACLE): $(ROOT)/oracle/osqp_oracle.c
+	@mkdir -p $(ORADIR)
+	$(CC) -O2 -fPIC -shared -std=c11 -ffp-contract=off -Wall -o $@ $< -lm -lpthread
+
+$(HARNESS): $(ROOT)/tests/native/core_harness.cpp $(CSRC)/admm_core.hpp $(CSRC)/symbolic.cpp $(CSRC)/symbolic.hpp
+	@mkdir -p $(HARNDIR)
+	$(HIPCC) -x hip -O2 -std=c++17 -fPIC -shared --offload-arch=$(ARCH) -ffp-contract=off \
+		$(ROOT)/tests/native/core_harness.cpp -x c++ $(CSRC)/symbolic.cpp -o $@
+
+clean:
+	rm -rf $(LIBDIR) $(ORADIR) $(HARNDIR)

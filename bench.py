@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""Benchmark of the batched MPC QP solve (BASELINE.json metric) on MI355X.
+
+One step = one pass of the hot path over one batch: for every QP of the workload, the device
+runs osqp_setup's numeric part (Ruiz scaling, rho vector, factorisation of P + sigma I + A'RA),
+the warm start, osqp_solve (ADMM to OSQP 0.6.2's termination) and the unscaling of x, y --
+i.e. everything mpcPlanner::solveTraj asks OsqpEigen for (mpcPlanner.cpp:475-526).  Inputs
+(P, q, A, l, u and the warm start) are resident in HBM before the timed region.
+
+Workload (BASELINE.json configs[2], the metric's batch=65536): per GPU 8192 planning instances x
+8 intent hypotheses, N=20, 8 predicted dynamic obstacles (hypotheses LEFT+FORWARD / RIGHT+FORWARD
+carry a 9th), synthetic data from impc.scenarios.intent_config, bucketed by obstacle count.
+
+Multi-GPU: one process per GPU (torchrun), each rank solves its own 65536 QPs (independent
+instances, weak scaling, no data-path collective); an all_gather of the per-QP cost/status
+records returns the hypothesis costs to every rank, outside the timed region.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "intent-mpc_amd", "python"))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PEAK_FP64_TFLOPS = 78.6    # MI355X FP64 vector peak (spec)
+
+
+def algorithmic_bytes(n, m, K, N):
+    """B_solve = 8(n + 2m + 4K W) + 8(n + m) + 16 per QP."""
+    W = N - 1
+    return 8 * (n + 2 * m + 4 * K * W) + 8 * (n + m) + 16
+
+
+def algorithmic_flops(n, m, nnzA, N, iters):
+    """F_iter ~ 754 N + 4 nnzA + 4m + 6n + 10m per ADMM iteration."""
+    return iters * (754 * N + 4 * nnzA + 4 * m + 6 * n + 10 * m) + 3700 * N
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--instances", type=int, default=8192, help="planning instances per GPU (x8 hypotheses)")
+    ap.add_argument("--cpu-sample", type=int, default=1024, help="QPs solved by the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-allgather", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist = tdist
+
+    import impc
+    from impc import scenarios
+
+    t_gen = time.time()
+    buckets = scenarios.intent_config(N=20, K=8, instances=args.instances, hyps=8, seed=3000 + 7919 * rank)
+    t_gen = time.time() - t_gen
+    settings = impc.default_settings(verbose=0)
+
+    ctx = impc.Context(local_rank if world > 1 else 0)
+    batches = []
+    for K, bk in sorted(buckets.items()):
+        pat, vals = bk["pattern"], bk["values"]
+        B = vals["q"].shape[0]
+        b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], B)
+        b.set_settings(settings)
+        b.set_values(vals["Px"], vals["q"], vals["Ax"], vals["l"], vals["u"])
+        b.warm_start(bk["x_ws"], np.zeros((B, pat["m"])))
+        b.set_profiling(True)
+        batches.append((K, bk, b))
+    total_qps = sum(b.B for _, _, b in batches)
+
+    def step():
+        for _, _, b in batches:
+            b.setup()
+            b.solve()
+
+    def sync():
+        ctx.synchronize()  # hipStreamSynchronize + hipDeviceSynchronize
+
+    for _ in range(args.warmup):
+        step()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    # timed region: barrier + device sync on both sides
+    t0 = time.perf_counter()
+    kt = {K: [0.0, 0.0, 0.0] for K, _, _ in batches}
+    for _ in range(args.steps):
+        step()
+    sync()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    # per-kernel durations of the last step (HIP events on the solver stream)
+    for K, _, b in batches:
+        kt[K] = list(b.timings())
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = 1000.0 * elapsed / args.steps
+
+    # results + parity-relevant statistics (outside the timed region)
+    iters_all, status_all = [], []
+    costs = []
+    for K, bk, b in batches:
+        x, y, info = b.get()
+        iters_all.append(info["iter"])
+        status_all.append(info["status_val"])
+        rec = np.zeros((b.B, 4))
+        rec[:, 0] = bk["inst"]
+        rec[:, 1] = bk["hyp"]
+        rec[:, 2] = info["obj_val"]
+        rec[:, 3] = info["status_val"]
+        costs.append(rec)
+    iters_all = np.concatenate(iters_all)
+    status_all = np.concatenate(status_all)
+    if dist is not None and not args.no_allgather:
+        import torch
+        local = torch.tensor(np.concatenate(costs), device="cuda", dtype=torch.float64)
+        gathered = [torch.empty_like(local) for _ in range(world)]
+        dist.all_gather(gathered, local)  # hypothesis costs to every rank
+
+    value = world * total_qps / elapsed  # whole-job QP solves per second
+
+    # roofline of the dominant kernel (k_solve), SURVEY.md 8(d) algorithmic bytes
+    solve_ms = sum(kt[K][1] for K in kt)
+    setup_ms = sum(kt[K][0] for K in kt)
+    alg_bytes = 0.0
+    alg_flops = 0.0
+    for K, bk, b in batches:
+        pat = bk["pattern"]
+        alg_bytes += b.B * algorithmic_bytes(pat["n"], pat["m"], K, 20)
+    mean_iter = float(iters_all.mean())
+    for K, bk, b in batches:
+        pat = bk["pattern"]
+        alg_flops += b.B * algorithmic_flops(pat["n"], pat["m"], int(pat["Ap"][-1]), 20, mean_iter)
+    achieved = alg_bytes / (solve_ms * 1e-3) / 1e9 if solve_ms > 0 else None
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_k_solve.json")
+    if os.path.exists(pmc_path):
+        try:
+            pm = json.load(open(pmc_path))
+            if pm.get("qps_per_launch") == total_qps:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        cpu = cpu_baseline(buckets, settings, args.cpu_sample, args.cpu_threads)
+
+    line = {
+        "metric": "QP-solves/s + p50 solve latency, N=20 horizon, batch=65536, 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "QP-solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "p50_latency_ms": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded intent-hypothesis scenarios, SURVEY.md 8d)",
+        "config": {
+            "workload": "configs[2]: 8192 instances x 8 intent hypotheses per GPU, N=20, 8(+1) dynamic obstacles",
+            "global_batch": world * total_qps,
+            "batch_per_gpu": total_qps,
+            "buckets": {str(K): int(b.B) for K, _, b in batches},
+            "horizon": 20,
+            "settings": "OSQP 0.6.2 defaults, adaptive_rho_interval auto->25, warm-started from previous plan",
+            "parallelism": f"independent QPs, {world} rank(s)",
+        },
+        "iters": {"mean": mean_iter, "p50": float(np.median(iters_all)), "max": int(iters_all.max())},
+        "status_counts": {str(int(k)): int(v) for k, v in zip(*np.unique(status_all, return_counts=True))},
+        "kernel_ms": {"k_setup": setup_ms, "k_solve": solve_ms,
+                      "outputs": sum(kt[K][2] for K in kt)},
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": PEAK_HBM_GBS,
+            "unit": "GB/s",
+            "frac": (achieved / PEAK_HBM_GBS) if achieved else None,
+            "traffic": traffic,
+            "kernel": "k_solve",
+            "algorithmic_bytes_per_launch": alg_bytes,
+        },
+        "fp64": {"achieved_tflops": alg_flops / ((solve_ms + setup_ms) * 1e-3) / 1e12 if solve_ms else None,
+                 "peak_tflops": PEAK_FP64_TFLOPS},
+        "cpu_baseline": cpu,
+        "gen_seconds": t_gen,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    for _, _, b in batches:
+        b.close()
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(buckets, settings, sample, threads):
+    """The oracle (C restatement of OSQP 0.6.2, reference per-call pattern) on host cores,
+    over a bounded sample of the same workload (first QPs of each bucket, bucket-proportional)."""
+    from oracle import osqp_oracle as ora
+    total = sum(bk["values"]["q"].shape[0] for bk in buckets.values())
+    s = ora.settings_from(settings)
+    t_all, n_all = 0.0, 0
+    for K, bk in sorted(buckets.items()):
+        B = bk["values"]["q"].shape[0]
+        k = max(1, int(round(sample * B / total)))
+        v = bk["values"]
+        t = time.perf_counter()
+        ora.solve_batch(bk["pattern"], v["Px"][:k], v["q"][:k], v["Ax"][:k], v["l"][:k], v["u"][:k], s,
+                        x_ws=bk["x_ws"][:k], threads=threads)
+        t_all += time.perf_counter() - t
+        n_all += k
+    return {"value": n_all / t_all, "unit": "QP-solves/s", "cores": threads, "kind": "port",
+            "sample": f"{n_all} QPs of the same workload (first of each bucket), one setup+warm-start+solve per QP"}
+
+
+if __name__ == "__main__":
+    main()

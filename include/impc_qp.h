@@ -1,0 +1,186 @@
+/*
+ * impc_qp.h -- C-ABI of the MI355X batched OSQP-0.6.2-equivalent QP solver (libimpc_qp.so).
+ *
+ * Drop-in boundary: the OsqpEigen::Solver call sequence mpcPlanner::solveTraj makes for every
+ * QP (reference trajectory_planner/include/trajectory_planner/mpcPlanner.cpp:436-527):
+ *
+ *   reference call (file:line)                               replaced by
+ *   ------------------------------------------------------   -------------------------------
+ *   OsqpEigen::Solver solver;            mpcPlanner.cpp:436  impc_ctx_create + impc_batch_create
+ *   settings()->setVerbosity/WarmStart/TimeLimit   :440-444  impc_default_settings +
+ *     (OsqpEigen Settings.hpp:172-196 -> OSQPSettings          impc_batch_set_settings
+ *      types.h:139-176)
+ *   data()->setNumberOfVariables/Constraints       :450-452  impc_batch_create(n, m, ...)
+ *   data()->setHessianMatrix   (Data.tpp:13-50, upper)  :453  impc_batch_create (pattern) +
+ *   data()->setLinearConstraintsMatrix (Data.tpp:52-87) :461    impc_batch_set_values (values)
+ *   data()->setGradient/setLowerBound/setUpperBound :457-469  impc_batch_set_values
+ *   initSolver()  -> osqp_setup (osqp.h:58)              :475  impc_batch_setup (device)
+ *   setWarmStart(x, y) -> osqp_warm_start (osqp.h:157)   :509  impc_batch_warm_start
+ *   solveProblem() -> osqp_solve (osqp.h:78)             :513  impc_batch_solve
+ *   getSolution()                (Solver.hpp:131)        :526  impc_batch_get
+ *   clearSolver() -> osqp_cleanup (osqp.h:90)            :527  impc_batch_destroy
+ *   updateGradient/updateBounds (Solver.hpp:151-182;          impc_batch_update_lin_cost /
+ *     osqp_update_lin_cost/bounds osqp.h:114-134)               impc_batch_update_bounds
+ *
+ * One batch = B independent QPs that share one sparsity pattern (the reference's QPs of one
+ * (N, #obstacles) shape share it by construction).  Per-QP host arrays are QP-major: QP b's
+ * block starts at b * len.  Indices are int64 (OSQP c_int with DLONG, osqp_configure.h:31),
+ * values double (c_float).  Status and error codes are OSQP 0.6.2's (constants.h:18-51).
+ *
+ * Threading: a context and its batches belong to one host thread; solves are asynchronous on
+ * the HIP stream passed in (NULL = the context's own stream); impc_batch_get synchronises.
+ */
+#ifndef IMPC_QP_H
+#define IMPC_QP_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* OSQP status values (constants.h:18-30) */
+#define IMPC_DUAL_INFEASIBLE_INACCURATE 4
+#define IMPC_PRIMAL_INFEASIBLE_INACCURATE 3
+#define IMPC_SOLVED_INACCURATE 2
+#define IMPC_SOLVED 1
+#define IMPC_MAX_ITER_REACHED (-2)
+#define IMPC_PRIMAL_INFEASIBLE (-3)
+#define IMPC_DUAL_INFEASIBLE (-4)
+#define IMPC_TIME_LIMIT_REACHED (-6)
+#define IMPC_NON_CVX (-7)
+#define IMPC_UNSOLVED (-10)
+
+/* OSQP error values (constants.h:43-51) plus library-level errors */
+#define IMPC_OK 0
+#define IMPC_DATA_VALIDATION_ERROR 1
+#define IMPC_SETTINGS_VALIDATION_ERROR 2
+#define IMPC_LINSYS_SOLVER_INIT_ERROR 4
+#define IMPC_NONCVX_ERROR 5
+#define IMPC_MEM_ALLOC_ERROR 6
+#define IMPC_WORKSPACE_NOT_INIT_ERROR 7
+#define IMPC_DEVICE_ERROR 100
+#define IMPC_INVALID_ARGUMENT 101
+#define IMPC_UNSUPPORTED 102
+
+/* Field-for-field mirror of OSQPSettings (types.h:139-176, PROFILING build). */
+typedef struct {
+    double rho;
+    double sigma;
+    int64_t scaling;
+    int64_t adaptive_rho;
+    int64_t adaptive_rho_interval; /* 0 = automatic: resolved to check_termination */
+    double adaptive_rho_tolerance;
+    double adaptive_rho_fraction;
+    int64_t max_iter;
+    double eps_abs;
+    double eps_rel;
+    double eps_prim_inf;
+    double eps_dual_inf;
+    double alpha;
+    int64_t linsys_solver; /* accepted for API parity; the device factorisation is always used */
+    double delta;
+    int64_t polish; /* must be 0 (the reference never polishes); 1 -> IMPC_UNSUPPORTED */
+    int64_t polish_refine_iter;
+    int64_t verbose; /* ignored (no printing on device) */
+    int64_t scaled_termination;
+    int64_t check_termination;
+    int64_t warm_start;
+    double time_limit; /* seconds per QP, measured on the device clock from the QP's ADMM start; 0 = off */
+} impc_settings;
+
+/* Subset of OSQPInfo (types.h:66-89), one per QP. */
+typedef struct {
+    int64_t iter;
+    int64_t status_val;
+    int64_t rho_updates;
+    int64_t setup_exitflag; /* per-QP osqp_setup outcome: 0, or IMPC_NONCVX_ERROR */
+    double obj_val;
+    double pri_res;
+    double dua_res;
+    double rho_estimate;
+} impc_info;
+
+typedef struct impc_ctx_s *impc_ctx;
+typedef struct impc_batch_s *impc_batch;
+
+/* osqp_set_default_settings (osqp.h:32) */
+void impc_default_settings(impc_settings *s);
+
+/* Message of the last error on this host thread. */
+const char *impc_last_error(void);
+
+/* Library/ABI version string. */
+const char *impc_version(void);
+
+int impc_ctx_create(int device, impc_ctx *out);
+int impc_ctx_destroy(impc_ctx ctx);
+/* The context's HIP stream (hipStream_t), for callers that want to enqueue around solves. */
+void *impc_ctx_stream(impc_ctx ctx);
+/* Block until all work of this context's device has finished (hipDeviceSynchronize). */
+int impc_ctx_synchronize(impc_ctx ctx);
+
+/* Shared pattern: P (n x n, upper triangle, CSC Pp[n+1]/Pi[nnzP]) and A (m x n, CSC Ap[n+1]/
+ * Ai[nnzA]).  Runs the symbolic analysis (fill-reducing ordering of P + sigma I + A' R A, its
+ * envelope, assembly schedule) once and allocates device storage for `batch` QPs. */
+int impc_batch_create(impc_ctx ctx, int64_t n, int64_t m, const int64_t *Pp, const int64_t *Pi, const int64_t *Ap,
+                      const int64_t *Ai, int64_t batch, impc_batch *out);
+int impc_batch_destroy(impc_batch b);
+
+int impc_batch_set_settings(impc_batch b, const impc_settings *s);
+
+/* Per-QP values, host, QP-major: Px [B][nnzP], q [B][n], Ax [B][nnzA], l [B][m], u [B][m].
+ * Validated like osqp_setup's validate_data (l <= u).  Copied to the device (stream-ordered). */
+int impc_batch_set_values(impc_batch b, const double *Px, const double *q, const double *Ax, const double *l,
+                          const double *u);
+/* Same, from device-resident QP-major arrays (no host round trip; validation skipped). */
+int impc_batch_set_values_device(impc_batch b, const double *Px, const double *q, const double *Ax, const double *l,
+                                 const double *u);
+
+/* osqp_warm_start(x, y) for every QP (host, QP-major; y may be NULL = zero duals).
+ * Pass x = NULL to clear a previous warm start (cold start). */
+int impc_batch_warm_start(impc_batch b, const double *x, const double *y);
+
+/* osqp_setup's numeric part on the device: Ruiz scaling, rho vector, KKT assembly and
+ * factorisation, then the pending warm start.  Asynchronous on `stream` (NULL = ctx stream). */
+int impc_batch_setup(impc_batch b, void *stream);
+
+/* osqp_solve on the device for every QP (ADMM, termination, adaptive rho with in-kernel
+ * refactorisation, unscaling).  Runs impc_batch_setup first if values changed since the last
+ * setup.  Asynchronous on `stream`. */
+int impc_batch_solve(impc_batch b, void *stream);
+
+/* Synchronise and copy results to host (any pointer may be NULL): x [B][n], y [B][m], info [B]. */
+int impc_batch_get(impc_batch b, double *x, double *y, impc_info *info);
+
+/* Device pointers of the QP-major result arrays, valid until the next solve / destroy. */
+int impc_batch_device_results(impc_batch b, double **x, double **y, impc_info **info);
+
+/* Persistent-workspace updates (osqp_update_lin_cost / osqp_update_bounds, osqp.h:114-134):
+ * rescale with the existing scaling, keep the factorisation unless a constraint changes type
+ * (equality / inequality / loose), and keep the iterates as the next warm start. */
+int impc_batch_update_lin_cost(impc_batch b, const double *q);
+int impc_batch_update_bounds(impc_batch b, const double *l, const double *u);
+
+/* Problem / analysis facts (for tests and roofline accounting). */
+typedef struct {
+    int64_t n, m, nnzP, nnzA, batch, batch_stride;
+    int64_t nnzL;        /* envelope entries of the factor of P + sigma I + A' R A */
+    int64_t nnzLcol;     /* column-envelope entries */
+    int64_t n_terms;     /* A' R A assembly terms */
+    int64_t bandwidth;   /* max row length of the envelope */
+    int64_t device_bytes;
+} impc_batch_stats;
+int impc_batch_get_stats(impc_batch b, impc_batch_stats *out);
+
+/* Kernel timing with HIP events recorded on the solve stream around k_setup, k_solve and the
+ * output transposes (profiling on: events are recorded by every subsequent setup/solve). */
+int impc_batch_set_profiling(impc_batch b, int on);
+/* Durations (ms) of the last profiled setup / solve-kernel / output-transpose launches. */
+int impc_batch_get_timings(impc_batch b, double *setup_ms, double *solve_ms, double *output_ms);
+
+/* Factor-order permutation chosen by the symbolic analysis (perm[k] = variable at position k). */
+int impc_batch_get_perm(impc_batch b, int64_t *perm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

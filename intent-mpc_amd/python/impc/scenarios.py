@@ -1,0 +1,167 @@
+"""Seeded synthetic MPC workloads for tests and bench.py.
+
+Produces the per-instance inputs mpcPlanner::solveTraj consumes (current state, reference
+trajectory, previous plan, obstacles / intent predictions) and turns them into batched QPs with
+the product builder (impc_mpc_build_values).  Synthetic data only: the reference's Gazebo /
+DYNUS worlds are not available, so obstacle placement follows the distributions SURVEY.md 8d
+derives from dynus_obstacles_node.cpp:74-133 and the predictor's 4-intent models
+(dynamicPredictor.cpp:351-501: FORWARD / LEFT / RIGHT / STOP at 0.1 s steps).
+"""
+import math
+
+import numpy as np
+
+from . import mpc_params, mpc_pattern, mpc_values
+
+# dynamicPredictor utils.h:15-20 intent enum order
+FORWARD, LEFT, RIGHT, STOP = 0, 1, 2, 3
+PRED_STEPS = 30  # predictor_param.yaml:2 (30 steps @ 0.1 s) -> 31 positions
+
+
+def _x0(rng, nb):
+    pos = np.stack([np.zeros(nb), rng.uniform(-1, 1, nb), rng.uniform(1.5, 2.5, nb)], axis=1)
+    vel = np.stack([rng.uniform(0, 5, nb), rng.uniform(-1, 1, nb), np.zeros(nb)], axis=1)
+    return pos, vel
+
+
+def _xref(rng, pos, N):
+    nb = pos.shape[0]
+    step = rng.uniform(0.5, 2.5, nb)  # m per 0.1 s step (ref_trajectory_dynus_benchmark.txt spacing)
+    xr = np.zeros((nb, N, 8))
+    k = np.arange(N)
+    xr[:, :, 0] = pos[:, None, 0] + k[None, :] * step[:, None]
+    xr[:, :, 1] = pos[:, None, 1]
+    xr[:, :, 2] = pos[:, None, 2]
+    return xr
+
+
+def _prev_plan(pos, vel, N, ts):
+    """A previous receding-horizon plan (currentStatesSol_): constant-velocity rollout."""
+    nb = pos.shape[0]
+    st = np.zeros((nb, N, 8))
+    k = np.arange(N) * ts
+    st[:, :, 0:3] = pos[:, None, :] + k[None, :, None] * vel[:, None, :]
+    st[:, :, 3:6] = vel[:, None, :]
+    return st
+
+
+def static_config(N=20, K=10, batch=4096, seed=2000, identical=True, params=None):
+    """Config 2: batch of N=20 QPs with K static-style obstacle rows (copies of one seed if identical)."""
+    p, pd = params if params is not None else mpc_params(horizon=N)
+    rng = np.random.default_rng(seed)
+    nb = 1 if identical else batch
+    pos, vel = _x0(rng, nb)
+    xref = _xref(rng, pos, N)
+    cen = np.stack([pos[:, None, 0] + rng.uniform(2, 20, (nb, K)), rng.uniform(-5, 5, (nb, K)),
+                    rng.uniform(0.5, 4.5, (nb, K))], axis=2)
+    tall = rng.uniform(size=(nb, K)) < 0.5
+    size = np.where(tall[:, :, None], np.array([0.4, 0.4, 4.0]), np.array([0.4, 4.0, 0.4]))
+    yaw = rng.uniform(-math.pi, math.pi, (nb, K))
+    if identical:
+        rep = lambda a: np.repeat(a, batch, axis=0)
+        pos, vel, xref, cen, size, yaw = map(rep, (pos, vel, xref, cen, size, yaw))
+    pat = mpc_pattern(p, K, 0)
+    vals = mpc_values(p, pos, vel, xref, None, st_centroid=cen, st_size=size, st_yaw=yaw)
+    return dict(pattern=pat, values=vals, x_ws=None, params=pd, K=K, N=N)
+
+
+def predict_intents(p0, v0, steps=PRED_STEPS, ts=0.1, omega=0.6, stop_time=1.0):
+    """[..., 4 intents, steps+1, 3] kinematic predictions (FORWARD/LEFT/RIGHT/STOP)."""
+    t = np.arange(steps + 1) * ts
+    sp = np.linalg.norm(v0[..., :2], axis=-1)
+    hd = np.arctan2(v0[..., 1], v0[..., 0])
+    out = np.zeros(p0.shape[:-1] + (4, steps + 1, 3))
+    # FORWARD: constant velocity
+    out[..., FORWARD, :, :] = p0[..., None, :] + t[:, None] * v0[..., None, :]
+    # LEFT / RIGHT: constant-speed turn at +-omega
+    for idx, sgn in ((LEFT, 1.0), (RIGHT, -1.0)):
+        w = sgn * omega
+        h = hd[..., None] + w * t
+        out[..., idx, :, 0] = p0[..., None, 0] + sp[..., None] / w * (np.sin(h) - np.sin(hd[..., None]))
+        out[..., idx, :, 1] = p0[..., None, 1] - sp[..., None] / w * (np.cos(h) - np.cos(hd[..., None]))
+        out[..., idx, :, 2] = p0[..., None, 2]
+    # STOP: linear deceleration to rest over stop_time
+    tt = np.minimum(t, stop_time)
+    frac = tt - tt * tt / (2 * stop_time)
+    out[..., STOP, :, :] = p0[..., None, :] + frac[:, None] * v0[..., None, :]
+    return out
+
+
+def intent_config(N=20, K=8, instances=8192, hyps=8, seed=3000, params=None):
+    """Config 3: `instances` planning instances x `hyps` hypotheses, K dynamic obstacles each.
+
+    Hypotheses 0-5 are mpcPlanner::getIntentComb's six combinations for the closest obstacle
+    (mpcPlanner.cpp:710-769, sorted by intent weight; the LEFT+FORWARD / RIGHT+FORWARD ones carry
+    K+1 obstacle trajectories), 6-7 are extra argmax variants (all-argmax, all-FORWARD).
+    Returns the QPs bucketed by obstacle count: {K: bucket, K+1: bucket}; each bucket has
+    pattern, values, warm start and the (instance, hypothesis) of every QP.
+    """
+    p, pd = params if params is not None else mpc_params(horizon=N)
+    rng = np.random.default_rng(seed)
+    ts = pd["ts"]
+    I = instances
+    pos, vel = _x0(rng, I)
+    xref = _xref(rng, pos, N)
+    prev = _prev_plan(pos, vel, N, ts)
+    obp = np.stack([pos[:, None, 0] + rng.uniform(3, 15, (I, K)), rng.uniform(-4, 4, (I, K)),
+                    rng.uniform(1.0, 3.0, (I, K))], axis=2)
+    spd = rng.uniform(0.5, 2.0, (I, K))
+    hdg = rng.uniform(-math.pi, math.pi, (I, K))
+    obv = np.stack([spd * np.cos(hdg), spd * np.sin(hdg), np.zeros((I, K))], axis=2)
+    pred = predict_intents(obp, obv, ts=ts)                 # [I, K, 4, 31, 3]
+    prob = rng.dirichlet(np.ones(4), size=(I, K))            # [I, K, 4]
+    size = np.full(3, 0.8)                                   # dynus_obstacles_node.cpp:81 cubes
+    # findClosestObstacle (first-time branch, :663-674): nearest current position
+    d = np.linalg.norm(obp - pos[:, None, :], axis=2)
+    ob = np.argmin(d, axis=1)
+    argmax_int = np.argmax(prob, axis=2)                     # [I, K]
+    buckets = {}
+    for kk in (K, K + 1):
+        buckets[kk] = dict(dyn_pos=[], inst=[], hyp=[])
+    for i in range(I):
+        o = ob[i]
+        pr = prob[i, o]
+        # getIntentComb weights (:722-728), std::sort ascending, take from the back (:753-756)
+        weight = [(pr[STOP], 0), (pr[LEFT], 1), (pr[RIGHT], 2), (pr[FORWARD], 3),
+                  (max(pr[LEFT], pr[FORWARD]), 4), (max(pr[RIGHT], pr[FORWARD]), 5)]
+        weight.sort()
+        combos = {0: [STOP], 1: [LEFT], 2: [RIGHT], 3: [FORWARD], 4: [LEFT, FORWARD], 5: [RIGHT, FORWARD]}
+        others = [pred[i, j, argmax_int[i, j]] for j in range(K) if j != o]
+        hyp_sets = []
+        for h in range(6):
+            cid = weight[5 - h][1]
+            hyp_sets.append([pred[i, o, it] for it in combos[cid]] + others)
+        hyp_sets.append([pred[i, o, argmax_int[i, o]]] + others)
+        hyp_sets.append([pred[i, j, FORWARD] for j in range(K)])
+        for h, sets in enumerate(hyp_sets[:hyps]):
+            kk = len(sets)
+            buckets[kk]["dyn_pos"].append(np.stack(sets))
+            buckets[kk]["inst"].append(i)
+            buckets[kk]["hyp"].append(h)
+    out = {}
+    for kk, bk in buckets.items():
+        if not bk["inst"]:
+            continue
+        inst = np.array(bk["inst"])
+        dp = np.stack(bk["dyn_pos"])                         # [nb, kk, 31, 3]
+        ds = np.broadcast_to(size, dp.shape).copy()
+        pat = mpc_pattern(p, 0, kk)
+        vals = mpc_values(p, pos[inst], vel[inst], xref[inst], prev[inst], dyn_pos=dp, dyn_size=ds)
+        nb = inst.size
+        n = pat["n"]
+        x_ws = np.zeros((nb, n))
+        x_ws[:, : 8 * N] = prev[inst].reshape(nb, -1)          # solveTraj warm start (:489-498)
+        out[kk] = dict(pattern=pat, values=vals, x_ws=x_ws, inst=inst, hyp=np.array(bk["hyp"]), K=kk, N=N,
+                       params=pd)
+    return out
+
+
+def first_call_config(N=20, batch=1, seed=1000, params=None):
+    """Config 1: the first makePlan() QP -- no obstacles, cold start (mpcPlanner.cpp:543-569)."""
+    p, pd = params if params is not None else mpc_params(horizon=N)
+    rng = np.random.default_rng(seed)
+    pos, vel = _x0(rng, batch)
+    xref = _xref(rng, pos, N)
+    pat = mpc_pattern(p, 0, 0)
+    vals = mpc_values(p, pos, vel, xref, None)
+    return dict(pattern=pat, values=vals, x_ws=None, params=pd, K=0, N=N)
