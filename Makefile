@@ -18,14 +18,16 @@ HOSTFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -Wall
 LIB     := $(LIBDIR)/libimpc_qp.so
 ORACLE  := $(ORADIR)/libosqp_oracle.so
 HARNESS := $(HARNDIR)/libimpc_core_cpu.so
+EMU     := $(HARNDIR)/libwave_emu.so
 
 .PHONY: all lib oracle harness clean
 all: lib oracle harness
 lib: $(LIB)
 oracle: $(ORACLE)
-harness: $(HARNESS)
+harness: $(HARNESS) $(EMU)
 
-$(LIBDIR)/impc_qp.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symbolic.hpp $(ROOT)/include/impc_qp.h
+$(LIBDIR)/impc_qp.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symbolic.hpp $(CSRC)/mpc_wave.hpp \
+		$(CSRC)/mpc_structure.hpp $(ROOT)/include/impc_qp.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -37,7 +39,11 @@ $(LIBDIR)/mpc_qp.o: $(CSRC)/mpc_qp.cpp $(ROOT)/include/impc_mpc.h
 	@mkdir -p $(LIBDIR)
 	$(CXX) $(HOSTFLAGS) -c $< -o $@
 
-$(LIB): $(LIBDIR)/impc_qp.o $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o
+$(LIBDIR)/mpc_structure.o: $(CSRC)/mpc_structure.cpp $(CSRC)/mpc_structure.hpp
+	@mkdir -p $(LIBDIR)
+	$(CXX) $(HOSTFLAGS) -c $< -o $@
+
+$(LIB): $(LIBDIR)/impc_qp.o $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ -o $@
 
 $(ORACLE): $(ROOT)/oracle/osqp_oracle.c
@@ -48,6 +54,12 @@ $(HARNESS): $(ROOT)/tests/native/core_harness.cpp $(CSRC)/admm_core.hpp $(CSRC)/
 	@mkdir -p $(HARNDIR)
 	$(HIPCC) -x hip -O2 -std=c++17 -fPIC -shared --offload-arch=$(ARCH) -ffp-contract=off \
 		$(ROOT)/tests/native/core_harness.cpp -x c++ $(CSRC)/symbolic.cpp -o $@
+
+$(EMU): $(ROOT)/tests/native/wave_emu.cpp $(CSRC)/mpc_wave.hpp $(CSRC)/admm_core.hpp $(CSRC)/mpc_structure.cpp \
+		$(CSRC)/mpc_structure.hpp
+	@mkdir -p $(HARNDIR)
+	$(HIPCC) -x hip --offload-host-only -std=c++20 -O2 -fPIC -shared -ffp-contract=off \
+		$(ROOT)/tests/native/wave_emu.cpp -x c++ $(CSRC)/mpc_structure.cpp -o $@
 
 clean:
 	rm -rf $(LIBDIR) $(ORADIR) $(HARNDIR)

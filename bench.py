@@ -53,22 +53,16 @@ def main():
     ap.add_argument("--no-allgather", action="store_true")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as tdist
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        dist = tdist
-
     import impc
+    from impc import distributed as D
     from impc import scenarios
 
+    rank, local_rank, world = D.env()
+    dist = D.init("nccl", local_rank) if world > 1 else None
+
+
     t_gen = time.time()
-    buckets = scenarios.intent_config(N=20, K=8, instances=args.instances, hyps=8, seed=3000 + 7919 * rank)
+    buckets = scenarios.intent_config(N=20, K=8, instances=args.instances, hyps=8, seed=D.rank_seed(3000, rank))
     t_gen = time.time() - t_gen
     settings = impc.default_settings(verbose=0)
 
@@ -104,42 +98,33 @@ def main():
     for _ in range(args.steps):
         step()
     sync()
+    if dist is not None:
+        dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
     # per-kernel durations of the last step (HIP events on the solver stream)
     for K, _, b in batches:
         kt[K] = list(b.timings())
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = D.max_over_ranks(dist, elapsed)
     ms_per_step = 1000.0 * elapsed / args.steps
 
     # results + parity-relevant statistics (outside the timed region)
-    iters_all, status_all = [], []
-    costs = []
+    iters_all, status_all, recs = [], [], []
     for K, bk, b in batches:
         x, y, info = b.get()
         iters_all.append(info["iter"])
         status_all.append(info["status_val"])
-        rec = np.zeros((b.B, 4))
-        rec[:, 0] = bk["inst"]
-        rec[:, 1] = bk["hyp"]
-        rec[:, 2] = info["obj_val"]
-        rec[:, 3] = info["status_val"]
-        costs.append(rec)
+        recs.append(D.make_records(rank, bk["inst"], bk["hyp"], info))
     iters_all = np.concatenate(iters_all)
     status_all = np.concatenate(status_all)
-    if dist is not None and not args.no_allgather:
-        import torch
-        local = torch.tensor(np.concatenate(costs), device="cuda", dtype=torch.float64)
-        gathered = [torch.empty_like(local) for _ in range(world)]
-        dist.all_gather(gathered, local)  # hypothesis costs to every rank
+    if not args.no_allgather:
+        D.gather_records(dist, np.concatenate(recs))  # hypothesis costs to every rank
 
     value = world * total_qps / elapsed  # whole-job QP solves per second
 
-    # roofline of the dominant kernel (k_solve), SURVEY.md 8(d) algorithmic bytes
+    # roofline of the dominant kernel, SURVEY.md 8(d) algorithmic bytes
+    kernel_name = "k_mpc_wave" if all(b.stats()["kernel"] == impc.KERNEL_STRUCTURED for _, _, b in batches) \
+        else "k_solve"
     solve_ms = sum(kt[K][1] for K in kt)
     setup_ms = sum(kt[K][0] for K in kt)
     alg_bytes = 0.0
@@ -157,7 +142,7 @@ def main():
     if os.path.exists(pmc_path):
         try:
             pm = json.load(open(pmc_path))
-            if pm.get("qps_per_launch") == total_qps:
+            if pm.get("qps_per_launch") == total_qps and pm.get("kernel") == kernel_name:
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -191,7 +176,7 @@ def main():
         },
         "iters": {"mean": mean_iter, "p50": float(np.median(iters_all)), "max": int(iters_all.max())},
         "status_counts": {str(int(k)): int(v) for k, v in zip(*np.unique(status_all, return_counts=True))},
-        "kernel_ms": {"k_setup": setup_ms, "k_solve": solve_ms,
+        "kernel_ms": {"setup": setup_ms, "solve": solve_ms,
                       "outputs": sum(kt[K][2] for K in kt)},
         "roofline": {
             "bound": "hbm",
@@ -200,7 +185,7 @@ def main():
             "unit": "GB/s",
             "frac": (achieved / PEAK_HBM_GBS) if achieved else None,
             "traffic": traffic,
-            "kernel": "k_solve",
+            "kernel": kernel_name,
             "algorithmic_bytes_per_launch": alg_bytes,
         },
         "fp64": {"achieved_tflops": alg_flops / ((solve_ms + setup_ms) * 1e-3) / 1e12 if solve_ms else None,

@@ -160,6 +160,14 @@ int impc_batch_device_results(impc_batch b, double **x, double **y, impc_info **
 int impc_batch_update_lin_cost(impc_batch b, const double *q);
 int impc_batch_update_bounds(impc_batch b, const double *l, const double *u);
 
+/* Kernel selection.  AUTO picks the one-QP-per-wavefront structured kernel when the pattern is
+ * the stage-structured mpcPlanner QP and fits its register layout, else the
+ * generic one-QP-per-lane kernel.  The persistent update calls need the GENERIC kernel. */
+#define IMPC_KERNEL_AUTO 0
+#define IMPC_KERNEL_GENERIC 1
+#define IMPC_KERNEL_STRUCTURED 2
+int impc_batch_set_kernel(impc_batch b, int kernel);
+
 /* Problem / analysis facts (for tests and roofline accounting). */
 typedef struct {
     int64_t n, m, nnzP, nnzA, batch, batch_stride;
@@ -168,6 +176,8 @@ typedef struct {
     int64_t n_terms;     /* A' R A assembly terms */
     int64_t bandwidth;   /* max row length of the envelope */
     int64_t device_bytes;
+    int64_t kernel;          /* IMPC_KERNEL_GENERIC or IMPC_KERNEL_STRUCTURED for the next solve */
+    int64_t structured_ok;   /* 1 if the pattern qualifies for the structured kernel */
 } impc_batch_stats;
 int impc_batch_get_stats(impc_batch b, impc_batch_stats *out);
 

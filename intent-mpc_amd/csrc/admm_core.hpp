@@ -658,7 +658,7 @@ IMPC_HD void qp_solve(const DevSym &sy, const DevWork &wk, const DevSettings &st
         for (int32_t i = 0; i < m; i++) {
             double yi = IMPC_AT(wk.y, i);
             if (scaled) {
-                yi = IMPC_AT(wk.Einv, i) * yi;
+                yi = IMPC_AT(wk.E, i) * yi;  // unscale_solution: y = E y / c
                 yi *= cinv;
             }
             IMPC_AT(wk.yo, i) = yi;

@@ -1,25 +1,31 @@
 // impc_qp.hip -- libimpc_qp.so: C-ABI (include/impc_qp.h), device memory management and the
 // gfx950 kernels of the batched OSQP-equivalent solver.
 //
-// Kernels (one QP per lane, batch-interleaved storage, see admm_core.hpp):
-//   k_interleave   QP-major -> interleaved (LDS-tiled transpose), used for inputs
-//   k_setup        osqp_setup numeric part + osqp_warm_start           (admm_core: qp_setup)
-//   k_solve        osqp_solve: ADMM, termination, adaptive rho, unscale (admm_core: qp_solve)
-//   k_deinterleave interleaved -> QP-major, used for outputs
-//   k_update_q / k_update_bounds  osqp_update_lin_cost / osqp_update_bounds
+// Two device paths, both OSQP 0.6.2 ADMM in FP64:
+//   STRUCTURED  k_mpc_wave<VS,GS>: one mpcPlanner QP per 64-lane wavefront, all per-QP state in
+//               VGPRs/LDS, waves pull QPs from a work queue (mpc_wave.hpp).  Used when the
+//               pattern is the stage-structured MPC QP (mpc_structure.hpp).
+//   GENERIC     k_setup + k_solve: any sparsity pattern, one QP per lane, batch-interleaved state
+//               in HBM, sparse LDL^T of the reduced KKT (admm_core.hpp, symbolic.hpp).  Also
+//               backs the persistent update calls.
+// Inputs are kept QP-major on the device (the layout the C-ABI receives them in); the generic
+// path interleaves them (LDS-tiled transpose) at setup.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "../../include/impc_qp.h"
 #include "admm_core.hpp"
+#include "mpc_structure.hpp"
+#include "mpc_wave.hpp"
 #include "symbolic.hpp"
 
-#define IMPC_VERSION "impc_qp 0.1.0 (OSQP 0.6.2 semantics, gfx950)"
+#define IMPC_VERSION "impc_qp 0.2.0 (OSQP 0.6.2 semantics, gfx950)"
 
 namespace {
 
@@ -37,16 +43,18 @@ int fail(int code, const std::string &msg) {
             return fail(IMPC_DEVICE_ERROR, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-constexpr int kBlock = 64;       // one wavefront per workgroup: one QP per lane
-constexpr int kTile = 64;        // transpose tile edge
+constexpr int kBlock = 64;  // generic path: one wavefront per workgroup, one QP per lane
+constexpr int kTile = 64;   // transpose tile edge
+constexpr int kTeam = 128;   // structured path: lanes per QP (two wavefronts)
+constexpr int kWaveVS = 2;  // variable slots per lane (n <= 256)
 
-// dst[e * S + b] = src[b * len + e]  for b < B, e < len.  64x64 tile through LDS so both the
-// global read (along e) and the global write (along b) are coalesced.
+// ------------------------------------------------------------------ layout transposes
+// dst[e * S + b] = src[b * len + e]; 64x64 tile through LDS so both sides are coalesced.
 __global__ __launch_bounds__(256) void k_interleave(const double *__restrict__ src, double *__restrict__ dst,
                                                     int64_t len, int64_t B, int64_t S) {
     __shared__ double tile[kTile][kTile + 1];
     const int64_t e0 = (int64_t)blockIdx.x * kTile, b0 = (int64_t)blockIdx.y * kTile;
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     for (int r = ty; r < kTile; r += 4) {
         int64_t b = b0 + r, e = e0 + tx;
         tile[r][tx] = (b < B && e < len) ? src[b * len + e] : 0.0;
@@ -75,6 +83,7 @@ __global__ __launch_bounds__(256) void k_deinterleave(const double *__restrict__
     }
 }
 
+// ------------------------------------------------------------------ generic path kernels
 __global__ __launch_bounds__(kBlock) void k_setup(impc::DevSym sy, impc::DevWork wk, impc::DevSettings st, int64_t B,
                                                   int has_ws) {
     const int lane = blockIdx.x * kBlock + threadIdx.x;
@@ -149,39 +158,104 @@ __global__ __launch_bounds__(kBlock) void k_update_bounds(impc::DevSym sy, impc:
     impc::refresh_v(sy, wk, lane);
 }
 
-struct DevBuf {
-    void *p = nullptr;
-    ~DevBuf() {
-        if (p) (void)hipFree(p);
+// ---------------------------------------------------------------- structured path kernel
+// Team policy of mpc_wave.hpp on gfx950: one QP per workgroup of NL threads (NL/64 wavefronts);
+// LDS exchange + workgroup barrier, readlane broadcast inside a wavefront, butterfly reductions
+// inside a wavefront combined across wavefronts through LDS in a fixed order (bitwise uniform).
+template <int NL>
+struct GpuTeam {
+    double *red;  // >= NL/64 doubles of LDS
+    __device__ int lane() const { return (int)threadIdx.x; }
+    __device__ void sync() { __syncthreads(); }
+    __device__ double bcast(double v, int src) {
+        int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
+        int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
+        return __hiloint2double(hi, lo);
+    }
+    __device__ double max(double v) {
+        for (int mask = 32; mask >= 1; mask >>= 1) {
+            double o = __shfl_xor(v, mask);
+            v = o > v ? o : v;
+        }
+        if (NL == 64) return v;
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+        __syncthreads();
+        double r = red[0];
+        for (int w = 1; w < NL / 64; w++) r = red[w] > r ? red[w] : r;
+        __syncthreads();
+        return r;
+    }
+    __device__ double sum(double v) {
+        for (int mask = 32; mask >= 1; mask >>= 1) v = v + __shfl_xor(v, mask);
+        v = bcast(v, 0);
+        if (NL == 64) return v;
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+        __syncthreads();
+        double r = red[0];
+        for (int w = 1; w < NL / 64; w++) r = r + red[w];
+        __syncthreads();
+        return r;
     }
 };
+
+template <int NL, int VS, int GS>
+__global__ __launch_bounds__(NL, 1) void k_mpc_wave(impc::WaveTables T, impc::WaveIO io, impc::DevSettings st,
+                                                    unsigned *counter) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    using LD = impc::WaveLds<NL, VS, GS>;
+    GpuTeam<NL> wv{smem + LD::RED_OFF};
+    __shared__ unsigned next;
+    for (;;) {
+        if (threadIdx.x == 0) next = atomicAdd(counter, 1u);
+        __syncthreads();
+        const unsigned b = next;
+        __syncthreads();
+        if ((int64_t)b >= io.B) break;
+        impc::WaveQP<GpuTeam<NL>, NL, VS, GS> qp(wv, T, io, st, smem);
+        qp.solve((int64_t)b);
+    }
+}
 
 }  // namespace
 
 struct impc_ctx_s {
     int device = 0;
+    int num_cu = 256;
     hipStream_t stream = nullptr;
 };
 
 struct impc_batch_s {
     impc_ctx ctx = nullptr;
-    impc::Symbolic sym;
+    int64_t n = 0, m = 0, nnzP = 0, nnzA = 0;
+    std::vector<int64_t> Pp, Pi, Ap, Ai;  // pattern (host copy)
     int64_t B = 0, S = 0;
     impc_settings settings{};
     impc::DevSettings dst{};
-    // device allocations
-    void *d_sym = nullptr;      // all int32 symbolic arrays
-    double *d_work = nullptr;   // all interleaved per-QP arrays
-    double *d_xout = nullptr;   // QP-major results
-    double *d_yout = nullptr;
+    int kernel_req = IMPC_KERNEL_AUTO;
+    // QP-major inputs on the device
+    double *d_in = nullptr;
+    double *in_Px = nullptr, *in_q = nullptr, *in_Ax = nullptr, *in_l = nullptr, *in_u = nullptr, *in_xws = nullptr,
+           *in_yws = nullptr;
+    double *d_xout = nullptr, *d_yout = nullptr;
     impc_info *d_info = nullptr;
-    double *d_stage = nullptr;  // QP-major staging for inputs
-    int64_t stage_len = 0;
     int64_t device_bytes = 0;
+    bool values_set = false, has_ws = false;
+    // ---- structured path
+    std::unique_ptr<impc::MpcStructure> ms;
+    bool structured_ok = false;
+    int gs = 0;
+    void *d_tables = nullptr;
+    double *d_scal = nullptr;
+    unsigned *d_counter = nullptr;
+    impc::WaveTables wt{};
+    // ---- generic path (allocated on first use)
+    std::unique_ptr<impc::Symbolic> sym;
+    void *d_sym = nullptr;
+    double *d_work = nullptr;
     impc::DevSym dsym{};
     impc::DevWork dwk{};
-    bool values_set = false, dirty = true, has_ws = false, setup_done = false;
-    // profiling: events around k_setup, k_solve, output transposes
+    bool generic_dirty = true, generic_setup_done = false;
+    // profiling
     bool profile = false;
     hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     bool ev_setup = false, ev_solve = false;
@@ -227,6 +301,11 @@ int to_dev_settings(const impc_settings *s, impc::DevSettings *d) {
 
 hipStream_t pick(impc_batch b, void *stream) { return stream ? (hipStream_t)stream : b->ctx->stream; }
 
+bool use_structured(impc_batch b) {
+    if (b->kernel_req == IMPC_KERNEL_GENERIC) return false;
+    return b->structured_ok;
+}
+
 int interleave(impc_batch b, const double *src_dev, double *dst, int64_t len, hipStream_t st) {
     if (len <= 0) return IMPC_OK;
     dim3 grid((unsigned)((len + kTile - 1) / kTile), (unsigned)((b->S + kTile - 1) / kTile));
@@ -243,14 +322,216 @@ int deinterleave(impc_batch b, const double *src, double *dst_dev, int64_t len, 
     return IMPC_OK;
 }
 
-// host QP-major array -> staging (H2D) -> interleaved destination
-int upload(impc_batch b, const double *host, double *dst, int64_t len) {
-    if (len <= 0) return IMPC_OK;
-    hipStream_t st = b->ctx->stream;
-    HIP_OK(hipMemcpyAsync(b->d_stage, host, sizeof(double) * (size_t)(len * b->B), hipMemcpyHostToDevice, st));
-    int rc = interleave(b, b->d_stage, dst, len, st);
+// ---- generic path: symbolic analysis + interleaved workspace, allocated on first use
+int ensure_generic(impc_batch b) {
+    if (b->d_work) return IMPC_OK;
+    b->sym.reset(new impc::Symbolic());
+    std::string err = b->sym->build(b->n, b->m, b->Pp.data(), b->Pi.data(), b->Ap.data(), b->Ai.data());
+    if (!err.empty()) return fail(IMPC_DATA_VALIDATION_ERROR, err);
+    const impc::Symbolic &s = *b->sym;
+    std::vector<const std::vector<int32_t> *> arrs = {&s.Pp, &s.Pi, &s.Ap, &s.Ai, &s.Arp, &s.Arpos, &s.Arcol,
+                                                      &s.Arcolf, &s.perm, &s.iperm, &s.Mp, &s.Mi, &s.Mdiag,
+                                                      &s.Pt_dest, &s.Pt_src, &s.At_dest, &s.At_a, &s.At_b,
+                                                      &s.At_r, &s.Lp, &s.Li, &s.Lrp, &s.Lrc, &s.Lrpos,
+                                                      &s.upd_ptr, &s.upd_c, &s.upd_js, &s.upd_je, &s.upd_w};
+    std::vector<size_t> offs;
+    size_t tot = 0;
+    for (auto *a : arrs) {
+        offs.push_back(tot);
+        tot += (a->size() + 63) / 64 * 64;
+    }
+    std::vector<int32_t> hsym(tot + 64, 0);
+    for (size_t k = 0; k < arrs.size(); k++)
+        if (!arrs[k]->empty()) std::memcpy(hsym.data() + offs[k], arrs[k]->data(), arrs[k]->size() * 4);
+    HIP_OK(hipMalloc(&b->d_sym, hsym.size() * 4));
+    HIP_OK(hipMemcpy(b->d_sym, hsym.data(), hsym.size() * 4, hipMemcpyHostToDevice));
+    const int32_t *base = (const int32_t *)b->d_sym;
+    impc::DevSym &d = b->dsym;
+    d.n = s.n;
+    d.m = s.m;
+    d.nnzP = s.nnzP;
+    d.nnzA = s.nnzA;
+    d.nnzM = (int32_t)s.nnzM;
+    d.nnzL = (int32_t)s.nnzL;
+    d.nPt = (int32_t)s.Pt_dest.size();
+    d.nAt = (int32_t)s.At_dest.size();
+    const int32_t **dst_ptrs[] = {&d.Pp, &d.Pi, &d.Ap, &d.Ai, &d.Arp, &d.Arpos, &d.Arcol, &d.Arcolf,
+                                  &d.perm, &d.iperm, &d.Mp, &d.Mi, &d.Mdiag, &d.Pt_dest, &d.Pt_src,
+                                  &d.At_dest, &d.At_a, &d.At_b, &d.At_r, &d.Lp, &d.Li, &d.Lrp, &d.Lrc,
+                                  &d.Lrpos, &d.upd_ptr, &d.upd_c, &d.upd_js, &d.upd_je, &d.upd_w};
+    for (size_t k = 0; k < arrs.size(); k++) *dst_ptrs[k] = base + offs[k];
+
+    const int64_t n_ = s.n, m_ = s.m, nP = s.nnzP, nA = s.nnzA, nM = s.nnzM, nL = s.nnzL;
+    struct Slot {
+        double **dst;
+        int64_t len;
+    };
+    impc::DevWork &w = b->dwk;
+    w.S = b->S;
+    double *Px_, *q_, *Ax_, *l_, *u_, *xws_, *yws_;
+    std::vector<Slot> slots = {
+        {&Px_, nP}, {&q_, n_}, {&Ax_, nA}, {&l_, m_}, {&u_, m_}, {&xws_, n_}, {&yws_, m_},
+        {&w.Ps, nP}, {&w.qs, n_}, {&w.As, nA}, {&w.ls, m_}, {&w.us, m_}, {&w.D, n_}, {&w.Dinv, n_},
+        {&w.E, m_}, {&w.Einv, m_}, {&w.rho, m_}, {&w.rhoinv, m_}, {&w.ctype, m_}, {&w.scal, impc::SC_NSCAL},
+        {&w.x, n_}, {&w.z, m_}, {&w.y, m_}, {&w.v, m_}, {&w.w, n_}, {&w.dx, n_}, {&w.dy, m_},
+        {&w.Mval, nM}, {&w.Lx, nL}, {&w.Dinvf, n_}, {&w.yf, n_}, {&w.tn1, n_}, {&w.tm1, m_},
+        {&w.xo, n_}, {&w.yo, m_}};
+    int64_t per_qp = 0;
+    for (auto &sl : slots) per_qp += std::max<int64_t>(sl.len, 1);
+    const size_t work_bytes = sizeof(double) * (size_t)per_qp * (size_t)b->S;
+    if (hipMalloc((void **)&b->d_work, work_bytes) != hipSuccess) {
+        b->d_work = nullptr;
+        return fail(IMPC_MEM_ALLOC_ERROR, "hipMalloc(generic workspace) failed: batch too large for device memory");
+    }
+    HIP_OK(hipMemset(b->d_work, 0, work_bytes));
+    int64_t off = 0;
+    for (auto &sl : slots) {
+        *sl.dst = b->d_work + off * b->S;
+        off += std::max<int64_t>(sl.len, 1);
+    }
+    w.Px = Px_;
+    w.q = q_;
+    w.Ax = Ax_;
+    w.l = l_;
+    w.u = u_;
+    w.xws = xws_;
+    w.yws = yws_;
+    w.info = b->d_info;
+    b->device_bytes += (int64_t)(work_bytes + hsym.size() * 4);
+    return IMPC_OK;
+}
+
+int generic_setup(impc_batch b, hipStream_t st) {
+    int rc = ensure_generic(b);
     if (rc) return rc;
-    HIP_OK(hipStreamSynchronize(st));  // staging buffer is reused by the next upload
+    impc::DevWork &w = b->dwk;
+    if ((rc = interleave(b, b->in_Px, const_cast<double *>(w.Px), b->nnzP, st))) return rc;
+    if ((rc = interleave(b, b->in_q, const_cast<double *>(w.q), b->n, st))) return rc;
+    if ((rc = interleave(b, b->in_Ax, const_cast<double *>(w.Ax), b->nnzA, st))) return rc;
+    if ((rc = interleave(b, b->in_l, const_cast<double *>(w.l), b->m, st))) return rc;
+    if ((rc = interleave(b, b->in_u, const_cast<double *>(w.u), b->m, st))) return rc;
+    if (b->has_ws) {
+        if ((rc = interleave(b, b->in_xws, const_cast<double *>(w.xws), b->n, st))) return rc;
+        if ((rc = interleave(b, b->in_yws, const_cast<double *>(w.yws), b->m, st))) return rc;
+    }
+    if (b->profile) HIP_OK(hipEventRecord(b->ev[0], st));
+    hipLaunchKernelGGL(k_setup, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk, b->dst, b->B,
+                       b->has_ws ? 1 : 0);
+    HIP_OK(hipGetLastError());
+    if (b->profile) {
+        HIP_OK(hipEventRecord(b->ev[1], st));
+        b->ev_setup = true;
+    }
+    b->generic_dirty = false;
+    b->generic_setup_done = true;
+    return IMPC_OK;
+}
+
+int generic_solve(impc_batch b, hipStream_t st) {
+    if (b->generic_dirty) {
+        int rc = generic_setup(b, st);
+        if (rc) return rc;
+    }
+    if (b->profile) HIP_OK(hipEventRecord(b->ev[2], st));
+    hipLaunchKernelGGL(k_solve, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk, b->dst, b->B);
+    HIP_OK(hipGetLastError());
+    if (b->profile) HIP_OK(hipEventRecord(b->ev[3], st));
+    int rc = deinterleave(b, b->dwk.xo, b->d_xout, b->n, st);
+    if (!rc) rc = deinterleave(b, b->dwk.yo, b->d_yout, b->m, st);
+    if (!rc && b->profile) {
+        HIP_OK(hipEventRecord(b->ev[4], st));
+        b->ev_solve = true;
+    }
+    return rc;
+}
+
+// ---- structured path
+template <int GS>
+int launch_wave(impc_batch b, hipStream_t st, const impc::WaveIO &io) {
+    using LD = impc::WaveLds<kTeam, kWaveVS, GS>;
+    const size_t lds = sizeof(double) * LD::SIZE;
+    static bool attr_set = false;
+    if (!attr_set) {
+        HIP_OK(hipFuncSetAttribute((const void *)k_mpc_wave<kTeam, kWaveVS, GS>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr_set = true;
+    }
+    const int per_cu = std::max<int>(1, std::min<int>(4, (int)((160 * 1024 - 1024) / lds)));
+    const int64_t groups = std::min<int64_t>(b->B, (int64_t)b->ctx->num_cu * per_cu);
+    hipLaunchKernelGGL((k_mpc_wave<kTeam, kWaveVS, GS>), dim3((unsigned)groups), dim3(kTeam), lds, st, b->wt, io,
+                       b->dst, b->d_counter);
+    HIP_OK(hipGetLastError());
+    return IMPC_OK;
+}
+
+int structured_solve(impc_batch b, hipStream_t st) {
+    impc::WaveIO io{b->B,        b->in_Px,  b->in_q,  b->in_Ax,  b->in_l,  b->in_u, b->in_xws, b->in_yws,
+                    b->has_ws ? 1 : 0, b->d_xout, b->d_yout, b->d_scal, b->d_info};
+    HIP_OK(hipMemsetAsync(b->d_counter, 0, 256, st));
+    if (b->profile) HIP_OK(hipEventRecord(b->ev[2], st));
+    int rc;
+    switch (b->gs) {
+        case 2: rc = launch_wave<2>(b, st, io); break;
+        case 3: rc = launch_wave<3>(b, st, io); break;
+        case 4: rc = launch_wave<4>(b, st, io); break;
+        default: return fail(IMPC_UNSUPPORTED, "no structured kernel for this size");
+    }
+    if (rc) return rc;
+    if (b->profile) {
+        HIP_OK(hipEventRecord(b->ev[3], st));
+        HIP_OK(hipEventRecord(b->ev[4], st));
+        b->ev_solve = true;
+        b->ev_setup = false;
+    }
+    return IMPC_OK;
+}
+
+int prepare_structured(impc_batch b) {
+    b->ms.reset(new impc::MpcStructure());
+    std::string why = b->ms->analyse(b->n, b->m, b->Pp.data(), b->Pi.data(), b->Ap.data(), b->Ai.data());
+    if (!why.empty() || b->ms->n > kTeam * kWaveVS) {
+        b->structured_ok = false;
+        return IMPC_OK;
+    }
+    const int mg = b->ms->mg;
+    b->gs = mg <= 2 * kTeam ? 2 : mg <= 3 * kTeam ? 3 : mg <= 4 * kTeam ? 4 : 0;
+    if (!b->gs) {
+        b->structured_ok = false;
+        return IMPC_OK;
+    }
+    const impc::MpcStructure &s = *b->ms;
+    std::vector<const std::vector<int32_t> *> arrs = {&s.var_orig, &s.var_pdiag, &s.var_boxrow, &s.var_boxpos,
+                                                      &s.gen_row,  &s.gen_col,   &s.gen_pos,    &s.colg,
+                                                      &s.term_ptr, &s.term};
+    std::vector<size_t> offs;
+    size_t tot = 0;
+    for (auto *a : arrs) {
+        offs.push_back(tot);
+        tot += (a->size() + 63) / 64 * 64;
+    }
+    std::vector<int32_t> h(tot + 64, 0);
+    for (size_t k = 0; k < arrs.size(); k++)
+        if (!arrs[k]->empty()) std::memcpy(h.data() + offs[k], arrs[k]->data(), arrs[k]->size() * 4);
+    HIP_OK(hipMalloc(&b->d_tables, h.size() * 4));
+    HIP_OK(hipMemcpy(b->d_tables, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    const int32_t *base = (const int32_t *)b->d_tables;
+    impc::WaveTables &t = b->wt;
+    t.n = s.n;
+    t.m = s.m;
+    t.mg = s.mg;
+    t.N = s.N;
+    t.W = s.W;
+    t.CG = s.CG;
+    t.nnzP = s.nnzP;
+    t.nnzA = s.nnzA;
+    const int32_t **dst_ptrs[] = {&t.var_orig, &t.var_pdiag, &t.var_boxrow, &t.var_boxpos, &t.gen_row,
+                                  &t.gen_col,  &t.gen_pos,   &t.colg,       &t.term_ptr,   &t.term};
+    for (size_t k = 0; k < arrs.size(); k++) *dst_ptrs[k] = base + offs[k];
+    const size_t scal_bytes = sizeof(double) * (size_t)b->B * (size_t)(2 * s.n + s.mg);
+    HIP_OK(hipMalloc((void **)&b->d_scal, scal_bytes));
+    HIP_OK(hipMalloc((void **)&b->d_counter, 256));
+    b->device_bytes += (int64_t)(scal_bytes + h.size() * 4 + 256);
+    b->structured_ok = true;
     return IMPC_OK;
 }
 
@@ -298,6 +579,9 @@ int impc_ctx_create(int device, impc_ctx *out) {
     HIP_OK(hipSetDevice(device));
     impc_ctx c = new impc_ctx_s();
     c->device = device;
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+        c->num_cu = ncu;
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
@@ -330,112 +614,55 @@ int impc_batch_create(impc_ctx ctx, int64_t n, int64_t m, const int64_t *Pp, con
     if (!ctx || !out) return fail(IMPC_INVALID_ARGUMENT, "null context or output");
     *out = nullptr;
     if (batch <= 0 || batch > (int64_t)1 << 30) return fail(IMPC_INVALID_ARGUMENT, "batch must be in [1, 2^30]");
+    if (n <= 0 || m < 0 || !Pp || !Ap) return fail(IMPC_DATA_VALIDATION_ERROR, "invalid dimensions or pattern");
+    // validate the pattern once (OSQP validate_data: P upper triangular, indices in range)
+    impc::Symbolic check;
+    std::string err = check.build(n, m, Pp, Pi, Ap, Ai);
+    if (!err.empty()) return fail(IMPC_DATA_VALIDATION_ERROR, err);
     HIP_OK(hipSetDevice(ctx->device));
-    impc_batch b = new impc_batch_s();
+    std::unique_ptr<impc_batch_s> b(new impc_batch_s());
     b->ctx = ctx;
-    std::string err = b->sym.build(n, m, Pp, Pi, Ap, Ai);
-    if (!err.empty()) {
-        delete b;
-        return fail(IMPC_DATA_VALIDATION_ERROR, err);
-    }
-    const impc::Symbolic &s = b->sym;
+    b->n = n;
+    b->m = m;
+    b->nnzP = Pp[n];
+    b->nnzA = Ap[n];
+    b->Pp.assign(Pp, Pp + n + 1);
+    b->Pi.assign(Pi ? Pi : Pp, Pi ? Pi + b->nnzP : Pp);
+    b->Ap.assign(Ap, Ap + n + 1);
+    b->Ai.assign(Ai, Ai + b->nnzA);
     b->B = batch;
     b->S = (batch + kBlock - 1) / kBlock * kBlock;
     impc_default_settings(&b->settings);
     to_dev_settings(&b->settings, &b->dst);
-
-    // ---- symbolic arrays: one int32 allocation
-    std::vector<const std::vector<int32_t> *> arrs = {&s.Pp, &s.Pi, &s.Ap, &s.Ai, &s.Arp, &s.Arpos, &s.Arcol,
-                                                      &s.Arcolf, &s.perm, &s.iperm, &s.Mp, &s.Mi, &s.Mdiag,
-                                                      &s.Pt_dest, &s.Pt_src, &s.At_dest, &s.At_a, &s.At_b,
-                                                      &s.At_r, &s.Lp, &s.Li, &s.Lrp, &s.Lrc, &s.Lrpos,
-                                                      &s.upd_ptr, &s.upd_c, &s.upd_js, &s.upd_je, &s.upd_w};
-    std::vector<size_t> offs;
-    size_t tot = 0;
-    for (auto *a : arrs) {
-        offs.push_back(tot);
-        tot += (a->size() + 63) / 64 * 64;  // 256-B aligned sub-arrays
-    }
-    std::vector<int32_t> hsym(tot + 64, 0);
-    for (size_t k = 0; k < arrs.size(); k++)
-        if (!arrs[k]->empty()) std::memcpy(hsym.data() + offs[k], arrs[k]->data(), arrs[k]->size() * 4);
-    hipError_t he = hipMalloc(&b->d_sym, hsym.size() * 4);
-    if (he != hipSuccess) {
-        delete b;
-        return fail(IMPC_MEM_ALLOC_ERROR, "hipMalloc(symbolic) failed");
-    }
-    he = hipMemcpy(b->d_sym, hsym.data(), hsym.size() * 4, hipMemcpyHostToDevice);
-    if (he != hipSuccess) {
-        impc_batch_destroy(b);
-        return fail(IMPC_DEVICE_ERROR, "hipMemcpy(symbolic) failed");
-    }
-    const int32_t *base = (const int32_t *)b->d_sym;
-    impc::DevSym &d = b->dsym;
-    d.n = s.n;
-    d.m = s.m;
-    d.nnzP = s.nnzP;
-    d.nnzA = s.nnzA;
-    d.nnzM = (int32_t)s.nnzM;
-    d.nnzL = (int32_t)s.nnzL;
-    d.nPt = (int32_t)s.Pt_dest.size();
-    d.nAt = (int32_t)s.At_dest.size();
-    const int32_t **dst_ptrs[] = {&d.Pp, &d.Pi, &d.Ap, &d.Ai, &d.Arp, &d.Arpos, &d.Arcol, &d.Arcolf,
-                                  &d.perm, &d.iperm, &d.Mp, &d.Mi, &d.Mdiag, &d.Pt_dest, &d.Pt_src,
-                                  &d.At_dest, &d.At_a, &d.At_b, &d.At_r, &d.Lp, &d.Li, &d.Lrp, &d.Lrc,
-                                  &d.Lrpos, &d.upd_ptr, &d.upd_c, &d.upd_js, &d.upd_je, &d.upd_w};
-    for (size_t k = 0; k < arrs.size(); k++) *dst_ptrs[k] = base + offs[k];
-
-    // ---- interleaved per-QP arrays: one double allocation, each sub-array len * S doubles
-    const int64_t n_ = s.n, m_ = s.m, nP = s.nnzP, nA = s.nnzA, nM = s.nnzM, nL = s.nnzL;
-    struct Slot {
-        double **dst;
-        int64_t len;
-    };
-    impc::DevWork &w = b->dwk;
-    w.S = b->S;
-    double *Px_, *q_, *Ax_, *l_, *u_, *xws_, *yws_;
-    std::vector<Slot> slots = {
-        {&Px_, nP}, {&q_, n_}, {&Ax_, nA}, {&l_, m_}, {&u_, m_}, {&xws_, n_}, {&yws_, m_},
-        {&w.Ps, nP}, {&w.qs, n_}, {&w.As, nA}, {&w.ls, m_}, {&w.us, m_}, {&w.D, n_}, {&w.Dinv, n_},
-        {&w.E, m_}, {&w.Einv, m_}, {&w.rho, m_}, {&w.rhoinv, m_}, {&w.ctype, m_}, {&w.scal, impc::SC_NSCAL},
-        {&w.x, n_}, {&w.z, m_}, {&w.y, m_}, {&w.v, m_}, {&w.w, n_}, {&w.dx, n_}, {&w.dy, m_},
-        {&w.Mval, nM}, {&w.Lx, nL}, {&w.Dinvf, n_}, {&w.yf, n_}, {&w.tn1, n_}, {&w.tm1, m_},
-        {&w.xo, n_}, {&w.yo, m_}};
-    int64_t per_qp = 0;
-    for (auto &sl : slots) per_qp += std::max<int64_t>(sl.len, 1);
-    const size_t work_bytes = sizeof(double) * (size_t)per_qp * (size_t)b->S;
-    he = hipMalloc((void **)&b->d_work, work_bytes);
-    if (he != hipSuccess) {
-        impc_batch_destroy(b);
-        return fail(IMPC_MEM_ALLOC_ERROR, "hipMalloc(work) failed: batch too large for device memory");
-    }
-    (void)hipMemset(b->d_work, 0, work_bytes);
-    int64_t off = 0;
-    for (auto &sl : slots) {
-        *sl.dst = b->d_work + off * b->S;
-        off += std::max<int64_t>(sl.len, 1);
-    }
-    w.Px = Px_;
-    w.q = q_;
-    w.Ax = Ax_;
-    w.l = l_;
-    w.u = u_;
-    w.xws = xws_;
-    w.yws = yws_;
-    b->stage_len = std::max<int64_t>({nP, nA, n_, m_, 1});
-    he = hipMalloc((void **)&b->d_stage, sizeof(double) * (size_t)(b->stage_len * b->B));
-    if (he == hipSuccess) he = hipMalloc((void **)&b->d_xout, sizeof(double) * (size_t)(std::max<int64_t>(n_, 1) * b->B));
-    if (he == hipSuccess) he = hipMalloc((void **)&b->d_yout, sizeof(double) * (size_t)(std::max<int64_t>(m_, 1) * b->B));
-    if (he == hipSuccess) he = hipMalloc((void **)&b->d_info, sizeof(impc_info) * (size_t)b->B);
-    if (he != hipSuccess) {
-        impc_batch_destroy(b);
-        return fail(IMPC_MEM_ALLOC_ERROR, "hipMalloc(staging/results) failed");
-    }
-    (void)hipMemset(b->d_info, 0, sizeof(impc_info) * (size_t)b->B);
-    w.info = b->d_info;
-    b->device_bytes = (int64_t)(work_bytes + hsym.size() * 4 + sizeof(double) * b->stage_len * b->B +
-                                sizeof(double) * (n_ + m_) * b->B + sizeof(impc_info) * b->B);
-    *out = b;
+    const int64_t B = batch;
+    const int64_t in_len = b->nnzP + b->n + b->nnzA + 2 * b->m + b->n + b->m;
+    const size_t in_bytes = sizeof(double) * (size_t)(in_len * B + 8);
+    if (hipMalloc((void **)&b->d_in, in_bytes) != hipSuccess)
+        return fail(IMPC_MEM_ALLOC_ERROR, "hipMalloc(inputs) failed: batch too large for device memory");
+    double *p = b->d_in;
+    b->in_Px = p;
+    p += b->nnzP * B;
+    b->in_q = p;
+    p += b->n * B;
+    b->in_Ax = p;
+    p += b->nnzA * B;
+    b->in_l = p;
+    p += b->m * B;
+    b->in_u = p;
+    p += b->m * B;
+    b->in_xws = p;
+    p += b->n * B;
+    b->in_yws = p;
+    HIP_OK(hipMemset(b->d_in, 0, in_bytes));
+    if (hipMalloc((void **)&b->d_xout, sizeof(double) * (size_t)(std::max<int64_t>(n, 1) * B)) != hipSuccess ||
+        hipMalloc((void **)&b->d_yout, sizeof(double) * (size_t)(std::max<int64_t>(m, 1) * B)) != hipSuccess ||
+        hipMalloc((void **)&b->d_info, sizeof(impc_info) * (size_t)B) != hipSuccess)
+        return fail(IMPC_MEM_ALLOC_ERROR, "hipMalloc(results) failed");
+    HIP_OK(hipMemset(b->d_info, 0, sizeof(impc_info) * (size_t)B));
+    b->device_bytes = (int64_t)(in_bytes + sizeof(double) * (n + m) * B + sizeof(impc_info) * B);
+    int rc = prepare_structured(b.get());
+    if (rc) return rc;
+    *out = b.release();
     return IMPC_OK;
 }
 
@@ -447,10 +674,21 @@ int impc_batch_destroy(impc_batch b) {
     }
     for (hipEvent_t e : b->ev)
         if (e) (void)hipEventDestroy(e);
-    void *ptrs[] = {b->d_sym, b->d_work, b->d_xout, b->d_yout, b->d_info, b->d_stage};
+    void *ptrs[] = {b->d_in, b->d_xout, b->d_yout, b->d_info, b->d_tables, b->d_scal, b->d_counter, b->d_sym,
+                    b->d_work};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete b;
+    return IMPC_OK;
+}
+
+int impc_batch_set_kernel(impc_batch b, int kernel) {
+    if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
+    if (kernel != IMPC_KERNEL_AUTO && kernel != IMPC_KERNEL_GENERIC && kernel != IMPC_KERNEL_STRUCTURED)
+        return fail(IMPC_INVALID_ARGUMENT, "unknown kernel id");
+    if (kernel == IMPC_KERNEL_STRUCTURED && !b->structured_ok)
+        return fail(IMPC_UNSUPPORTED, "pattern is not a stage-structured MPC QP within the wave kernel's limits");
+    b->kernel_req = kernel;
     return IMPC_OK;
 }
 
@@ -459,9 +697,8 @@ int impc_batch_set_settings(impc_batch b, const impc_settings *s) {
     impc::DevSettings d;
     int rc = to_dev_settings(s, &d);
     if (rc) return rc;
-    // settings that change the setup phase invalidate it (OSQP takes them at osqp_setup)
     if (s->rho != b->settings.rho || s->sigma != b->settings.sigma || s->scaling != b->settings.scaling)
-        b->dirty = true;
+        b->generic_dirty = true;
     b->settings = *s;
     b->dst = d;
     return IMPC_OK;
@@ -470,44 +707,46 @@ int impc_batch_set_settings(impc_batch b, const impc_settings *s) {
 int impc_batch_set_values(impc_batch b, const double *Px, const double *q, const double *Ax, const double *l,
                           const double *u) {
     if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
-    const impc::Symbolic &s = b->sym;
-    if ((s.nnzP && !Px) || !q || (s.nnzA && !Ax) || (s.m && (!l || !u)))
+    if ((b->nnzP && !Px) || !q || (b->nnzA && !Ax) || (b->m && (!l || !u)))
         return fail(IMPC_INVALID_ARGUMENT, "null value array");
-    for (int64_t k = 0; k < (int64_t)s.m * b->B; k++)
+    for (int64_t k = 0; k < b->m * b->B; k++)
         if (l[k] > u[k]) {
             char msg[160];
             std::snprintf(msg, sizeof msg, "lower bound greater than upper bound (QP %lld, row %lld)",
-                          (long long)(k / s.m), (long long)(k % s.m));
+                          (long long)(k / b->m), (long long)(k % b->m));
             return fail(IMPC_DATA_VALIDATION_ERROR, msg);
         }
     HIP_OK(hipSetDevice(b->ctx->device));
-    int rc;
-    if ((rc = upload(b, Px, const_cast<double *>(b->dwk.Px), s.nnzP))) return rc;
-    if ((rc = upload(b, q, const_cast<double *>(b->dwk.q), s.n))) return rc;
-    if ((rc = upload(b, Ax, const_cast<double *>(b->dwk.Ax), s.nnzA))) return rc;
-    if ((rc = upload(b, l, const_cast<double *>(b->dwk.l), s.m))) return rc;
-    if ((rc = upload(b, u, const_cast<double *>(b->dwk.u), s.m))) return rc;
+    const size_t B = (size_t)b->B;
+    if (b->nnzP) HIP_OK(hipMemcpy(b->in_Px, Px, sizeof(double) * b->nnzP * B, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(b->in_q, q, sizeof(double) * b->n * B, hipMemcpyHostToDevice));
+    if (b->nnzA) HIP_OK(hipMemcpy(b->in_Ax, Ax, sizeof(double) * b->nnzA * B, hipMemcpyHostToDevice));
+    if (b->m) {
+        HIP_OK(hipMemcpy(b->in_l, l, sizeof(double) * b->m * B, hipMemcpyHostToDevice));
+        HIP_OK(hipMemcpy(b->in_u, u, sizeof(double) * b->m * B, hipMemcpyHostToDevice));
+    }
     b->values_set = true;
-    b->dirty = true;
+    b->generic_dirty = true;
     return IMPC_OK;
 }
 
 int impc_batch_set_values_device(impc_batch b, const double *Px, const double *q, const double *Ax, const double *l,
                                  const double *u) {
     if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
-    const impc::Symbolic &s = b->sym;
-    if ((s.nnzP && !Px) || !q || (s.nnzA && !Ax) || (s.m && (!l || !u)))
+    if ((b->nnzP && !Px) || !q || (b->nnzA && !Ax) || (b->m && (!l || !u)))
         return fail(IMPC_INVALID_ARGUMENT, "null value array");
     HIP_OK(hipSetDevice(b->ctx->device));
     hipStream_t st = b->ctx->stream;
-    int rc;
-    if ((rc = interleave(b, Px, const_cast<double *>(b->dwk.Px), s.nnzP, st))) return rc;
-    if ((rc = interleave(b, q, const_cast<double *>(b->dwk.q), s.n, st))) return rc;
-    if ((rc = interleave(b, Ax, const_cast<double *>(b->dwk.Ax), s.nnzA, st))) return rc;
-    if ((rc = interleave(b, l, const_cast<double *>(b->dwk.l), s.m, st))) return rc;
-    if ((rc = interleave(b, u, const_cast<double *>(b->dwk.u), s.m, st))) return rc;
+    const size_t B = (size_t)b->B;
+    if (b->nnzP) HIP_OK(hipMemcpyAsync(b->in_Px, Px, sizeof(double) * b->nnzP * B, hipMemcpyDeviceToDevice, st));
+    HIP_OK(hipMemcpyAsync(b->in_q, q, sizeof(double) * b->n * B, hipMemcpyDeviceToDevice, st));
+    if (b->nnzA) HIP_OK(hipMemcpyAsync(b->in_Ax, Ax, sizeof(double) * b->nnzA * B, hipMemcpyDeviceToDevice, st));
+    if (b->m) {
+        HIP_OK(hipMemcpyAsync(b->in_l, l, sizeof(double) * b->m * B, hipMemcpyDeviceToDevice, st));
+        HIP_OK(hipMemcpyAsync(b->in_u, u, sizeof(double) * b->m * B, hipMemcpyDeviceToDevice, st));
+    }
     b->values_set = true;
-    b->dirty = true;
+    b->generic_dirty = true;
     return IMPC_OK;
 }
 
@@ -516,19 +755,19 @@ int impc_batch_warm_start(impc_batch b, const double *x, const double *y) {
     HIP_OK(hipSetDevice(b->ctx->device));
     if (!x) {
         b->has_ws = false;
-        b->dirty = true;
+        b->generic_dirty = true;
         return IMPC_OK;
     }
-    int rc = upload(b, x, const_cast<double *>(b->dwk.xws), b->sym.n);
-    if (rc) return rc;
-    if (y) {
-        rc = upload(b, y, const_cast<double *>(b->dwk.yws), b->sym.m);
-        if (rc) return rc;
-    } else if (b->sym.m) {
-        HIP_OK(hipMemsetAsync(const_cast<double *>(b->dwk.yws), 0, sizeof(double) * b->sym.m * b->S, b->ctx->stream));
+    const size_t B = (size_t)b->B;
+    HIP_OK(hipMemcpy(b->in_xws, x, sizeof(double) * b->n * B, hipMemcpyHostToDevice));
+    if (b->m) {
+        if (y)
+            HIP_OK(hipMemcpy(b->in_yws, y, sizeof(double) * b->m * B, hipMemcpyHostToDevice));
+        else
+            HIP_OK(hipMemset(b->in_yws, 0, sizeof(double) * b->m * B));
     }
     b->has_ws = true;
-    b->dirty = true;
+    b->generic_dirty = true;
     return IMPC_OK;
 }
 
@@ -536,39 +775,17 @@ int impc_batch_setup(impc_batch b, void *stream) {
     if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
     if (!b->values_set) return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "values not set");
     HIP_OK(hipSetDevice(b->ctx->device));
-    hipStream_t st = pick(b, stream);
-    if (b->profile) HIP_OK(hipEventRecord(b->ev[0], st));
-    hipLaunchKernelGGL(k_setup, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk, b->dst, b->B,
-                       b->has_ws ? 1 : 0);
-    HIP_OK(hipGetLastError());
-    if (b->profile) {
-        HIP_OK(hipEventRecord(b->ev[1], st));
-        b->ev_setup = true;
-    }
-    b->dirty = false;
-    b->setup_done = true;
-    return IMPC_OK;
+    if (use_structured(b)) return IMPC_OK;  // the wave kernel runs setup and solve per QP in one launch
+    return generic_setup(b, pick(b, stream));
 }
 
 int impc_batch_solve(impc_batch b, void *stream) {
     if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
-    if (b->dirty) {
-        int rc = impc_batch_setup(b, stream);
-        if (rc) return rc;
-    }
+    if (!b->values_set) return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "values not set");
     HIP_OK(hipSetDevice(b->ctx->device));
     hipStream_t st = pick(b, stream);
-    if (b->profile) HIP_OK(hipEventRecord(b->ev[2], st));
-    hipLaunchKernelGGL(k_solve, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk, b->dst, b->B);
-    HIP_OK(hipGetLastError());
-    if (b->profile) HIP_OK(hipEventRecord(b->ev[3], st));
-    int rc = deinterleave(b, b->dwk.xo, b->d_xout, b->sym.n, st);
-    if (!rc) rc = deinterleave(b, b->dwk.yo, b->d_yout, b->sym.m, st);
-    if (!rc && b->profile) {
-        HIP_OK(hipEventRecord(b->ev[4], st));
-        b->ev_solve = true;
-    }
-    return rc;
+    if (use_structured(b)) return structured_solve(b, st);
+    return generic_solve(b, st);
 }
 
 int impc_batch_get(impc_batch b, double *x, double *y, impc_info *info) {
@@ -576,8 +793,8 @@ int impc_batch_get(impc_batch b, double *x, double *y, impc_info *info) {
     HIP_OK(hipSetDevice(b->ctx->device));
     HIP_OK(hipStreamSynchronize(b->ctx->stream));
     HIP_OK(hipDeviceSynchronize());
-    if (x) HIP_OK(hipMemcpy(x, b->d_xout, sizeof(double) * b->sym.n * b->B, hipMemcpyDeviceToHost));
-    if (y && b->sym.m) HIP_OK(hipMemcpy(y, b->d_yout, sizeof(double) * b->sym.m * b->B, hipMemcpyDeviceToHost));
+    if (x) HIP_OK(hipMemcpy(x, b->d_xout, sizeof(double) * b->n * b->B, hipMemcpyDeviceToHost));
+    if (y && b->m) HIP_OK(hipMemcpy(y, b->d_yout, sizeof(double) * b->m * b->B, hipMemcpyDeviceToHost));
     if (info) HIP_OK(hipMemcpy(info, b->d_info, sizeof(impc_info) * b->B, hipMemcpyDeviceToHost));
     return IMPC_OK;
 }
@@ -590,10 +807,21 @@ int impc_batch_device_results(impc_batch b, double **x, double **y, impc_info **
     return IMPC_OK;
 }
 
+static int upload_interleaved(impc_batch b, const double *host, double *qp_major, double *dst, int64_t len) {
+    HIP_OK(hipMemcpy(qp_major, host, sizeof(double) * len * b->B, hipMemcpyHostToDevice));
+    int rc = interleave(b, qp_major, dst, len, b->ctx->stream);
+    if (rc) return rc;
+    HIP_OK(hipStreamSynchronize(b->ctx->stream));
+    return IMPC_OK;
+}
+
 int impc_batch_update_lin_cost(impc_batch b, const double *q) {
     if (!b || !q) return fail(IMPC_INVALID_ARGUMENT, "null batch or q");
-    if (!b->setup_done || b->dirty) return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "setup has not run on current data");
-    int rc = upload(b, q, const_cast<double *>(b->dwk.q), b->sym.n);
+    if (use_structured(b))
+        return fail(IMPC_UNSUPPORTED, "persistent updates need impc_batch_set_kernel(b, IMPC_KERNEL_GENERIC)");
+    if (!b->generic_setup_done || b->generic_dirty)
+        return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "setup has not run on current data");
+    int rc = upload_interleaved(b, q, b->in_q, const_cast<double *>(b->dwk.q), b->n);
     if (rc) return rc;
     hipLaunchKernelGGL(k_update_q, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, b->ctx->stream, b->dsym, b->dwk,
                        b->dst, b->B);
@@ -602,12 +830,15 @@ int impc_batch_update_lin_cost(impc_batch b, const double *q) {
 }
 
 int impc_batch_update_bounds(impc_batch b, const double *l, const double *u) {
-    if (!b || (b->sym.m && (!l || !u))) return fail(IMPC_INVALID_ARGUMENT, "null batch or bounds");
-    if (!b->setup_done || b->dirty) return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "setup has not run on current data");
-    for (int64_t k = 0; k < (int64_t)b->sym.m * b->B; k++)
+    if (!b || (b->m && (!l || !u))) return fail(IMPC_INVALID_ARGUMENT, "null batch or bounds");
+    if (use_structured(b))
+        return fail(IMPC_UNSUPPORTED, "persistent updates need impc_batch_set_kernel(b, IMPC_KERNEL_GENERIC)");
+    if (!b->generic_setup_done || b->generic_dirty)
+        return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "setup has not run on current data");
+    for (int64_t k = 0; k < b->m * b->B; k++)
         if (l[k] > u[k]) return fail(IMPC_DATA_VALIDATION_ERROR, "lower bound greater than upper bound");
-    int rc = upload(b, l, const_cast<double *>(b->dwk.l), b->sym.m);
-    if (!rc) rc = upload(b, u, const_cast<double *>(b->dwk.u), b->sym.m);
+    int rc = upload_interleaved(b, l, b->in_l, const_cast<double *>(b->dwk.l), b->m);
+    if (!rc) rc = upload_interleaved(b, u, b->in_u, const_cast<double *>(b->dwk.u), b->m);
     if (rc) return rc;
     hipLaunchKernelGGL(k_update_bounds, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, b->ctx->stream, b->dsym,
                        b->dwk, b->dst, b->B);
@@ -617,17 +848,22 @@ int impc_batch_update_bounds(impc_batch b, const double *l, const double *u) {
 
 int impc_batch_get_stats(impc_batch b, impc_batch_stats *out) {
     if (!b || !out) return fail(IMPC_INVALID_ARGUMENT, "null argument");
-    out->n = b->sym.n;
-    out->m = b->sym.m;
-    out->nnzP = b->sym.nnzP;
-    out->nnzA = b->sym.nnzA;
+    std::memset(out, 0, sizeof(*out));
+    out->n = b->n;
+    out->m = b->m;
+    out->nnzP = b->nnzP;
+    out->nnzA = b->nnzA;
     out->batch = b->B;
     out->batch_stride = b->S;
-    out->nnzL = b->sym.nnzL;
-    out->nnzLcol = b->sym.nnzL;
-    out->n_terms = (int64_t)b->sym.At_dest.size();
-    out->bandwidth = b->sym.max_row_L;
+    if (b->sym) {
+        out->nnzL = b->sym->nnzL;
+        out->nnzLcol = b->sym->nnzL;
+        out->n_terms = (int64_t)b->sym->At_dest.size();
+        out->bandwidth = b->sym->max_row_L;
+    }
     out->device_bytes = b->device_bytes;
+    out->kernel = use_structured(b) ? IMPC_KERNEL_STRUCTURED : IMPC_KERNEL_GENERIC;
+    out->structured_ok = b->structured_ok ? 1 : 0;
     return IMPC_OK;
 }
 
@@ -672,7 +908,9 @@ int impc_batch_get_timings(impc_batch b, double *setup_ms, double *solve_ms, dou
 
 int impc_batch_get_perm(impc_batch b, int64_t *perm) {
     if (!b || !perm) return fail(IMPC_INVALID_ARGUMENT, "null argument");
-    for (int32_t k = 0; k < b->sym.n; k++) perm[k] = b->sym.perm[k];
+    int rc = ensure_generic(b);
+    if (rc) return rc;
+    for (int32_t k = 0; k < b->sym->n; k++) perm[k] = b->sym->perm[k];
     return IMPC_OK;
 }
 

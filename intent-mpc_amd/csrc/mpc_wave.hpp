@@ -1,0 +1,994 @@
+// mpc_wave.hpp -- one mpcPlanner QP per NL-lane team (NL = 64 or 128 = 1 or 2 wavefronts),
+// all per-QP state on chip.
+//
+// Why: the ADMM of OSQP 0.6.2 (reference osqp.h:78, osqp_solve) runs hundreds to thousands of
+// iterations per QP; each needs one solve with M = P + sigma I + A' R A plus two SpMVs.  Streaming
+// that state from HBM per iteration (the generic one-QP-per-lane kernel) is latency/bandwidth
+// bound.  Here a wave keeps its QP's factor, A values, iterates and bounds in VGPRs and uses LDS
+// only as an exchange buffer, and the waves of the grid pull QPs from a work queue so QPs that
+// need 4000 iterations do not stall the ones that need 200.
+//
+// Data layout (stage order v' = 13k + r, see mpc_structure.hpp):
+//   var slot s of lane L  <-> v' = NL s + L   (VS slots):  x, q, P_jj, the variable's box row
+//       (A value, z, y, l, u, type), row v'%13 of Ainv_k (13) and an 8-wide coupling row
+//   general-row slot s    <-> g = NL s + L    (GS slots): 4 A values + columns, z, y, l, u, type
+//   LDS: F_k (the 8x8 stage-coupling matrices), exchange vectors r / t / e / x~, products buffer
+//
+// Linear solve (block LDL^T of the stage-tridiagonal M, with Ahat_k the Schur complements):
+//   G_k = Bbar_k Ahat_k^{-1} (8 x 13), F_k = G_k[:, :8]
+//   forward : a_0 = r_0[:8],  a_{k+1} = r_{k+1}[:8] - G_k[:, 8:] r_k[8:] - F_k a_k   (8-dim recursion)
+//   middle  : e_k = Ahat_k^{-1} (a_k, r_k[8:])                                     (parallel)
+//   backward: x_{N-1} = e_{N-1},  x_k = e_k - G_k^T x_{k+1}[:8]                      (8-dim recursion)
+// The 8-dim recursions are the only serial part (2 x (N-1) steps of an 8x8 mat-vec).
+//
+// The kernel body is written against a team policy `WV`: lane() in [0, NL), sync() (team barrier
+// with LDS visibility), bcast(v, j) (v of lane j of the CALLER's wavefront), max()/sum() over the
+// team, so the same code runs on the GPU (policy in impc_qp.hip) and, for tests only, in an
+// NL-thread CPU emulation (tests/native/wave_emu.cpp).  The 8-dim recursions are computed
+// redundantly by every wavefront of the team (lanes i = L & 7), so bcast never crosses waves.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/impc_qp.h"
+#include "admm_core.hpp"
+#include "mpc_structure.hpp"
+
+namespace impc {
+
+#define IMPC_WF __host__ __device__ __forceinline__
+
+struct WaveTables {
+    int32_t n, m, mg, N, W, CG, nnzP, nnzA;
+    const int32_t *var_orig, *var_pdiag, *var_boxrow, *var_boxpos;
+    const int32_t *gen_row, *gen_col, *gen_pos, *colg, *term_ptr, *term;
+};
+
+struct WaveIO {
+    int64_t B;
+    const double *Px, *q, *Ax, *l, *u, *xws, *yws;  // QP-major inputs
+    int32_t has_ws;
+    double *xo, *yo;   // QP-major outputs (unscaled)
+    double *scal;      // per-QP scratch [B][n + n + mg]: D, E(box), E(general)
+    impc_info *info;
+};
+
+// LDS doubles per wave for (VS, GS)
+template <int NL, int VS, int GS>
+struct WaveLds {
+    static constexpr int NMAX = NL * VS;
+    static constexpr int WMAX = (NMAX + 5) / 13 - 1;       // max control stages
+    static constexpr int NP = NMAX + 192;                   // exchange vector length (zero tail)
+    static constexpr int F_OFF = 0;                         // [WMAX][64]
+    static constexpr int R_OFF = F_OFF + WMAX * 64;         // rbuf
+    static constexpr int T_OFF = R_OFF + NP;                // tbuf
+    static constexpr int E_OFF = T_OFF + NP;                // ebuf
+    static constexpr int X_OFF = E_OFF + NP;                // xbuf
+    static constexpr int P_OFF = X_OFF + NP;                // products [4 * NL GS]
+    static constexpr int RED_OFF = P_OFF + 4 * NL * GS;     // team reduction scratch
+    static constexpr int SIZE = RED_OFF + 64;
+    // factorisation aliases (inside R..X region and the products buffer)
+    static constexpr int FA = R_OFF, FL = FA + 169, FI = FL + 169, FB = FI + 169, FG = FB + 104, FE = FG + 104,
+                         RHOG = FE + 64, DIAGX = RHOG + NL * GS;
+    static_assert(DIAGX + NMAX <= P_OFF, "factorisation scratch does not fit");
+};
+
+struct WaveRho {
+    double rho, r_eq, r_ineq, r_loose, i_eq, i_ineq, i_loose;
+    IMPC_WF void set(double r) {
+        rho = r;
+        r_ineq = r;
+        r_eq = kRhoEqOverIneq * r;
+        r_loose = kRhoMin;
+        i_ineq = 1. / r_ineq;
+        i_eq = 1. / r_eq;
+        i_loose = 1. / r_loose;
+    }
+    // Value selection by arithmetic (t in {-1, 0, 1}): a ternary between fields would become a
+    // select of member addresses and keep the whole per-QP object out of registers.
+    IMPC_WF double of(int t) const {
+        double e = t > 0 ? 1.0 : 0.0, i = t == 0 ? 1.0 : 0.0, l = t < 0 ? 1.0 : 0.0;
+        return (e * r_eq + i * r_ineq) + l * r_loose;
+    }
+    IMPC_WF double inv(int t) const {
+        double e = t > 0 ? 1.0 : 0.0, i = t == 0 ? 1.0 : 0.0, l = t < 0 ? 1.0 : 0.0;
+        return (e * i_eq + i * i_ineq) + l * i_loose;
+    }
+};
+
+IMPC_WF int row_type(double l, double u) {  // set_rho_vec (auxil.h:34)
+    if ((l < -kInf * kMinScaling) && (u > kInf * kMinScaling)) return -1;
+    if (u - l < kRhoTol) return 1;
+    return 0;
+}
+
+template <class WV, int NL, int VS, int GS>
+struct WaveQP {
+    using LD = WaveLds<NL, VS, GS>;
+    WV &wv;
+    const WaveTables &T;
+    const WaveIO &io;
+    const DevSettings &st;
+    double *lds;
+    int L;
+    // ---- variable slots
+    double x[VS], q[VS], pd[VS], ab[VS], zb[VS], yb[VS], lb[VS], ub[VS], dxv[VS], dyb[VS];
+    double ainv[VS][13], cp[VS][8];
+    double rhob[VS], rhoib[VS];  // rho and 1/rho of each variable's box row
+    int bt[VS], vs_[VS], vr_[VS];
+    bool vok[VS];
+    // ---- general-row slots
+    double a[GS][4], z[GS], y[GS], lg[GS], ug[GS], dyg[GS], rhog_[GS], rhoig_[GS];
+    int gc[GS][4], gt[GS];
+    bool gok[GS];
+    WaveRho R;
+    double c = 1.0, cinv = 1.0;
+
+    IMPC_WF WaveQP(WV &w, const WaveTables &t, const WaveIO &i, const DevSettings &s, double *l)
+        : wv(w), T(t), io(i), st(s), lds(l), L(w.lane()) {}
+
+    IMPC_WF void set_rho(double r) {
+        R.set(r);
+        _Pragma("unroll") for (int s = 0; s < VS; s++) {
+            rhob[s] = R.of(bt[s]);
+            rhoib[s] = R.inv(bt[s]);
+        }
+        _Pragma("unroll") for (int s = 0; s < GS; s++) {
+            rhog_[s] = R.of(gt[s]);
+            rhoig_[s] = R.inv(gt[s]);
+        }
+    }
+
+    IMPC_WF double *F() { return lds + LD::F_OFF; }
+    IMPC_WF double *rbuf() { return lds + LD::R_OFF; }
+    IMPC_WF double *tbuf() { return lds + LD::T_OFF; }
+    IMPC_WF double *ebuf() { return lds + LD::E_OFF; }
+    IMPC_WF double *xbuf() { return lds + LD::X_OFF; }
+    IMPC_WF double *pbuf() { return lds + LD::P_OFF; }
+
+    // zero the exchange vectors (their tails are the zero slots read by padded entries)
+    IMPC_WF void clear_exchange() {
+        for (int i = L; i < 4 * LD::NP; i += NL) lds[LD::R_OFF + i] = 0.0;
+        wv.sync();
+    }
+
+    // ------------------------------------------------------------------ load + scaling
+    IMPC_WF void load(int64_t b) {
+        const int n = T.n, m = T.m;
+        const int64_t bn = b * n, bm = b * m, bP = b * T.nnzP, bA = b * T.nnzA;
+        _Pragma("unroll") for (int s = 0; s < VS; s++) {
+            int v = NL * s + L;
+            vok[s] = v < n;
+            vs_[s] = vok[s] ? v / 13 : 0;
+            vr_[s] = vok[s] ? v % 13 : 0;
+            x[s] = q[s] = pd[s] = ab[s] = zb[s] = yb[s] = lb[s] = ub[s] = dxv[s] = dyb[s] = 0.0;
+            bt[s] = 0;
+            if (vok[s]) {
+                int ov = T.var_orig[v];
+                q[s] = io.q[bn + ov];
+                int pp = T.var_pdiag[v];
+                pd[s] = pp >= 0 ? io.Px[bP + pp] : 0.0;
+                ab[s] = io.Ax[bA + T.var_boxpos[v]];
+                int br = T.var_boxrow[v];
+                lb[s] = dmin(dmax(io.l[bm + br], -kInf), kInf);
+                ub[s] = dmin(dmax(io.u[bm + br], -kInf), kInf);
+            }
+        }
+        _Pragma("unroll") for (int s = 0; s < GS; s++) {
+            int g = NL * s + L;
+            gok[s] = g < T.mg;
+            z[s] = y[s] = lg[s] = ug[s] = dyg[s] = 0.0;
+            gt[s] = 0;
+            _Pragma("unroll") for (int e = 0; e < 4; e++) {
+                a[s][e] = 0.0;
+                gc[s][e] = LD::NMAX;  // zero slot
+            }
+            if (gok[s]) {
+                _Pragma("unroll") for (int e = 0; e < 4; e++) {
+                    int col = T.gen_col[4 * g + e], pos = T.gen_pos[4 * g + e];
+                    if (col >= 0) {
+                        gc[s][e] = col;
+                        a[s][e] = io.Ax[bA + pos];
+                    }
+                }
+                int row = T.gen_row[g];
+                lg[s] = dmin(dmax(io.l[bm + row], -kInf), kInf);
+                ug[s] = dmin(dmax(io.u[bm + row], -kInf), kInf);
+            }
+        }
+    }
+
+    // gather sum over the general entries of this variable's column from the products buffer
+    IMPC_WF double col_gather(int v) {
+        double s = 0.0;
+        const int32_t *cl = T.colg + (int64_t)v * T.CG;
+        const double *pb = pbuf();
+        for (int t = 0; t < T.CG; t++) {
+            int idx = cl[t];
+            if (idx >= 0) s += pb[idx];
+        }
+        return s;
+    }
+    IMPC_WF double col_gather_max(int v) {
+        double s = 0.0;
+        const int32_t *cl = T.colg + (int64_t)v * T.CG;
+        const double *pb = pbuf();
+        for (int t = 0; t < T.CG; t++) {
+            int idx = cl[t];
+            if (idx >= 0) s = dmax(pb[idx], s);
+        }
+        return s;
+    }
+
+    // scale_data (scaling.h:21): Ruiz equilibration + cost scaling; D, E kept in registers here,
+    // written to the per-QP scratch at the end.
+    IMPC_WF void scale(int64_t b, double D[VS], double Eb[VS], double Eg[GS]) {
+        const int n = T.n;
+        _Pragma("unroll") for (int s = 0; s < VS; s++) D[s] = Eb[s] = 1.0;
+        _Pragma("unroll") for (int s = 0; s < GS; s++) Eg[s] = 1.0;
+        c = 1.0;
+        double *pb = pbuf(), *xb = xbuf();
+        for (int it = 0; it < st.scaling; it++) {
+            // |A| entries of general rows -> products buffer
+            _Pragma("unroll") for (int s = 0; s < GS; s++) {
+                int g = NL * s + L;
+                if (gok[s])
+                    _Pragma("unroll") for (int e = 0; e < 4; e++) pb[4 * g + e] = fabs(a[s][e]);
+            }
+            wv.sync();
+            double Dt[VS], Etb[VS], Etg[GS];
+            _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                // colnorm_sym(P) (diagonal), max with colnorm(A) = max(box, general entries)
+                double d = fabs(pd[s]);
+                double an = dmax(fabs(ab[s]), 0.0);
+                if (vok[s]) an = dmax(col_gather_max(NL * s + L), an);
+                d = dmax(d, an);
+                d = d < kMinScaling ? 1.0 : d;
+                d = d > kMaxScaling ? kMaxScaling : d;
+                Dt[s] = 1.0 / sqrt(d);
+                double e = fabs(ab[s]);
+                e = e < kMinScaling ? 1.0 : e;
+                e = e > kMaxScaling ? kMaxScaling : e;
+                Etb[s] = 1.0 / sqrt(e);
+            }
+            _Pragma("unroll") for (int s = 0; s < GS; s++) {
+                double e = 0.0;
+                _Pragma("unroll") for (int k = 0; k < 4; k++) e = dmax(fabs(a[s][k]), e);
+                e = e < kMinScaling ? 1.0 : e;
+                e = e > kMaxScaling ? kMaxScaling : e;
+                Etg[s] = 1.0 / sqrt(e);
+            }
+            // D_temp of every column to LDS for the general rows
+            _Pragma("unroll") for (int s = 0; s < VS; s++)
+                if (vok[s]) xb[NL * s + L] = Dt[s];
+            wv.sync();
+            _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                pd[s] = (pd[s] * Dt[s]) * Dt[s];
+                ab[s] = (ab[s] * Etb[s]) * Dt[s];
+                q[s] = Dt[s] * q[s];
+                D[s] = D[s] * Dt[s];
+                Eb[s] = Eb[s] * Etb[s];
+            }
+            _Pragma("unroll") for (int s = 0; s < GS; s++) {
+                _Pragma("unroll") for (int e = 0; e < 4; e++) a[s][e] = (a[s][e] * Etg[s]) * xb[gc[s][e]];
+                Eg[s] = Eg[s] * Etg[s];
+            }
+            // cost normalisation
+            double psum = 0.0, qn = 0.0;
+            _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                if (vok[s]) {
+                    psum += fabs(pd[s]);
+                    qn = dmax(fabs(q[s]), qn);
+                }
+            }
+            double ct = wv.sum(psum) / (double)n;
+            qn = wv.max(qn);
+            qn = qn < kMinScaling ? 1.0 : qn;
+            qn = qn > kMaxScaling ? kMaxScaling : qn;
+            ct = dmax(ct, qn);
+            ct = ct < kMinScaling ? 1.0 : ct;
+            ct = ct > kMaxScaling ? kMaxScaling : ct;
+            ct = 1. / ct;
+            _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                pd[s] *= ct;
+                q[s] *= ct;
+            }
+            c *= ct;
+            wv.sync();
+        }
+        cinv = 1. / c;
+        _Pragma("unroll") for (int s = 0; s < VS; s++) {
+            lb[s] = Eb[s] * lb[s];
+            ub[s] = Eb[s] * ub[s];
+            bt[s] = row_type(lb[s], ub[s]);
+        }
+        _Pragma("unroll") for (int s = 0; s < GS; s++) {
+            lg[s] = Eg[s] * lg[s];
+            ug[s] = Eg[s] * ug[s];
+            gt[s] = row_type(lg[s], ug[s]);
+        }
+        double *sc = io.scal + b * (int64_t)(2 * T.n + T.mg);
+        _Pragma("unroll") for (int s = 0; s < VS; s++)
+            if (vok[s]) {
+                sc[NL * s + L] = D[s];
+                sc[T.n + NL * s + L] = Eb[s];
+            }
+        _Pragma("unroll") for (int s = 0; s < GS; s++)
+            if (gok[s]) sc[2 * T.n + NL * s + L] = Eg[s];
+    }
+
+    // ------------------------------------------------------------ block factorisation
+    // Returns 1 if a pivot is not positive (OSQP_NONCVX_ERROR).
+    IMPC_WF int factorize() {
+        const int n = T.n, N = T.N, W = T.W;
+        double *w = pbuf(), *rhog = lds + LD::RHOG, *diagx = lds + LD::DIAGX;
+        double *A = lds + LD::FA, *Li = lds + LD::FL, *Ai = lds + LD::FI, *Bb = lds + LD::FB, *G = lds + LD::FG,
+               *E = lds + LD::FE, *Fm = F();
+        _Pragma("unroll") for (int s = 0; s < GS; s++) {
+            int g = NL * s + L;
+            if (gok[s]) {
+                _Pragma("unroll") for (int e = 0; e < 4; e++) w[4 * g + e] = a[s][e];
+                rhog[g] = rhog_[s];
+            }
+        }
+        _Pragma("unroll") for (int s = 0; s < VS; s++) {
+            if (vok[s]) {
+                double rb = rhob[s];
+                diagx[NL * s + L] = (pd[s] + st.sigma) + rb * ab[s] * ab[s];
+            }
+        }
+        wv.sync();
+        int bad = 0;
+        for (int k = 0; k < N; k++) {
+            const int sz = k < W ? 13 : 8;
+            // assemble M_kk and Bbar_k
+            for (int d = L; d < kStageDests; d += NL) {
+                const bool isB = d >= 169;
+                if (isB && k == W) continue;
+                const int dd = isB ? d - 169 : d;
+                const int r = dd / 13, cc = dd % 13;
+                double val = 0.0;
+                if (isB || (r < sz && cc < sz)) {
+                    const int32_t t0 = T.term_ptr[(int64_t)k * kStageDests + d];
+                    const int32_t t1 = T.term_ptr[(int64_t)k * kStageDests + d + 1];
+                    for (int32_t t = t0; t < t1; t++) {
+                        int32_t code = T.term[t];
+                        int32_t g = code >> 4, e = (code >> 2) & 3, f = code & 3;
+                        val += rhog[g] * w[4 * g + e] * w[4 * g + f];
+                    }
+                    if (!isB && r == cc) val += diagx[13 * k + r];
+                }
+                if (isB)
+                    Bb[dd] = val;
+                else
+                    A[dd] = val;
+            }
+            wv.sync();
+            if (k > 0) {
+                if (L < 64) {
+                    int i = L >> 3, j = L & 7;
+                    A[13 * i + j] -= E[8 * i + j];
+                }
+                wv.sync();
+            }
+            // Cholesky of A (sz x sz, stride 13)
+            for (int j = 0; j < sz; j++) {
+                if (L == 0) {
+                    double dj = A[13 * j + j];
+                    if (!(dj > 0.0)) bad = 1;
+                    A[13 * j + j] = sqrt(dj);
+                }
+                wv.sync();
+                if (L > j && L < sz) A[13 * L + j] /= A[13 * j + j];
+                wv.sync();
+                const int rem = sz - 1 - j, cnt = rem * (rem + 1) / 2;
+                for (int p = L; p < cnt; p += NL) {
+                    // p -> (i, cc) with j < cc <= i < sz, row-major over i
+                    int i = j + 1, off = p;
+                    while (off >= i - j) {
+                        off -= i - j;
+                        i++;
+                    }
+                    int cc = j + 1 + off;
+                    A[13 * i + cc] -= A[13 * i + j] * A[13 * cc + j];
+                }
+                wv.sync();
+            }
+            // Linv column by column (lane = column)
+            if (L < sz) {
+                const int cc = L;
+                Li[13 * cc + cc] = 1.0 / A[13 * cc + cc];
+                for (int i = cc + 1; i < sz; i++) {
+                    double s = 0.0;
+                    for (int t = cc; t < i; t++) s += A[13 * i + t] * Li[13 * t + cc];
+                    Li[13 * i + cc] = -s / A[13 * i + i];
+                }
+            }
+            wv.sync();
+            // Ainv = Linv' Linv
+            for (int p = L; p < sz * sz; p += NL) {
+                int r = p / sz, cc = p % sz;
+                int t0 = r > cc ? r : cc;
+                double s = 0.0;
+                for (int t = t0; t < sz; t++) s += Li[13 * t + r] * Li[13 * t + cc];
+                Ai[13 * r + cc] = s;
+            }
+            wv.sync();
+            _Pragma("unroll") for (int s = 0; s < VS; s++)
+                if (vok[s] && vs_[s] == k)
+                    _Pragma("unroll") for (int cc = 0; cc < 13; cc++) ainv[s][cc] = cc < sz ? Ai[13 * vr_[s] + cc] : 0.0;
+            if (k < W) {
+                for (int p = L; p < 104; p += NL) {
+                    int i = p / 13, cc = p % 13;
+                    double s = 0.0;
+                    for (int t = 0; t < 13; t++) s += Bb[13 * i + t] * Ai[13 * t + cc];
+                    G[p] = s;
+                }
+                wv.sync();
+                if (L < 64) {
+                    int i = L >> 3, j = L & 7;
+                    double s = 0.0;
+                    for (int t = 0; t < 13; t++) s += G[13 * i + t] * Bb[13 * j + t];
+                    E[8 * i + j] = s;
+                    Fm[64 * k + 8 * i + j] = G[13 * i + j];
+                }
+                _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                    if (!vok[s]) continue;
+                    if (vs_[s] == k && vr_[s] >= 8)
+                        _Pragma("unroll") for (int j = 0; j < 8; j++) cp[s][j] = G[13 * j + vr_[s]];
+                    if (vs_[s] == k + 1 && vr_[s] < 8)
+                        _Pragma("unroll") for (int j = 0; j < 8; j++) cp[s][j] = j < 5 ? G[13 * vr_[s] + 8 + j] : 0.0;
+                }
+                wv.sync();
+            }
+        }
+        _Pragma("unroll") for (int s = 0; s < VS; s++)
+            if (vok[s] && vs_[s] == 0 && vr_[s] < 8)
+                _Pragma("unroll") for (int j = 0; j < 8; j++) cp[s][j] = 0.0;
+        bad = (int)wv.bcast((double)bad, 0);
+        clear_exchange();
+        (void)n;
+        return bad;
+    }
+
+    // v = rho z - y products of the general rows for the next rhs
+    IMPC_WF void write_v_products() {
+        double *pb = pbuf();
+        _Pragma("unroll") for (int s = 0; s < GS; s++) {
+            int g = NL * s + L;
+            if (gok[s]) {
+                double vv = rhog_[s] * z[s] - y[s];
+                _Pragma("unroll") for (int e = 0; e < 4; e++) pb[4 * g + e] = a[s][e] * vv;
+            }
+        }
+        wv.sync();
+    }
+
+    // --------------------------------------------------------------- one ADMM iteration
+    IMPC_WF void iterate(bool need_delta) {
+        const int n = T.n, W = T.W;
+        double *rb = rbuf(), *tb = tbuf(), *eb = ebuf(), *xb = xbuf(), *Fm = F();
+        const double sigma = st.sigma, alpha = st.alpha, oma = (double)1.0 - st.alpha;
+        // rhs = sigma x - q + A' v   (stage order)
+        _Pragma("unroll") for (int s = 0; s < VS; s++) {
+            if (!vok[s]) continue;
+            int v = NL * s + L;
+            double vb = rhob[s] * zb[s] - yb[s];
+            double r = sigma * x[s] - q[s];
+            r += ab[s] * vb;
+            r += col_gather(v);
+            rb[v] = r;
+        }
+        wv.sync();
+        // S1: t_k = r_k[:8] - G_{k-1}[:, 8:] r_{k-1}[8:]
+        _Pragma("unroll") for (int s = 0; s < VS; s++) {
+            if (!vok[s] || vr_[s] >= 8) continue;
+            int v = NL * s + L;
+            double t = rb[v];
+            if (vs_[s] > 0) {
+                const double *rp = rb + 13 * (vs_[s] - 1) + 8;
+                _Pragma("unroll") for (int cc = 0; cc < 5; cc++) t -= cp[s][cc] * rp[cc];
+            }
+            tb[v] = t;
+        }
+        wv.sync();
+        // S2: forward 8-dim recursion (lanes 0..7; the others mirror lane L & 7)
+        {
+            const int i = L & 7;
+            double ai = tb[i];
+            if (L < 8) rb[i] = ai;
+            for (int k = 0; k < W; k++) {
+                double s = tb[13 * (k + 1) + i];
+                const double *Fk = Fm + 64 * k + 8 * i;
+                _Pragma("unroll") for (int j = 0; j < 8; j++) s -= Fk[j] * wv.bcast(ai, j);
+                ai = s;
+                if (L < 8) rb[13 * (k + 1) + i] = s;
+            }
+        }
+        wv.sync();
+        // S3: e_k = Ahat_k^{-1} rhat_k
+        _Pragma("unroll") for (int s = 0; s < VS; s++) {
+            if (!vok[s]) continue;
+            const double *rk = rb + 13 * vs_[s];
+            double e = 0.0;
+            _Pragma("unroll") for (int cc = 0; cc < 13; cc++) e += ainv[s][cc] * rk[cc];
+            eb[NL * s + L] = e;
+        }
+        wv.sync();
+        // S4: backward 8-dim recursion x_k[:8] = e_k[:8] - F_k' x_{k+1}[:8]
+        {
+            const int i = L & 7;
+            double xi = eb[13 * W + i];
+            if (L < 8) xb[13 * W + i] = xi;
+            for (int k = W - 1; k >= 0; k--) {
+                double s = eb[13 * k + i];
+                const double *Fk = Fm + 64 * k + i;
+                _Pragma("unroll") for (int j = 0; j < 8; j++) s -= Fk[8 * j] * wv.bcast(xi, j);
+                xi = s;
+                if (L < 8) xb[13 * k + i] = s;
+            }
+        }
+        wv.sync();
+        // S5: controls x_k[8:] = e_k[8:] - G_k[:, 8:]' x_{k+1}[:8]
+        _Pragma("unroll") for (int s = 0; s < VS; s++) {
+            if (!vok[s] || vr_[s] < 8) continue;
+            const double *xn = xb + 13 * (vs_[s] + 1);
+            double t = eb[NL * s + L];
+            _Pragma("unroll") for (int j = 0; j < 8; j++) t -= cp[s][j] * xn[j];
+            xb[NL * s + L] = t;
+        }
+        wv.sync();
+        // update_x and the box rows (update_z / project / update_y)
+        _Pragma("unroll") for (int s = 0; s < VS; s++) {
+            if (!vok[s]) continue;
+            double xt = xb[NL * s + L];
+            double xn = alpha * xt + oma * x[s];
+            if (need_delta) dxv[s] = xn - x[s];
+            x[s] = xn;
+            double zt = ab[s] * xt;
+            double zr = alpha * zt + oma * zb[s];
+            double zn = dmin(dmax(zr + rhoib[s] * yb[s], lb[s]), ub[s]);
+            double dy = rhob[s] * (zr - zn);
+            yb[s] += dy;
+            if (need_delta) dyb[s] = dy;
+            zb[s] = zn;
+        }
+        // general rows
+        _Pragma("unroll") for (int s = 0; s < GS; s++) {
+            if (!gok[s]) continue;
+            double zt = 0.0;
+            _Pragma("unroll") for (int e = 0; e < 4; e++) zt += a[s][e] * xb[gc[s][e]];
+            double zr = alpha * zt + oma * z[s];
+            double zn = dmin(dmax(zr + rhoig_[s] * y[s], lg[s]), ug[s]);
+            double dy = rhog_[s] * (zr - zn);
+            y[s] += dy;
+            if (need_delta) dyg[s] = dy;
+            z[s] = zn;
+        }
+        wv.sync();
+        write_v_products();
+        (void)n;
+    }
+
+    // ------------------------------------------------------------ update_info + checks
+    struct Info {
+        double pri_res, dua_res, pri_norm_u, dua_norm_u, pri_norm_s, dua_norm_s, pri_plain, dua_plain;
+    };
+
+    IMPC_WF void load_scal(int64_t b, double D[VS], double Eb[VS], double Eg[GS]) {
+        const double *sc = io.scal + b * (int64_t)(2 * T.n + T.mg);
+        _Pragma("unroll") for (int s = 0; s < VS; s++) {
+            D[s] = vok[s] ? sc[NL * s + L] : 1.0;
+            Eb[s] = vok[s] ? sc[T.n + NL * s + L] : 1.0;
+        }
+        _Pragma("unroll") for (int s = 0; s < GS; s++) Eg[s] = gok[s] ? sc[2 * T.n + NL * s + L] : 1.0;
+    }
+
+    IMPC_WF void update_info(Info &inf, const double D[VS], const double Eb[VS], const double Eg[GS]) {
+        const bool unsc = st.scaling > 0 && !st.scaled_termination;
+        double *xb = xbuf(), *pb = pbuf();
+        _Pragma("unroll") for (int s = 0; s < VS; s++)
+            if (vok[s]) xb[NL * s + L] = x[s];
+        // A'y products of the general rows
+        _Pragma("unroll") for (int s = 0; s < GS; s++) {
+            int g = NL * s + L;
+            if (gok[s])
+                _Pragma("unroll") for (int e = 0; e < 4; e++) pb[4 * g + e] = a[s][e] * y[s];
+        }
+        wv.sync();
+        double pr_u = 0, z_u = 0, ax_u = 0, pr_p = 0, z_p = 0, ax_p = 0;
+        _Pragma("unroll") for (int s = 0; s < VS; s++) {
+            if (!vok[s]) continue;
+            double ax = ab[s] * x[s], r = ax + -1 * zb[s], ei = 1. / Eb[s];
+            pr_p = dmax(pr_p, fabs(r));
+            z_p = dmax(z_p, fabs(zb[s]));
+            ax_p = dmax(ax_p, fabs(ax));
+            pr_u = dmax(pr_u, fabs(ei * r));
+            z_u = dmax(z_u, fabs(ei * zb[s]));
+            ax_u = dmax(ax_u, fabs(ei * ax));
+        }
+        _Pragma("unroll") for (int s = 0; s < GS; s++) {
+            if (!gok[s]) continue;
+            double ax = 0.0;
+            _Pragma("unroll") for (int e = 0; e < 4; e++) ax += a[s][e] * xb[gc[s][e]];
+            double r = ax + -1 * z[s], ei = 1. / Eg[s];
+            pr_p = dmax(pr_p, fabs(r));
+            z_p = dmax(z_p, fabs(z[s]));
+            ax_p = dmax(ax_p, fabs(ax));
+            pr_u = dmax(pr_u, fabs(ei * r));
+            z_u = dmax(z_u, fabs(ei * z[s]));
+            ax_u = dmax(ax_u, fabs(ei * ax));
+        }
+        double dr_u = 0, q_u = 0, aty_u = 0, px_u = 0, dr_p = 0, q_p = 0, aty_p = 0, px_p = 0;
+        _Pragma("unroll") for (int s = 0; s < VS; s++) {
+            if (!vok[s]) continue;
+            double aty = ab[s] * yb[s] + col_gather(NL * s + L);
+            double px = pd[s] * x[s];
+            double r = q[s] + 1 * px;
+            r = r + 1 * aty;
+            double di = 1. / D[s];
+            dr_p = dmax(dr_p, fabs(r));
+            q_p = dmax(q_p, fabs(q[s]));
+            aty_p = dmax(aty_p, fabs(aty));
+            px_p = dmax(px_p, fabs(px));
+            dr_u = dmax(dr_u, fabs(di * r));
+            q_u = dmax(q_u, fabs(di * q[s]));
+            aty_u = dmax(aty_u, fabs(di * aty));
+            px_u = dmax(px_u, fabs(di * px));
+        }
+        pr_u = wv.max(pr_u);
+        z_u = wv.max(z_u);
+        ax_u = wv.max(ax_u);
+        pr_p = wv.max(pr_p);
+        z_p = wv.max(z_p);
+        ax_p = wv.max(ax_p);
+        dr_u = wv.max(dr_u);
+        q_u = wv.max(q_u);
+        aty_u = wv.max(aty_u);
+        px_u = wv.max(px_u);
+        dr_p = wv.max(dr_p);
+        q_p = wv.max(q_p);
+        aty_p = wv.max(aty_p);
+        px_p = wv.max(px_p);
+        inf.pri_plain = pr_p;
+        inf.dua_plain = dr_p;
+        inf.pri_norm_s = dmax(z_p, ax_p);
+        inf.dua_norm_s = dmax(dmax(q_p, aty_p), px_p);
+        if (unsc) {
+            inf.pri_res = T.m == 0 ? 0.0 : pr_u;
+            inf.dua_res = cinv * dr_u;
+            inf.pri_norm_u = dmax(z_u, ax_u);
+            inf.dua_norm_u = dmax(dmax(q_u, aty_u), px_u) * cinv;
+        } else {
+            inf.pri_res = T.m == 0 ? 0.0 : pr_p;
+            inf.dua_res = dr_p;
+            inf.pri_norm_u = inf.pri_norm_s;
+            inf.dua_norm_u = inf.dua_norm_s;
+        }
+        wv.sync();
+    }
+
+    // is_primal_infeasible (projects dy in place)
+    IMPC_WF int primal_infeasible(double eps, const double D[VS], const double Eb[VS], const double Eg[GS]) {
+        const bool unsc = st.scaling > 0 && !st.scaled_termination;
+        double nrm = 0.0, lhs = 0.0;
+        _Pragma("unroll") for (int s = 0; s < VS; s++) {
+            if (!vok[s]) continue;
+            double d = dyb[s];
+            if (ub[s] > kInf * kMinScaling)
+                d = (lb[s] < -kInf * kMinScaling) ? 0.0 : dmin(d, 0.0);
+            else if (lb[s] < -kInf * kMinScaling)
+                d = dmax(d, 0.0);
+            dyb[s] = d;
+            nrm = dmax(nrm, fabs(unsc ? Eb[s] * d : d));
+            lhs += ub[s] * dmax(d, 0) + lb[s] * dmin(d, 0);
+        }
+        _Pragma("unroll") for (int s = 0; s < GS; s++) {
+            if (!gok[s]) continue;
+            double d = dyg[s];
+            if (ug[s] > kInf * kMinScaling)
+                d = (lg[s] < -kInf * kMinScaling) ? 0.0 : dmin(d, 0.0);
+            else if (lg[s] < -kInf * kMinScaling)
+                d = dmax(d, 0.0);
+            dyg[s] = d;
+            nrm = dmax(nrm, fabs(unsc ? Eg[s] * d : d));
+            lhs += ug[s] * dmax(d, 0) + lg[s] * dmin(d, 0);
+        }
+        nrm = wv.max(nrm);
+        lhs = wv.sum(lhs);
+        int res = 0;
+        if (nrm > kDivTol && lhs < eps * nrm) {
+            double *pb = pbuf();
+            _Pragma("unroll") for (int s = 0; s < GS; s++) {
+                int g = NL * s + L;
+                if (gok[s])
+                    _Pragma("unroll") for (int e = 0; e < 4; e++) pb[4 * g + e] = a[s][e] * dyg[s];
+            }
+            wv.sync();
+            double mx = 0.0;
+            _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                if (!vok[s]) continue;
+                double t = ab[s] * dyb[s] + col_gather(NL * s + L);
+                if (unsc) t = (1. / D[s]) * t;
+                mx = dmax(mx, fabs(t));
+            }
+            mx = wv.max(mx);
+            res = mx < eps * nrm;
+            wv.sync();
+        }
+        return res;
+    }
+
+    // is_dual_infeasible
+    IMPC_WF int dual_infeasible(double eps, const double D[VS], const double Eb[VS], const double Eg[GS]) {
+        const bool unsc = st.scaling > 0 && !st.scaled_termination;
+        double nrm = 0.0, qdx = 0.0, cs = unsc ? c : 1.0;
+        _Pragma("unroll") for (int s = 0; s < VS; s++) {
+            if (!vok[s]) continue;
+            nrm = dmax(nrm, fabs(unsc ? D[s] * dxv[s] : dxv[s]));
+            qdx += q[s] * dxv[s];
+        }
+        nrm = wv.max(nrm);
+        qdx = wv.sum(qdx);
+        int res = 0;
+        if (nrm > kDivTol && qdx < cs * eps * nrm) {
+            double mx = 0.0;
+            _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                if (!vok[s]) continue;
+                double pv = pd[s] * dxv[s];
+                if (unsc) pv = (1. / D[s]) * pv;
+                mx = dmax(mx, fabs(pv));
+            }
+            mx = wv.max(mx);
+            if (mx < cs * eps * nrm) {
+                double *xb = xbuf();
+                _Pragma("unroll") for (int s = 0; s < VS; s++)
+                    if (vok[s]) xb[NL * s + L] = dxv[s];
+                wv.sync();
+                double viol = 0.0;
+                _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                    if (!vok[s]) continue;
+                    double t = ab[s] * dxv[s];
+                    if (unsc) t = (1. / Eb[s]) * t;
+                    if ((ub[s] < kInf * kMinScaling && t > eps * nrm) || (lb[s] > -kInf * kMinScaling && t < -eps * nrm))
+                        viol = 1.0;
+                }
+                _Pragma("unroll") for (int s = 0; s < GS; s++) {
+                    if (!gok[s]) continue;
+                    double t = 0.0;
+                    _Pragma("unroll") for (int e = 0; e < 4; e++) t += a[s][e] * xb[gc[s][e]];
+                    if (unsc) t = (1. / Eg[s]) * t;
+                    if ((ug[s] < kInf * kMinScaling && t > eps * nrm) || (lg[s] > -kInf * kMinScaling && t < -eps * nrm))
+                        viol = 1.0;
+                }
+                viol = wv.max(viol);
+                res = viol == 0.0;
+                wv.sync();
+            }
+        }
+        return res;
+    }
+
+    IMPC_WF int check_termination(const Info &inf, int approximate, int64_t &status, double &obj, const double D[VS],
+                                  const double Eb[VS], const double Eg[GS]) {
+        if ((inf.pri_res > kInf) || (inf.dua_res > kInf)) {
+            status = IMPC_NON_CVX;
+            obj = kNan;
+            return 1;
+        }
+        double eps_abs = st.eps_abs, eps_rel = st.eps_rel, eps_pinf = st.eps_prim_inf, eps_dinf = st.eps_dual_inf;
+        if (approximate) {
+            eps_abs *= 10;
+            eps_rel *= 10;
+            eps_pinf *= 10;
+            eps_dinf *= 10;
+        }
+        int prim_ok = 0, dual_ok = 0, prim_inf = 0, dual_inf = 0;
+        if (T.m == 0) {
+            prim_ok = 1;
+        } else {
+            if (inf.pri_res < eps_abs + eps_rel * inf.pri_norm_u)
+                prim_ok = 1;
+            else
+                prim_inf = primal_infeasible(eps_pinf, D, Eb, Eg);
+        }
+        if (inf.dua_res < eps_abs + eps_rel * inf.dua_norm_u)
+            dual_ok = 1;
+        else
+            dual_inf = dual_infeasible(eps_dinf, D, Eb, Eg);
+        if (prim_ok && dual_ok) {
+            status = approximate ? IMPC_SOLVED_INACCURATE : IMPC_SOLVED;
+            return 1;
+        } else if (prim_inf) {
+            status = approximate ? IMPC_PRIMAL_INFEASIBLE_INACCURATE : IMPC_PRIMAL_INFEASIBLE;
+            obj = kInf;
+            return 1;
+        } else if (dual_inf) {
+            status = approximate ? IMPC_DUAL_INFEASIBLE_INACCURATE : IMPC_DUAL_INFEASIBLE;
+            obj = -kInf;
+            return 1;
+        }
+        return 0;
+    }
+
+    IMPC_WF double rho_estimate(const Info &inf) const {
+        double pri = inf.pri_plain / (inf.pri_norm_s + kDivTol);
+        double dua = inf.dua_plain / (inf.dua_norm_s + kDivTol);
+        double est = R.rho * sqrt(pri / (dua + kDivTol));
+        return dmin(dmax(est, kRhoMin), kRhoMax);
+    }
+
+    // ------------------------------------------------------------------ whole solve
+    // The scaling vectors D, E live in the per-QP global scratch (written by scale()) and are
+    // reloaded only where OSQP needs them (warm start, termination checks, unscaling), so they do
+    // not occupy registers across the ADMM loop.
+    IMPC_WF void solve(int64_t b) {
+        const int n = T.n, m = T.m;
+        clear_exchange();
+        load(b);
+        {
+            double D[VS], Eb[VS], Eg[GS];
+            scale(b, D, Eb, Eg);
+        }
+        set_rho(dmin(dmax(st.rho, kRhoMin), kRhoMax));
+        int bad = factorize();
+        impc_info *out = io.info + b;
+        if (bad) {
+            _Pragma("unroll") for (int s = 0; s < VS; s++)
+                if (vok[s]) io.xo[b * n + T.var_orig[NL * s + L]] = kNan;
+            _Pragma("unroll") for (int s = 0; s < VS; s++)
+                if (vok[s]) io.yo[b * m + T.var_boxrow[NL * s + L]] = kNan;
+            _Pragma("unroll") for (int s = 0; s < GS; s++)
+                if (gok[s]) io.yo[b * m + T.gen_row[NL * s + L]] = kNan;
+            if (L == 0) {
+                out->iter = 0;
+                out->status_val = IMPC_NON_CVX;
+                out->rho_updates = 0;
+                out->setup_exitflag = IMPC_NONCVX_ERROR;
+                out->obj_val = kNan;
+                out->pri_res = out->dua_res = 0.0;
+                out->rho_estimate = R.rho;
+            }
+            wv.sync();
+            return;
+        }
+        // iterates: zero, then osqp_warm_start (x <- Dinv x, y <- c Einv y, z <- A x)
+        if (io.has_ws) {
+            double D[VS], Eb[VS], Eg[GS];
+            load_scal(b, D, Eb, Eg);
+            double *xb = xbuf();
+            _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                if (!vok[s]) continue;
+                int ov = T.var_orig[NL * s + L];
+                double xv = io.xws[b * n + ov];
+                x[s] = st.scaling > 0 ? (1. / D[s]) * xv : xv;
+                double yv = io.yws[b * m + T.var_boxrow[NL * s + L]];
+                if (st.scaling > 0) {
+                    yv = (1. / Eb[s]) * yv;
+                    yv *= c;
+                }
+                yb[s] = yv;
+                zb[s] = ab[s] * x[s];
+                xb[NL * s + L] = x[s];
+            }
+            wv.sync();
+            _Pragma("unroll") for (int s = 0; s < GS; s++) {
+                if (!gok[s]) continue;
+                double yv = io.yws[b * m + T.gen_row[NL * s + L]];
+                if (st.scaling > 0) {
+                    yv = (1. / Eg[s]) * yv;
+                    yv *= c;
+                }
+                y[s] = yv;
+                double zz = 0.0;
+                _Pragma("unroll") for (int e = 0; e < 4; e++) zz += a[s][e] * xb[gc[s][e]];
+                z[s] = zz;
+            }
+            wv.sync();
+            clear_exchange();
+        }
+        write_v_products();
+
+        int64_t status = IMPC_UNSOLVED, rho_updates = 0, iter;
+        double obj = 0.0, rho_est = R.rho;
+        Info inf{};
+        int64_t info_iter = 0;
+        const int chk = st.check_termination;
+        int can_check = 0;
+        const uint64_t t0 = device_clock_100mhz();
+        bool time_limited = false;
+        for (iter = 1; iter <= st.max_iter; iter++) {
+            const bool need_delta = (chk && iter % chk == 0) || iter == st.max_iter || st.time_limit > 0;
+            iterate(need_delta);
+            if (st.time_limit > 0) {
+                double el = (double)(device_clock_100mhz() - t0) * 1e-8;
+                el = wv.bcast(el, 0);
+                if (el >= st.time_limit) {
+                    time_limited = true;
+                    can_check = 0;
+                    break;
+                }
+            }
+            can_check = chk && (iter % chk == 0);
+            if (can_check) {
+                double D[VS], Eb[VS], Eg[GS];
+                load_scal(b, D, Eb, Eg);
+                update_info(inf, D, Eb, Eg);
+                info_iter = iter;
+                int done = check_termination(inf, 0, status, obj, D, Eb, Eg);
+                write_v_products();
+                if (done) break;
+            }
+            if (st.adaptive_rho && st.rho_interval && (iter % st.rho_interval == 0)) {
+                if (!can_check) {
+                    double D[VS], Eb[VS], Eg[GS];
+                    load_scal(b, D, Eb, Eg);
+                    update_info(inf, D, Eb, Eg);
+                    info_iter = iter;
+                    write_v_products();
+                }
+                double rn = rho_estimate(inf);
+                rho_est = rn;
+                if ((rn > R.rho * st.adaptive_rho_tolerance) || (rn < R.rho / st.adaptive_rho_tolerance)) {
+                    set_rho(dmin(dmax(rn, kRhoMin), kRhoMax));
+                    factorize();
+                    write_v_products();
+                    rho_updates += 1;
+                }
+            }
+        }
+        double D[VS], Eb[VS], Eg[GS];
+        load_scal(b, D, Eb, Eg);
+        if (time_limited || !can_check) {
+            update_info(inf, D, Eb, Eg);
+            info_iter = time_limited ? iter : iter - 1;
+            status = IMPC_UNSOLVED;
+            check_termination(inf, 0, status, obj, D, Eb, Eg);
+        }
+        const bool has_sol = status != IMPC_PRIMAL_INFEASIBLE && status != IMPC_PRIMAL_INFEASIBLE_INACCURATE &&
+                             status != IMPC_DUAL_INFEASIBLE && status != IMPC_DUAL_INFEASIBLE_INACCURATE &&
+                             status != IMPC_NON_CVX;
+        if (has_sol) {
+            double qf = 0.0;
+            _Pragma("unroll") for (int s = 0; s < VS; s++)
+                if (vok[s]) qf += (double).5 * pd[s] * x[s] * x[s] + q[s] * x[s];
+            obj = wv.sum(qf);
+            if (st.scaling > 0) obj *= cinv;
+        }
+        if (status == IMPC_UNSOLVED) {
+            if (!check_termination(inf, 1, status, obj, D, Eb, Eg))
+                status = time_limited ? IMPC_TIME_LIMIT_REACHED : IMPC_MAX_ITER_REACHED;
+        }
+        rho_est = rho_estimate(inf);
+        const bool has_sol2 = status != IMPC_PRIMAL_INFEASIBLE && status != IMPC_PRIMAL_INFEASIBLE_INACCURATE &&
+                              status != IMPC_DUAL_INFEASIBLE && status != IMPC_DUAL_INFEASIBLE_INACCURATE &&
+                              status != IMPC_NON_CVX;
+        const bool scaled = st.scaling > 0;
+        _Pragma("unroll") for (int s = 0; s < VS; s++) {
+            if (!vok[s]) continue;
+            int v = NL * s + L;
+            io.xo[b * n + T.var_orig[v]] = has_sol2 ? (scaled ? D[s] * x[s] : x[s]) : kNan;
+            double yv = has_sol2 ? (scaled ? (Eb[s] * yb[s]) * cinv : yb[s]) : kNan;
+            io.yo[b * m + T.var_boxrow[v]] = yv;
+        }
+        _Pragma("unroll") for (int s = 0; s < GS; s++) {
+            if (!gok[s]) continue;
+            double yv = has_sol2 ? (scaled ? (Eg[s] * y[s]) * cinv : y[s]) : kNan;
+            io.yo[b * m + T.gen_row[NL * s + L]] = yv;
+        }
+        if (L == 0) {
+            out->iter = info_iter;
+            out->status_val = status;
+            out->rho_updates = rho_updates;
+            out->setup_exitflag = 0;
+            out->obj_val = obj;
+            out->pri_res = inf.pri_res;
+            out->dua_res = inf.dua_res;
+            out->rho_estimate = rho_est;
+        }
+        wv.sync();
+    }
+};
+
+}  // namespace impc

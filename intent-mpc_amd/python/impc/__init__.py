@@ -54,7 +54,8 @@ INFO_DTYPE = np.dtype([("iter", np.int64), ("status_val", np.int64), ("rho_updat
 
 class Stats(C.Structure):
     _fields_ = [(k, C.c_int64) for k in ("n", "m", "nnzP", "nnzA", "batch", "batch_stride", "nnzL", "nnzLcol",
-                                         "n_terms", "bandwidth", "device_bytes")]
+                                         "n_terms", "bandwidth", "device_bytes", "kernel",
+                                         "structured_ok")]
 
 
 class MpcParams(C.Structure):
@@ -107,6 +108,7 @@ _sig("impc_batch_get_stats", C.c_int, _P, C.POINTER(Stats))
 _sig("impc_batch_get_perm", C.c_int, _P, _i64p)
 _sig("impc_batch_set_profiling", C.c_int, _P, C.c_int)
 _sig("impc_batch_get_timings", C.c_int, _P, _dp, _dp, _dp)
+_sig("impc_batch_set_kernel", C.c_int, _P, C.c_int)
 _sig("impc_mpc_dims", C.c_int, C.POINTER(MpcParams), C.c_int32, C.c_int32, C.POINTER(Dims))
 _sig("impc_mpc_build_pattern", C.c_int, C.POINTER(MpcParams), C.c_int32, C.c_int32, _i64p, _i64p, _i64p, _i64p)
 _sig("impc_mpc_build_values", C.c_int, C.POINTER(MpcParams), C.c_int64, _dp, _dp, _dp, _dp, C.c_int32, _dp, _dp,
@@ -114,13 +116,15 @@ _sig("impc_mpc_build_values", C.c_int, C.POINTER(MpcParams), C.c_int64, _dp, _dp
 _sig("impc_mpc_warm_start", C.c_int, C.POINTER(MpcParams), C.c_int64, _dp, _dp, _dp)
 
 # every symbol declared in include/*.h (checked by tests/test_abi.py)
+KERNEL_AUTO, KERNEL_GENERIC, KERNEL_STRUCTURED = 0, 1, 2
+
 EXPORTED = [
     "impc_default_settings", "impc_last_error", "impc_version", "impc_ctx_create", "impc_ctx_destroy",
     "impc_ctx_stream", "impc_ctx_synchronize", "impc_batch_create", "impc_batch_destroy", "impc_batch_set_settings",
     "impc_batch_set_values", "impc_batch_set_values_device", "impc_batch_warm_start", "impc_batch_setup",
     "impc_batch_solve", "impc_batch_get", "impc_batch_device_results", "impc_batch_update_lin_cost",
     "impc_batch_update_bounds", "impc_batch_get_stats", "impc_batch_get_perm", "impc_batch_set_profiling",
-    "impc_batch_get_timings", "impc_mpc_dims",
+    "impc_batch_get_timings", "impc_batch_set_kernel", "impc_mpc_dims",
     "impc_mpc_build_pattern", "impc_mpc_build_values", "impc_mpc_warm_start",
 ]
 
@@ -242,6 +246,11 @@ class Batch:
         s = Stats()
         _check(lib.impc_batch_get_stats(self.h, C.byref(s)), "impc_batch_get_stats")
         return {f: getattr(s, f) for f, _ in Stats._fields_}
+
+    def set_kernel(self, kernel):
+        """impc_batch_set_kernel: KERNEL_AUTO / KERNEL_GENERIC / KERNEL_STRUCTURED."""
+        _check(lib.impc_batch_set_kernel(self.h, int(kernel)), "impc_batch_set_kernel")
+        return self
 
     def set_profiling(self, on=True):
         _check(lib.impc_batch_set_profiling(self.h, 1 if on else 0), "impc_batch_set_profiling")

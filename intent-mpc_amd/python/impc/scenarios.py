@@ -110,6 +110,24 @@ def intent_config(N=20, K=8, instances=8192, hyps=8, seed=3000, params=None):
     obv = np.stack([spd * np.cos(hdg), spd * np.sin(hdg), np.zeros((I, K))], axis=2)
     pred = predict_intents(obp, obv, ts=ts)                 # [I, K, 4, 31, 3]
     prob = rng.dirichlet(np.ones(4), size=(I, K))            # [I, K, 4]
+    # The previous plan (the linearisation point, mpcPlanner.cpp:1042-1051) was the collision-free
+    # answer of the last replan: re-draw obstacles whose most likely predicted track enters the
+    # inflated ellipsoid around it (semi-axis size/2 + dynamic safety distance).
+    clear = 0.4 + pd["dynamic_safety_dist"]
+    for _ in range(64):
+        am = np.argmax(prob, axis=2)
+        track = np.take_along_axis(pred, am[:, :, None, None, None], axis=2)[:, :, 0, :N]   # [I, K, N, 3]
+        bad = (np.linalg.norm(track - prev[:, None, :, :3], axis=3) < clear).any(axis=2)   # [I, K]
+        if not bad.any():
+            break
+        nb_ = int(bad.sum())
+        obp[bad] = np.stack([pos[np.nonzero(bad)[0], 0] + rng.uniform(3, 15, nb_), rng.uniform(-4, 4, nb_),
+                             rng.uniform(1.0, 3.0, nb_)], axis=1)
+        h2 = rng.uniform(-math.pi, math.pi, nb_)
+        s2 = rng.uniform(0.5, 2.0, nb_)
+        obv[bad] = np.stack([s2 * np.cos(h2), s2 * np.sin(h2), np.zeros(nb_)], axis=1)
+        pred[bad] = predict_intents(obp[bad], obv[bad], ts=ts)
+        prob[bad] = rng.dirichlet(np.ones(4), size=nb_)
     size = np.full(3, 0.8)                                   # dynus_obstacles_node.cpp:81 cubes
     # findClosestObstacle (first-time branch, :663-674): nearest current position
     d = np.linalg.norm(obp - pos[:, None, :], axis=2)

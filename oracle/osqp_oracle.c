@@ -961,7 +961,7 @@ static void store_solution(ora_ws *w) {
         memcpy(w->sol_y, w->y, sizeof(c_float) * (size_t)w->m);
         if (w->scaled) {
             for (c_int i = 0; i < w->n; i++) w->sol_x[i] = w->D[i] * w->sol_x[i];
-            for (c_int i = 0; i < w->m; i++) w->sol_y[i] = w->Einv[i] * w->sol_y[i];
+            for (c_int i = 0; i < w->m; i++) w->sol_y[i] = w->E[i] * w->sol_y[i]; /* y = E y / c */
             for (c_int i = 0; i < w->m; i++) w->sol_y[i] *= w->cinv;
         }
     } else {
@@ -1187,7 +1187,7 @@ void ora_get(const ora_ws *w, c_float *x, c_float *y, ora_info *info) {
 /* Unscaled (x, y) iterates, for the persistent-workspace tests. */
 void ora_get_iterates(const ora_ws *w, c_float *x, c_float *y) {
     for (c_int i = 0; i < w->n; i++) x[i] = w->scaled ? w->D[i] * w->x[i] : w->x[i];
-    for (c_int i = 0; i < w->m; i++) y[i] = w->scaled ? w->Einv[i] * w->y[i] * w->cinv : w->y[i];
+    for (c_int i = 0; i < w->m; i++) y[i] = w->scaled ? w->E[i] * w->y[i] * w->cinv : w->y[i];
 }
 
 void ora_cleanup(ora_ws *w) {

@@ -1,0 +1,125 @@
+// wave_emu.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// Executes the one-QP-per-wavefront kernel body (intent-mpc_amd/csrc/mpc_wave.hpp) on the CPU by
+// running its 64 lanes as 64 threads that meet at a barrier wherever the GPU wave synchronises
+// (LDS exchange, readlane broadcast, wave reductions).  This lets the structured solver be
+// checked against the oracle in the GPU-less container.  Never linked into libimpc_qp.so.
+#include <barrier>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../../intent-mpc_amd/csrc/mpc_structure.hpp"
+#include "../../intent-mpc_amd/csrc/mpc_wave.hpp"
+
+namespace {
+
+constexpr int NL = 128;
+
+struct EmuShared {
+    std::barrier<> bar{NL};
+    double scratch[2][NL];
+};
+
+struct EmuWave {
+    int l;
+    EmuShared *sh;
+    int par = 0;
+    int lane() const { return l; }
+    void sync() { sh->bar.arrive_and_wait(); }
+    double *next_buf() {
+        double *b = sh->scratch[par];
+        par ^= 1;
+        return b;
+    }
+    double bcast(double v, int src) {  // lane src of the caller's 64-lane wavefront
+        double *b = next_buf();
+        b[l] = v;
+        sync();
+        return b[(l & ~63) + src];
+    }
+    double max(double v) {
+        double *b = next_buf();
+        b[l] = v;
+        sync();
+        double r = b[0];
+        for (int i = 1; i < NL; i++) r = b[i] > r ? b[i] : r;
+        return r;
+    }
+    double sum(double v) {  // per-wavefront xor butterfly (lane 0's value), waves added in order
+        double *b = next_buf();
+        b[l] = v;
+        sync();
+        double r = 0.0;
+        for (int w = 0; w < NL / 64; w++) {
+            double s[64];
+            for (int i = 0; i < 64; i++) s[i] = b[64 * w + i];
+            for (int mask = 32; mask >= 1; mask >>= 1) {
+                double t[64];
+                for (int i = 0; i < 64; i++) t[i] = s[i] + s[i ^ mask];
+                for (int i = 0; i < 64; i++) s[i] = t[i];
+            }
+            r = w == 0 ? s[0] : r + s[0];
+        }
+        return r;
+    }
+};
+
+template <int VS, int GS>
+void run(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSettings &st) {
+    using LD = impc::WaveLds<NL, VS, GS>;
+    std::vector<double> lds(LD::SIZE, 0.0);
+    EmuShared sh;
+    std::vector<std::thread> th;
+    for (int l = 0; l < NL; l++)
+        th.emplace_back([&, l] {
+            EmuWave wv{l, &sh};
+            for (int64_t b = 0; b < io.B; b++) {
+                impc::WaveQP<EmuWave, NL, VS, GS> qp(wv, T, io, st, lds.data());
+                qp.solve(b);
+            }
+        });
+    for (auto &t : th) t.join();
+}
+
+}  // namespace
+
+extern "C" int emu_wave_solve_batch(int64_t n, int64_t m, const int64_t *Pp, const int64_t *Pi, const int64_t *Ap,
+                                    const int64_t *Ai, int64_t B, const double *Px, const double *q, const double *Ax,
+                                    const double *l, const double *u, const impc_settings *s, const double *xws,
+                                    const double *yws, double *xo, double *yo, impc_info *info) {
+    impc::MpcStructure ms;
+    if (!ms.analyse(n, m, Pp, Pi, Ap, Ai).empty()) return 1;
+    impc::WaveTables T{ms.n, ms.m, ms.mg, ms.N, ms.W, ms.CG, ms.nnzP, ms.nnzA,
+                       ms.var_orig.data(), ms.var_pdiag.data(), ms.var_boxrow.data(), ms.var_boxpos.data(),
+                       ms.gen_row.data(), ms.gen_col.data(), ms.gen_pos.data(), ms.colg.data(),
+                       ms.term_ptr.data(), ms.term.data()};
+    std::vector<double> zx((size_t)B * n, 0.0), zy((size_t)B * m, 0.0), scal((size_t)B * (2 * n + ms.mg), 0.0);
+    impc::WaveIO io{B, Px, q, Ax, l, u, xws ? xws : zx.data(), yws ? yws : zy.data(), xws ? 1 : 0,
+                    xo, yo, scal.data(), info};
+    impc::DevSettings st{};
+    st.rho = s->rho;
+    st.sigma = s->sigma;
+    st.adaptive_rho_tolerance = s->adaptive_rho_tolerance;
+    st.eps_abs = s->eps_abs;
+    st.eps_rel = s->eps_rel;
+    st.eps_prim_inf = s->eps_prim_inf;
+    st.eps_dual_inf = s->eps_dual_inf;
+    st.alpha = s->alpha;
+    st.time_limit = 0;
+    st.scaling = (int32_t)s->scaling;
+    st.adaptive_rho = (int32_t)s->adaptive_rho;
+    st.rho_interval = s->adaptive_rho_interval ? (int32_t)s->adaptive_rho_interval
+                                               : (int32_t)(s->check_termination ? s->check_termination : 25);
+    st.max_iter = (int32_t)s->max_iter;
+    st.scaled_termination = (int32_t)s->scaled_termination;
+    st.check_termination = (int32_t)s->check_termination;
+    st.warm_start = (int32_t)s->warm_start;
+    if (ms.n <= 2 * NL && ms.mg <= 3 * NL)
+        run<2, 3>(T, io, st);
+    else if (ms.n <= 2 * NL && ms.mg <= 4 * NL)
+        run<2, 4>(T, io, st);
+    else
+        return 2;
+    return 0;
+}

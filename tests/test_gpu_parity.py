@@ -14,41 +14,58 @@ from helpers import compare, gpu, oracle
 pytestmark = pytest.mark.gpu
 
 S25 = dict(verbose=0, adaptive_rho_interval=25)
+KERNELS = pytest.mark.parametrize("kernel", [impc.KERNEL_GENERIC, impc.KERNEL_STRUCTURED], ids=["generic", "structured"])
 
 
-def test_config1_first_call(ctx):
+@KERNELS
+def test_config1_first_call(ctx, kernel):
     cfg = scenarios.first_call_config(batch=64, seed=101)
     s = impc.default_settings(**S25)
-    compare(gpu(ctx, cfg, s), oracle(cfg, s))
+    compare(gpu(ctx, cfg, s, kernel), oracle(cfg, s))
 
 
-def test_config2_static_obstacles(ctx):
+@KERNELS
+def test_config2_static_obstacles(ctx, kernel):
     cfg = scenarios.static_config(batch=96, identical=False, seed=202)
     s = impc.default_settings(**S25)
-    compare(gpu(ctx, cfg, s), oracle(cfg, s))
+    compare(gpu(ctx, cfg, s, kernel), oracle(cfg, s))
 
 
-def test_config3_intent_hypotheses(ctx):
+@KERNELS
+def test_config3_intent_hypotheses(ctx, kernel):
     buckets = scenarios.intent_config(instances=24, seed=303)
     s = impc.default_settings(**S25)
     for K, bk in buckets.items():
-        compare(gpu(ctx, bk, s), oracle(bk, s))
+        compare(gpu(ctx, bk, s, kernel), oracle(bk, s))
 
 
-def test_default_auto_interval_matches_pinned(ctx):
+@KERNELS
+def test_default_auto_interval_matches_pinned(ctx, kernel):
     """adaptive_rho_interval = 0 resolves to check_termination (25) on the device."""
     cfg = scenarios.static_config(batch=32, identical=False, seed=404)
-    r0 = gpu(ctx, cfg, impc.default_settings(verbose=0))
-    r25 = gpu(ctx, cfg, impc.default_settings(**S25))
+    r0 = gpu(ctx, cfg, impc.default_settings(verbose=0), kernel)
+    r25 = gpu(ctx, cfg, impc.default_settings(**S25), kernel)
     assert np.array_equal(r0[0], r25[0]) and np.array_equal(r0[2]["iter"], r25[2]["iter"])
 
 
-def test_identical_batch_full_size(ctx):
+@KERNELS
+def test_identical_batch_full_size(ctx, kernel):
     """Config 2 shape at batch 4096: every copy of one QP gives bitwise the same answer, and that
     answer matches the oracle's single solve (size-independent property at full batch)."""
     cfg = scenarios.static_config(batch=4096, identical=True, seed=2000)
     s = impc.default_settings(verbose=0)
-    x, y, info = gpu(ctx, cfg, s)
+    x, y, info = gpu(ctx, cfg, s, kernel)
     assert np.all(x == x[0]) and np.all(info["iter"] == info["iter"][0])
     one = dict(cfg, values={k: v[:1] for k, v in cfg["values"].items()})
     compare((x[:1], y[:1], info[:1]), oracle(one, s))
+
+
+def test_auto_selects_structured_for_mpc_patterns(ctx):
+    for cfg in (scenarios.first_call_config(batch=2), scenarios.static_config(batch=2)):
+        pat = cfg["pattern"]
+        b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], 2)
+        try:
+            st = b.stats()
+            assert st["structured_ok"] == 1 and st["kernel"] == impc.KERNEL_STRUCTURED
+        finally:
+            b.close()

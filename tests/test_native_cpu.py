@@ -1,0 +1,64 @@
+"""The device algorithms, compiled for the host (test-only builds under tests/native/), against
+the oracle -- the GPU-less half of the parity story.
+
+* admm_core.hpp (generic one-QP-per-lane kernel body) through tests/native/core_harness.cpp
+* mpc_wave.hpp (structured one-QP-per-128-lane-team kernel body) through tests/native/wave_emu.cpp,
+  which runs the 128 lanes as threads meeting at a barrier wherever the GPU team synchronises.
+
+Both must reproduce the oracle's iteration count and status exactly and its primal/dual to
+PRIMAL_RTOL (they use different but exact-arithmetic-equivalent linear algebra).
+"""
+import numpy as np
+import pytest
+
+import impc
+from impc import scenarios
+
+from helpers import compare, emulate, harness, oracle, take
+
+S25 = dict(verbose=0, adaptive_rho_interval=25)
+
+
+def configs():
+    b3 = scenarios.intent_config(instances=3, seed=303)
+    return {
+        "config1": scenarios.first_call_config(batch=4, seed=101),
+        "config2": scenarios.static_config(batch=4, identical=False, seed=202),
+        "config3_K8": b3[8],
+        "config3_K9": b3[9],
+        "config5_N40": scenarios.static_config(N=40, K=10, batch=2, identical=False, seed=505),
+    }
+
+
+CFG = configs()
+
+
+@pytest.mark.parametrize("name", list(CFG))
+def test_generic_core_matches_oracle(name):
+    s = impc.default_settings(**S25)
+    compare(harness(CFG[name], s), oracle(CFG[name], s))
+
+
+@pytest.mark.parametrize("rho", [0.1, 1e-3])
+def test_generic_core_infeasible_and_rho_paths(rho):
+    """Primal-infeasible instances (a box row contradicting the pinned initial state) and a small initial rho that forces
+    adaptive rho updates (in-kernel refactorisation) follow the oracle too."""
+    cfg = scenarios.static_config(batch=4, identical=False, seed=909)
+    v = cfg["values"]
+    l = v["l"].copy()
+    N = cfg["N"]
+    l[1, 8 * N + 1] = 4.9  # y of x0 boxed to [4.9, 5] while the dynamics rows pin x0 -> infeasible
+    cfg = dict(cfg, values=dict(v, l=l))
+    s = impc.default_settings(rho=rho, **S25)
+    res, ref = harness(cfg, s), oracle(cfg, s)
+    compare(res, ref)
+    assert ref[2]["status_val"][1] in (-3, 3)
+    if rho < 0.1:
+        assert ref[2]["rho_updates"].max() >= 1
+
+
+def test_structured_emulation_matches_oracle():
+    """One intent-hypothesis QP (config 3 shape, warm-started) through the 128-lane emulation."""
+    cfg = take(CFG["config3_K9"], 1)
+    s = impc.default_settings(**S25)
+    compare(emulate(cfg, s), oracle(cfg, s))

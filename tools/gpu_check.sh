@@ -1,0 +1,23 @@
+#!/bin/bash
+# GPU-box check run: parity tests, smoke, bench, kernel-trace profile.  Every GPU step has its own
+# time limit and the script stops at the first failure.
+set -o pipefail
+R="$GRAFT_REPO_ROOT"
+cd "$R" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() { echo "== $1"; }
+step pytest
+timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+tail -3 gpurun_out/pytest_gpu.log
+step smoke
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -30 gpurun_out/smoke.log; exit 1; }
+step bench
+timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1 || { tail -30 gpurun_out/bench.log; exit 1; }
+tail -c 2500 gpurun_out/bench.log
+if [ -n "${PROFILE:-}" ]; then
+  step rocprof
+  cd /tmp || exit 1
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 > "$R/gpurun_out/prof.log" 2>&1 || { tail -30 "$R/gpurun_out/prof.log"; exit 1; }
+  find "$R/gpurun_out/prof" -name "*kernel_stats.csv" -exec cat {} \;
+fi
