@@ -18,6 +18,13 @@ tail -c 2500 gpurun_out/bench.log
 if [ -n "${PROFILE:-}" ]; then
   step rocprof
   cd /tmp || exit 1
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 > "$R/gpurun_out/prof.log" 2>&1 || { tail -30 "$R/gpurun_out/prof.log"; exit 1; }
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" ${BENCH_ARGS:-} > "$R/gpurun_out/prof.log" 2>&1 || { tail -30 "$R/gpurun_out/prof.log"; exit 1; }
   find "$R/gpurun_out/prof" -name "*kernel_stats.csv" -exec cat {} \;
+fi
+if [ -n "${PMC:-}" ]; then
+  step pmc
+  cd /tmp || exit 1
+  timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/gpurun_out/pmc_fetch" -o pmc -- python3 "$R/bench.py" --steps 1 --warmup 0 --cpu-sample 0 > "$R/gpurun_out/pmc_fetch.log" 2>&1 || { tail -30 "$R/gpurun_out/pmc_fetch.log"; exit 1; }
+  timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/gpurun_out/pmc_write" -o pmc -- python3 "$R/bench.py" --steps 1 --warmup 0 --cpu-sample 0 > "$R/gpurun_out/pmc_write.log" 2>&1 || { tail -30 "$R/gpurun_out/pmc_write.log"; exit 1; }
+  python3 "$R/tools/pmc_summary.py" "$R/gpurun_out/pmc_fetch" "$R/gpurun_out/pmc_write" k_mpc_wave 65536 > "$R/gpurun_out/pmc_k_solve.json" && cat "$R/gpurun_out/pmc_k_solve.json"
 fi

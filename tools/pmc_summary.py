@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""Summarise two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) of `bench.py --steps 1 --warmup 0`
+into the per-step HBM traffic of the solver kernel (MI355X_MICROARCH.md, HBM section: FETCH_SIZE
+counts half the bytes of wide coalesced reads on gfx950 -> x2; WRITE_SIZE exact; both in KB).
+
+usage: pmc_summary.py FETCH_DIR WRITE_DIR KERNEL QPS_PER_STEP > pmc_k_solve.json
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def collect(d, counter, kernel):
+    vals = []
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if row.get("Counter_Name") == counter and kernel in row.get("Kernel_Name", ""):
+                vals.append(float(row["Counter_Value"]))
+    return vals
+
+
+def main():
+    fdir, wdir, kernel, qps = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+    fetch = collect(fdir, "FETCH_SIZE", kernel)
+    write = collect(wdir, "WRITE_SIZE", kernel)
+    if not fetch or not write:
+        sys.exit(f"no {kernel} rows (fetch {len(fetch)}, write {len(write)})")
+    fetch_b = 2.0 * 1024.0 * sum(fetch)   # KB -> bytes, gfx950 half-count correction
+    write_b = 1024.0 * sum(write)
+    print(json.dumps({
+        "kernel": kernel, "qps_per_launch": qps, "launches": len(fetch),
+        "fetch_size_kb_raw": sum(fetch), "write_size_kb_raw": sum(write),
+        "hbm_bytes_per_launch": fetch_b + write_b, "fetch_bytes": fetch_b, "write_bytes": write_b,
+        "correction": "FETCH_SIZE x2 (gfx950 wide-read half count), WRITE_SIZE x1; summed over the step's launches",
+    }, indent=1))
+
+
+if __name__ == "__main__":
+    main()
