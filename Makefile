@@ -16,11 +16,12 @@ HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-funct
 HOSTFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -Wall
 
 LIB     := $(LIBDIR)/libimpc_qp.so
+PROFLIB := $(LIBDIR)/libimpc_qp_prof.so
 ORACLE  := $(ORADIR)/libosqp_oracle.so
 HARNESS := $(HARNDIR)/libimpc_core_cpu.so
 EMU     := $(HARNDIR)/libwave_emu.so
 
-.PHONY: all lib oracle harness clean
+.PHONY: all lib oracle harness prof clean
 all: lib oracle harness
 lib: $(LIB)
 oracle: $(ORACLE)
@@ -30,6 +31,15 @@ $(LIBDIR)/impc_qp.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symbolic.
 		$(CSRC)/mpc_structure.hpp $(ROOT)/include/impc_qp.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# section-profiling variant of the library (tools/section_profile.py; never the product)
+prof: $(PROFLIB)
+$(LIBDIR)/impc_qp_prof.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symbolic.hpp $(CSRC)/mpc_wave.hpp \
+		$(CSRC)/mpc_structure.hpp $(ROOT)/include/impc_qp.h
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DIMPC_SECTION_PROF -c $< -o $@
+$(PROFLIB): $(LIBDIR)/impc_qp_prof.o $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ -o $@
 
 $(LIBDIR)/symbolic.o: $(CSRC)/symbolic.cpp $(CSRC)/symbolic.hpp
 	@mkdir -p $(LIBDIR)

@@ -31,6 +31,12 @@ PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PEAK_FP64_TFLOPS = 78.6    # MI355X FP64 vector peak (spec)
 
 
+def throughput(world, qps_per_rank, steps, elapsed_s):
+    """Whole-job QP solves per second: every rank solves qps_per_rank QPs per step, `steps` steps
+    in `elapsed_s` (max over ranks)."""
+    return world * qps_per_rank * steps / elapsed_s
+
+
 def algorithmic_bytes(n, m, K, N):
     """B_solve = 8(n + 2m + 4K W) + 8(n + m) + 16 per QP."""
     W = N - 1
@@ -120,7 +126,7 @@ def main():
     if not args.no_allgather:
         D.gather_records(dist, np.concatenate(recs))  # hypothesis costs to every rank
 
-    value = world * total_qps / elapsed  # whole-job QP solves per second
+    value = throughput(world, total_qps, args.steps, elapsed)
 
     # roofline of the dominant kernel, SURVEY.md 8(d) algorithmic bytes
     kernel_name = "k_mpc_wave" if all(b.stats()["kernel"] == impc.KERNEL_STRUCTURED for _, _, b in batches) \

@@ -172,6 +172,50 @@ struct GpuTeam {
         int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
         return __hiloint2double(hi, lo);
     }
+    // v of lane src (per-lane) of the caller's wavefront: ds_bpermute on both halves
+    __device__ double shfl(double v, int src) {
+        const int addr = src << 2;
+        int lo = __builtin_amdgcn_ds_bpermute(addr, __double2loint(v));
+        int hi = __builtin_amdgcn_ds_bpermute(addr, __double2hiint(v));
+        return __hiloint2double(hi, lo);
+    }
+    template <int CTRL>
+    __device__ static double dpp(double v) {
+        int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+        int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+        return __hiloint2double(hi, lo);
+    }
+    // sum over lanes {8i, .., 8i+7}: quad_perm xor 1, quad_perm xor 2, row_half_mirror.  Every
+    // stage adds a commuted operand pair, so all 8 lanes hold bitwise the same
+    // ((v0+v1)+(v2+v3)) + ((v4+v5)+(v6+v7)).
+    __device__ double sum_contig8(double v) {
+        v = v + dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+        v = v + dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+        v = v + dpp<0x141>(v);  // row_half_mirror
+        return v;
+    }
+    // (x[low], x[high]) of the lane pair l, l ^ 16 (P16) or l, l ^ 32 (P32), gfx950 permlane swaps
+    template <bool P32>
+    __device__ static double pair_sum(double v) {
+        const int lo = __double2loint(v), hi = __double2hiint(v);
+        if (P32) {
+            auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+            auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+            return __hiloint2double(rh[0], rl[0]) + __hiloint2double(rh[1], rl[1]);
+        } else {
+            auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+            auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+            return __hiloint2double(rh[0], rl[0]) + __hiloint2double(rh[1], rl[1]);
+        }
+    }
+    // sum over lanes {j, j+8, .., j+56}: row_ror 8 (xor 8), then xor 16 and xor 32 pair sums,
+    // low + high in both partners: ((v0+v1)+(v2+v3)) + ((v4+v5)+(v6+v7)) over the 8 rows i
+    __device__ double sum_stride8(double v) {
+        v = v + dpp<0x128>(v);  // row_ror:8
+        v = pair_sum<false>(v);
+        v = pair_sum<true>(v);
+        return v;
+    }
     __device__ double max(double v) {
         for (int mask = 32; mask >= 1; mask >>= 1) {
             double o = __shfl_xor(v, mask);
@@ -205,6 +249,7 @@ __global__ __launch_bounds__(NL, 1) void k_mpc_wave(impc::WaveTables T, impc::Wa
     using LD = impc::WaveLds<NL, VS, GS>;
     GpuTeam<NL> wv{smem + LD::RED_OFF};
     __shared__ unsigned next;
+    impc::WaveQP<GpuTeam<NL>, NL, VS, GS>::load_tables(wv, T, smem);
     for (;;) {
         if (threadIdx.x == 0) next = atomicAdd(counter, 1u);
         __syncthreads();
@@ -247,6 +292,7 @@ struct impc_batch_s {
     void *d_tables = nullptr;
     double *d_scal = nullptr;
     unsigned *d_counter = nullptr;
+    unsigned long long *d_sec = nullptr;  // section-profiling build only
     impc::WaveTables wt{};
     // ---- generic path (allocated on first use)
     std::unique_ptr<impc::Symbolic> sym;
@@ -468,6 +514,13 @@ int structured_solve(impc_batch b, hipStream_t st) {
     impc::WaveIO io{b->B,        b->in_Px,  b->in_q,  b->in_Ax,  b->in_l,  b->in_u, b->in_xws, b->in_yws,
                     b->has_ws ? 1 : 0, b->d_xout, b->d_yout, b->d_scal, b->d_info};
     HIP_OK(hipMemsetAsync(b->d_counter, 0, 256, st));
+#ifdef IMPC_SECTION_PROF
+    if (!b->d_sec) {
+        HIP_OK(hipMalloc((void **)&b->d_sec, sizeof(unsigned long long) * impc::kSecCount));
+        HIP_OK(hipMemsetAsync(b->d_sec, 0, sizeof(unsigned long long) * impc::kSecCount, st));
+    }
+    io.sec = b->d_sec;
+#endif
     if (b->profile) HIP_OK(hipEventRecord(b->ev[2], st));
     int rc;
     switch (b->gs) {
@@ -489,7 +542,7 @@ int structured_solve(impc_batch b, hipStream_t st) {
 int prepare_structured(impc_batch b) {
     b->ms.reset(new impc::MpcStructure());
     std::string why = b->ms->analyse(b->n, b->m, b->Pp.data(), b->Pi.data(), b->Ap.data(), b->Ai.data());
-    if (!why.empty() || b->ms->n > kTeam * kWaveVS) {
+    if (!why.empty() || b->ms->n > kTeam * kWaveVS || b->ms->CG > impc::WaveLds<kTeam, kWaveVS, 2>::CGM) {
         b->structured_ok = false;
         return IMPC_OK;
     }
@@ -675,7 +728,7 @@ int impc_batch_destroy(impc_batch b) {
     for (hipEvent_t e : b->ev)
         if (e) (void)hipEventDestroy(e);
     void *ptrs[] = {b->d_in, b->d_xout, b->d_yout, b->d_info, b->d_tables, b->d_scal, b->d_counter, b->d_sym,
-                    b->d_work};
+                    b->d_work, b->d_sec};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete b;
@@ -905,6 +958,20 @@ int impc_batch_get_timings(impc_batch b, double *setup_ms, double *solve_ms, dou
     }
     return IMPC_OK;
 }
+
+#ifdef IMPC_SECTION_PROF
+// Profiling build only (not part of include/impc_qp.h): cycle sums per section since the first
+// structured solve of this batch (enum kSec* in mpc_wave.hpp), then resets them.
+extern "C" int impc_debug_sections(impc_batch b, unsigned long long *out) {
+    if (!b || !out) return fail(IMPC_INVALID_ARGUMENT, "null argument");
+    for (int i = 0; i < impc::kSecCount; i++) out[i] = 0;
+    if (!b->d_sec) return IMPC_OK;
+    HIP_OK(hipStreamSynchronize(b->ctx->stream));
+    HIP_OK(hipMemcpy(out, b->d_sec, sizeof(unsigned long long) * impc::kSecCount, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemset(b->d_sec, 0, sizeof(unsigned long long) * impc::kSecCount));
+    return IMPC_OK;
+}
+#endif
 
 int impc_batch_get_perm(impc_batch b, int64_t *perm) {
     if (!b || !perm) return fail(IMPC_INVALID_ARGUMENT, "null argument");

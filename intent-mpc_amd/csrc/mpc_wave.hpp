@@ -25,7 +25,8 @@
 // with LDS visibility), bcast(v, j) (v of lane j of the CALLER's wavefront), max()/sum() over the
 // team, so the same code runs on the GPU (policy in impc_qp.hip) and, for tests only, in an
 // NL-thread CPU emulation (tests/native/wave_emu.cpp).  The 8-dim recursions are computed
-// redundantly by every wavefront of the team (lanes i = L & 7), so bcast never crosses waves.
+// redundantly by every wavefront of the team on its own 8x8 lane grid, so no exchange crosses
+// wavefronts inside them.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -52,7 +53,27 @@ struct WaveIO {
     double *xo, *yo;   // QP-major outputs (unscaled)
     double *scal;      // per-QP scratch [B][n + n + mg]: D, E(box), E(general)
     impc_info *info;
+    unsigned long long *sec = nullptr;  // section-profiling build only: cycle sums [kSecCount]
 };
+
+// Section profiling (profiling build of the library only, -DIMPC_SECTION_PROF): lane 0 of each
+// team accumulates s_memtime deltas per section; IMPC_SEC(X) closes section X.
+enum {
+    kSecSetup, kSecFactor, kSecWarm, kSecRhs, kSecS1, kSecFwd, kSecS3, kSecBwd, kSecS5, kSecUpdate, kSecProducts,
+    kSecChecks, kSecOutput, kSecIters = 15, kSecCount = 16
+};
+#if defined(IMPC_SECTION_PROF) && defined(__HIP_DEVICE_COMPILE__)
+#define IMPC_SEC(X)                                    \
+    do {                                               \
+        uint64_t t_ = __builtin_amdgcn_s_memtime();    \
+        sec_acc[X] += t_ - sec_t0;                     \
+        sec_t0 = t_;                                   \
+    } while (0)
+#define IMPC_SEC_START() (sec_t0 = __builtin_amdgcn_s_memtime())
+#else
+#define IMPC_SEC(X) ((void)0)
+#define IMPC_SEC_START() ((void)0)
+#endif
 
 // LDS doubles per wave for (VS, GS)
 template <int NL, int VS, int GS>
@@ -65,9 +86,13 @@ struct WaveLds {
     static constexpr int T_OFF = R_OFF + NP;                // tbuf
     static constexpr int E_OFF = T_OFF + NP;                // ebuf
     static constexpr int X_OFF = E_OFF + NP;                // xbuf
-    static constexpr int P_OFF = X_OFF + NP;                // products [4 * NL GS]
-    static constexpr int RED_OFF = P_OFF + 4 * NL * GS;     // team reduction scratch
-    static constexpr int SIZE = RED_OFF + 64;
+    static constexpr int P_OFF = X_OFF + NP;                // products [4 * NL GS] + zero slot
+    static constexpr int PZ = 4 * NL * GS;                  // zero slot (relative to P_OFF)
+    static constexpr int RED_OFF = P_OFF + PZ + 8;          // team reduction scratch
+    static constexpr int JUNK_OFF = RED_OFF + 64;           // per-lane discard slots [NL]
+    static constexpr int CGM = 24;                          // max general entries per column
+    static constexpr int CG_OFF = JUNK_OFF + NL;            // int16 column table [CGM][NMAX]
+    static constexpr int SIZE = CG_OFF + NMAX * CGM / 4;
     // factorisation aliases (inside R..X region and the products buffer)
     static constexpr int FA = R_OFF, FL = FA + 169, FI = FL + 169, FB = FI + 169, FG = FB + 104, FE = FG + 104,
                          RHOG = FE + 64, DIAGX = RHOG + NL * GS;
@@ -103,6 +128,16 @@ IMPC_WF int row_type(double l, double u) {  // set_rho_vec (auxil.h:34)
     return 0;
 }
 
+// a * b rounded on its own (never contracted into a following add), so the symmetric
+// cross-lane sums that consume it give bitwise-identical results in every lane of a group
+IMPC_WF double prod_nc(double a, double b) {
+    double p = a * b;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(p));
+#endif
+    return p;
+}
+
 template <class WV, int NL, int VS, int GS>
 struct WaveQP {
     using LD = WaveLds<NL, VS, GS>;
@@ -124,6 +159,9 @@ struct WaveQP {
     bool gok[GS];
     WaveRho R;
     double c = 1.0, cinv = 1.0;
+#if defined(IMPC_SECTION_PROF) && defined(__HIP_DEVICE_COMPILE__)
+    uint64_t sec_t0 = 0, sec_acc[kSecCount] = {};
+#endif
 
     IMPC_WF WaveQP(WV &w, const WaveTables &t, const WaveIO &i, const DevSettings &s, double *l)
         : wv(w), T(t), io(i), st(s), lds(l), L(w.lane()) {}
@@ -199,25 +237,43 @@ struct WaveQP {
         }
     }
 
+    // The per-column list of general-row entries (mpc_structure colg) as an int16 table in LDS,
+    // transposed ([t][v]) and padded to a multiple of 4 with the products buffer's zero slot, so
+    // the per-iteration gathers are branch-free LDS reads.  Loaded once per workgroup.
+    static IMPC_WF void load_tables(WV &w, const WaveTables &T, double *lds) {
+        int16_t *cg = (int16_t *)(lds + LD::CG_OFF);
+        const int CG4 = (T.CG + 3) & ~3;
+        for (int e = w.lane(); e < CG4 * LD::NMAX; e += NL) {
+            const int t = e / LD::NMAX, v = e % LD::NMAX;
+            int idx = (v < T.n && t < T.CG) ? T.colg[v * T.CG + t] : -1;
+            cg[e] = (int16_t)(idx >= 0 ? idx : LD::PZ);
+        }
+        if (w.lane() == 0) lds[LD::P_OFF + LD::PZ] = 0.0;
+        w.sync();
+    }
+
     // gather sum over the general entries of this variable's column from the products buffer
     IMPC_WF double col_gather(int v) {
-        double s = 0.0;
-        const int32_t *cl = T.colg + (int64_t)v * T.CG;
+        const int16_t *cg = (const int16_t *)(lds + LD::CG_OFF) + v;
         const double *pb = pbuf();
-        for (int t = 0; t < T.CG; t++) {
-            int idx = cl[t];
-            if (idx >= 0) s += pb[idx];
+        const int CG4 = (T.CG + 3) & ~3;
+        double s = 0.0;
+        for (int t = 0; t < CG4; t += 4) {
+            const int i0 = cg[t * LD::NMAX], i1 = cg[(t + 1) * LD::NMAX], i2 = cg[(t + 2) * LD::NMAX],
+                      i3 = cg[(t + 3) * LD::NMAX];
+            s += pb[i0];
+            s += pb[i1];
+            s += pb[i2];
+            s += pb[i3];
         }
         return s;
     }
     IMPC_WF double col_gather_max(int v) {
-        double s = 0.0;
-        const int32_t *cl = T.colg + (int64_t)v * T.CG;
+        const int16_t *cg = (const int16_t *)(lds + LD::CG_OFF) + v;
         const double *pb = pbuf();
-        for (int t = 0; t < T.CG; t++) {
-            int idx = cl[t];
-            if (idx >= 0) s = dmax(pb[idx], s);
-        }
+        const int CG4 = (T.CG + 3) & ~3;
+        double s = 0.0;
+        for (int t = 0; t < CG4; t++) s = dmax(pb[cg[t * LD::NMAX]], s);
         return s;
     }
 
@@ -431,7 +487,8 @@ struct WaveQP {
                     double s = 0.0;
                     for (int t = 0; t < 13; t++) s += G[13 * i + t] * Bb[13 * j + t];
                     E[8 * i + j] = s;
-                    Fm[64 * k + 8 * i + j] = G[13 * i + j];
+                    // recursion layout: lane (i,j) of step k reads F_k[j][i] (k even) / F_k[i][j]
+                    Fm[64 * k + 8 * i + j] = (k & 1) ? G[13 * i + j] : G[13 * j + i];
                 }
                 _Pragma("unroll") for (int s = 0; s < VS; s++) {
                     if (!vok[s]) continue;
@@ -450,6 +507,44 @@ struct WaveQP {
         clear_exchange();
         (void)n;
         return bad;
+    }
+
+    // One step of a stage recursion on the 8x8 lane grid: returns c - R(F v), R the strided
+    // (STRIDE) or contiguous 8-lane sum, and stores it at dst (a discard slot for non-writers).
+    template <bool STRIDE>
+    IMPC_WF double rstep(double f, double c, double v, double *dst) {
+        const double p = prod_nc(f, v);
+        const double r = c - (STRIDE ? wv.sum_stride8(p) : wv.sum_contig8(p));
+        *dst = r;
+        return r;
+    }
+
+    // S4 body for a first step k = W-1 of parity ODD: steps alternate strided (odd k) and
+    // contiguous (even k) reductions; x_k sits at index j (odd k) / i (even k).
+    template <bool ODD>
+    IMPC_WF void bwd_sweep(const double *eb, double *xb, int W) {
+        const double *Fm = lds + LD::F_OFF;
+        const int l = L & 63, i = l >> 3, j = l & 7;
+        double *junk = lds + LD::JUNK_OFF + L;
+        const bool wri = L < 64 && j == 0, wrj = L < 64 && i == 0;
+        // x_W: W = (W-1)+1 has the opposite parity of the first step
+        double x = eb[13 * W + (ODD ? i : j)];
+        if (L < 8) xb[13 * W + L] = eb[13 * W + L];
+        const int k1 = W - 2 > 0 ? W - 2 : 0;
+        double fa = Fm[64 * (W - 1) + l], ea = eb[13 * (W - 1) + (ODD ? j : i)];
+        double fb = Fm[64 * k1 + l], ebv = eb[13 * k1 + (ODD ? i : j)];
+        for (int k = W - 1; k >= 0; k -= 2) {
+            const int k2 = k - 2 > 0 ? k - 2 : 0, k3 = k - 3 > 0 ? k - 3 : 0;
+            const double f0 = fa, e0 = ea;
+            fa = Fm[64 * k2 + l];
+            ea = eb[13 * k2 + (ODD ? j : i)];
+            x = rstep<ODD>(f0, e0, x, ODD ? (wrj ? xb + 13 * k + j : junk) : (wri ? xb + 13 * k + i : junk));
+            if (k - 1 < 0) break;
+            const double f1 = fb, e1 = ebv;
+            fb = Fm[64 * k3 + l];
+            ebv = eb[13 * k3 + (ODD ? i : j)];
+            x = rstep<!ODD>(f1, e1, x, ODD ? (wri ? xb + 13 * (k - 1) + i : junk) : (wrj ? xb + 13 * (k - 1) + j : junk));
+        }
     }
 
     // v = rho z - y products of the general rows for the next rhs
@@ -481,6 +576,7 @@ struct WaveQP {
             rb[v] = r;
         }
         wv.sync();
+        IMPC_SEC(kSecRhs);
         // S1: t_k = r_k[:8] - G_{k-1}[:, 8:] r_{k-1}[8:]
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (!vok[s] || vr_[s] >= 8) continue;
@@ -493,20 +589,37 @@ struct WaveQP {
             tb[v] = t;
         }
         wv.sync();
-        // S2: forward 8-dim recursion (lanes 0..7; the others mirror lane L & 7)
+        IMPC_SEC(kSecS1);
+        // S2: forward 8-dim recursion a_{k+1} = t_{k+1} - F_k a_k on the 8x8 lane grid of each
+        // wavefront (lane l = 8i + j).  Vectors of even stages sit at index i, of odd stages at
+        // index j; F_k is stored as F_k[j][i] (k even) / F_k[i][j] (k odd), so even steps reduce
+        // over i (strided: DPP row_ror 8, permlane16/32 swaps) and odd steps over j (contiguous
+        // DPP), all in the VALU, with no transpose.  The next F and t are loaded one step ahead.
+        // Both wavefronts compute it; one lane per element of wavefront 0 writes, the rest write
+        // to discard slots (no divergent branch).
         {
-            const int i = L & 7;
-            double ai = tb[i];
-            if (L < 8) rb[i] = ai;
-            for (int k = 0; k < W; k++) {
-                double s = tb[13 * (k + 1) + i];
-                const double *Fk = Fm + 64 * k + 8 * i;
-                _Pragma("unroll") for (int j = 0; j < 8; j++) s -= Fk[j] * wv.bcast(ai, j);
-                ai = s;
-                if (L < 8) rb[13 * (k + 1) + i] = s;
+            const int l = L & 63, i = l >> 3, j = l & 7;
+            double *junk = lds + LD::JUNK_OFF + L;
+            const bool wri = L < 64 && j == 0, wrj = L < 64 && i == 0;
+            double a = tb[i];
+            if (L < 8) rb[L] = tb[L];
+            // (F, t) of the next even / odd step, loaded two steps ahead (reads past the last
+            // stage stay inside the LDS buffers and are never used)
+            double fe = Fm[l], te = tb[13 + j], fo = Fm[64 + l], to = tb[26 + i];
+            for (int k = 0; k < W; k += 2) {
+                const double f0 = fe, t0 = te;
+                fe = Fm[64 * (k + 2) + l];
+                te = tb[13 * (k + 3) + j];
+                a = rstep<true>(f0, t0, a, wrj ? rb + 13 * (k + 1) + j : junk);
+                if (k + 1 >= W) break;
+                const double f1 = fo, t1 = to;
+                fo = Fm[64 * (k + 3) + l];
+                to = tb[13 * (k + 4) + i];
+                a = rstep<false>(f1, t1, a, wri ? rb + 13 * (k + 2) + i : junk);
             }
         }
         wv.sync();
+        IMPC_SEC(kSecFwd);
         // S3: e_k = Ahat_k^{-1} rhat_k
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (!vok[s]) continue;
@@ -516,20 +629,15 @@ struct WaveQP {
             eb[NL * s + L] = e;
         }
         wv.sync();
-        // S4: backward 8-dim recursion x_k[:8] = e_k[:8] - F_k' x_{k+1}[:8]
-        {
-            const int i = L & 7;
-            double xi = eb[13 * W + i];
-            if (L < 8) xb[13 * W + i] = xi;
-            for (int k = W - 1; k >= 0; k--) {
-                double s = eb[13 * k + i];
-                const double *Fk = Fm + 64 * k + i;
-                _Pragma("unroll") for (int j = 0; j < 8; j++) s -= Fk[8 * j] * wv.bcast(xi, j);
-                xi = s;
-                if (L < 8) xb[13 * k + i] = s;
-            }
-        }
+        IMPC_SEC(kSecS3);
+        // S4: backward 8-dim recursion x_k[:8] = e_k[:8] - F_k' x_{k+1}[:8] on the same grid and
+        // stored layout: even steps reduce over j (contiguous), odd steps over i (strided).
+        if ((W - 1) & 1)
+            bwd_sweep<true>(eb, xb, W);
+        else
+            bwd_sweep<false>(eb, xb, W);
         wv.sync();
+        IMPC_SEC(kSecBwd);
         // S5: controls x_k[8:] = e_k[8:] - G_k[:, 8:]' x_{k+1}[:8]
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (!vok[s] || vr_[s] < 8) continue;
@@ -539,6 +647,7 @@ struct WaveQP {
             xb[NL * s + L] = t;
         }
         wv.sync();
+        IMPC_SEC(kSecS5);
         // update_x and the box rows (update_z / project / update_y)
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (!vok[s]) continue;
@@ -567,7 +676,9 @@ struct WaveQP {
             z[s] = zn;
         }
         wv.sync();
+        IMPC_SEC(kSecUpdate);
         write_v_products();
+        IMPC_SEC(kSecProducts);
         (void)n;
     }
 
@@ -825,6 +936,7 @@ struct WaveQP {
     // not occupy registers across the ADMM loop.
     IMPC_WF void solve(int64_t b) {
         const int n = T.n, m = T.m;
+        IMPC_SEC_START();
         clear_exchange();
         load(b);
         {
@@ -832,7 +944,9 @@ struct WaveQP {
             scale(b, D, Eb, Eg);
         }
         set_rho(dmin(dmax(st.rho, kRhoMin), kRhoMax));
+        IMPC_SEC(kSecSetup);
         int bad = factorize();
+        IMPC_SEC(kSecFactor);
         impc_info *out = io.info + b;
         if (bad) {
             _Pragma("unroll") for (int s = 0; s < VS; s++)
@@ -889,6 +1003,7 @@ struct WaveQP {
             clear_exchange();
         }
         write_v_products();
+        IMPC_SEC(kSecWarm);
 
         int64_t status = IMPC_UNSOLVED, rho_updates = 0, iter;
         double obj = 0.0, rho_est = R.rho;
@@ -912,12 +1027,14 @@ struct WaveQP {
             }
             can_check = chk && (iter % chk == 0);
             if (can_check) {
+                IMPC_SEC_START();
                 double D[VS], Eb[VS], Eg[GS];
                 load_scal(b, D, Eb, Eg);
                 update_info(inf, D, Eb, Eg);
                 info_iter = iter;
                 int done = check_termination(inf, 0, status, obj, D, Eb, Eg);
                 write_v_products();
+                IMPC_SEC(kSecChecks);
                 if (done) break;
             }
             if (st.adaptive_rho && st.rho_interval && (iter % st.rho_interval == 0)) {
@@ -931,13 +1048,16 @@ struct WaveQP {
                 double rn = rho_estimate(inf);
                 rho_est = rn;
                 if ((rn > R.rho * st.adaptive_rho_tolerance) || (rn < R.rho / st.adaptive_rho_tolerance)) {
+                    IMPC_SEC(kSecChecks);
                     set_rho(dmin(dmax(rn, kRhoMin), kRhoMax));
                     factorize();
                     write_v_products();
+                    IMPC_SEC(kSecFactor);
                     rho_updates += 1;
                 }
             }
         }
+        IMPC_SEC_START();
         double D[VS], Eb[VS], Eg[GS];
         load_scal(b, D, Eb, Eg);
         if (time_limited || !can_check) {
@@ -988,6 +1108,13 @@ struct WaveQP {
             out->rho_estimate = rho_est;
         }
         wv.sync();
+#if defined(IMPC_SECTION_PROF) && defined(__HIP_DEVICE_COMPILE__)
+        IMPC_SEC(kSecOutput);
+        if (L == 0 && io.sec) {
+            sec_acc[kSecIters] = (uint64_t)info_iter;
+            _Pragma("unroll") for (int i = 0; i < kSecCount; i++) atomicAdd(io.sec + i, (unsigned long long)sec_acc[i]);
+        }
+#endif
     }
 };
 

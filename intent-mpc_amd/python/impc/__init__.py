@@ -12,6 +12,8 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _PKG = os.path.dirname(os.path.dirname(_HERE))  # .../intent-mpc_amd
 LIB_PATH = os.path.join(_PKG, "lib", "libimpc_qp.so")
+if os.environ.get("IMPC_SECTION_PROF") == "1":  # profiling variant (tools/section_profile.py only)
+    LIB_PATH = os.path.join(_PKG, "lib", "libimpc_qp_prof.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"libimpc_qp.so not built at {LIB_PATH} (run __graft_entry__.build() or `make lib`)")

@@ -38,6 +38,21 @@ struct EmuWave {
         sync();
         return b[(l & ~63) + src];
     }
+    double shfl(double v, int src) { return bcast(v, src); }
+    double sum_contig8(double v) {  // the GPU's DPP order: ((v0+v1)+(v2+v3)) + ((v4+v5)+(v6+v7))
+        double *b = next_buf();
+        b[l] = v;
+        sync();
+        const double *g = b + (l & ~7);
+        return ((g[0] + g[1]) + (g[2] + g[3])) + ((g[4] + g[5]) + (g[6] + g[7]));
+    }
+    double sum_stride8(double v) {  // same shape over lanes j, j+8, .., j+56 of the wavefront
+        double *b = next_buf();
+        b[l] = v;
+        sync();
+        const double *g = b + (l & ~63) + (l & 7);
+        return ((g[0] + g[8]) + (g[16] + g[24])) + ((g[32] + g[40]) + (g[48] + g[56]));
+    }
     double max(double v) {
         double *b = next_buf();
         b[l] = v;
@@ -74,6 +89,7 @@ void run(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSetti
     for (int l = 0; l < NL; l++)
         th.emplace_back([&, l] {
             EmuWave wv{l, &sh};
+            impc::WaveQP<EmuWave, NL, VS, GS>::load_tables(wv, T, lds.data());
             for (int64_t b = 0; b < io.B; b++) {
                 impc::WaveQP<EmuWave, NL, VS, GS> qp(wv, T, io, st, lds.data());
                 qp.solve(b);

@@ -62,3 +62,10 @@ def test_structured_emulation_matches_oracle():
     cfg = take(CFG["config3_K9"], 1)
     s = impc.default_settings(**S25)
     compare(emulate(cfg, s), oracle(cfg, s))
+
+
+def test_structured_emulation_odd_stage_count():
+    """N=19 (W-1 odd) takes the other parity of the backward sweep (mpc_wave.hpp bwd_sweep)."""
+    cfg = scenarios.static_config(N=19, K=4, batch=1, identical=False, seed=1919)
+    s = impc.default_settings(**S25)
+    compare(emulate(cfg, s), oracle(cfg, s))
