@@ -12,7 +12,10 @@ LIBDIR  := $(ROOT)/intent-mpc_amd/lib
 ORADIR  := $(ROOT)/oracle/build
 HARNDIR := $(ROOT)/tests/native/build
 
-HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
+# -fno-unroll-loops: the structured kernel's runtime-bound loops (stage recursions, gathers,
+# Cholesky) are unrolled by hand where it pays; compiler unrolling of the rest only raises
+# register pressure past the 2-waves-per-SIMD budget (measured).
+HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -fno-unroll-loops
 HOSTFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -Wall
 
 LIB     := $(LIBDIR)/libimpc_qp.so
@@ -20,12 +23,13 @@ PROFLIB := $(LIBDIR)/libimpc_qp_prof.so
 ORACLE  := $(ORADIR)/libosqp_oracle.so
 HARNESS := $(HARNDIR)/libimpc_core_cpu.so
 EMU     := $(HARNDIR)/libwave_emu.so
+SHIMT   := $(HARNDIR)/shim_test
 
 .PHONY: all lib oracle harness prof clean
 all: lib oracle harness
 lib: $(LIB)
 oracle: $(ORACLE)
-harness: $(HARNESS) $(EMU)
+harness: $(HARNESS) $(EMU) $(SHIMT)
 
 $(LIBDIR)/impc_qp.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symbolic.hpp $(CSRC)/mpc_wave.hpp \
 		$(CSRC)/mpc_structure.hpp $(ROOT)/include/impc_qp.h
@@ -70,6 +74,12 @@ $(EMU): $(ROOT)/tests/native/wave_emu.cpp $(CSRC)/mpc_wave.hpp $(CSRC)/admm_core
 	@mkdir -p $(HARNDIR)
 	$(HIPCC) -x hip --offload-host-only -std=c++20 -O2 -fPIC -shared -ffp-contract=off \
 		$(ROOT)/tests/native/wave_emu.cpp -x c++ $(CSRC)/mpc_structure.cpp -o $@
+
+# OsqpEigen shim driver (test-only Eigen stand-in; links the product library)
+$(SHIMT): $(ROOT)/tests/native/shim_test.cpp $(ROOT)/include/OsqpEigen/OsqpEigen.h $(LIB)
+	@mkdir -p $(HARNDIR)
+	$(CXX) -O2 -std=c++17 -Wall -I$(ROOT)/tests/native/mock_eigen -I$(ROOT)/include $< -L$(LIBDIR) -limpc_qp \
+		-Wl,-rpath,'$$ORIGIN/../../../intent-mpc_amd/lib' -o $@
 
 clean:
 	rm -rf $(LIBDIR) $(ORADIR) $(HARNDIR)

@@ -1,0 +1,368 @@
+/*
+ * OsqpEigen/OsqpEigen.h -- OsqpEigen-compatible C++ front end of libimpc_qp.so (header only).
+ *
+ * Lets the reference's caller compile unchanged against the MI355X solver: mpcPlanner.h includes
+ * <trajectory_planner/third_party/OsqpEigen/OsqpEigen.h> (reference mpcPlanner.h:22); pointing that
+ * include at this header keeps every call in mpcPlanner::solveTraj
+ * (mpcPlanner.cpp:436-527) as it is.  Mirrors the OsqpEigen 0.7 surface the reference uses:
+ *
+ *   OsqpEigen::Settings  (Settings.hpp:25-202)  setVerbosity, setWarmStart, setTimeLimit, ... ->
+ *                                               impc_settings (OSQPSettings mirror)
+ *   OsqpEigen::Data      (Data.hpp:44-151)      setNumberOf*, setHessianMatrix (upper triangle,
+ *                                               Data.tpp:38), setGradient, setLinearConstraints-
+ *                                               Matrix, setLower/UpperBound
+ *   OsqpEigen::Solver    (Solver.hpp:87-249)    initSolver, setWarmStart, solveProblem, getStatus,
+ *                                               getSolution, getDualSolution, clearSolver,
+ *                                               updateGradient / updateLower|UpperBound / updateBounds
+ *   Status / ErrorExitFlag values               (Constants.hpp:14-56, OSQP constants.h:18-51)
+ *
+ * Each Solver owns a one-QP batch on a process-wide context (device IMPC_DEVICE, default 0); the
+ * context belongs to the thread that first initialises a solver (the reference's single mpc
+ * worker thread, mpcNavigation.cpp:177-178).  Differences from OsqpEigen, all benign for the
+ * reference's call pattern: Data copies vectors when they are set (OsqpEigen keeps the caller's
+ * pointer until initSolver); osqp_setup's numeric work runs on the device at the first solve, so
+ * a non-convex P surfaces as ErrorExitFlag::NonCvxError from solveProblem instead of a failed
+ * initSolver; the update* calls on a stage-structured pattern re-run setup on the device and
+ * warm-start from the last solution (the generic kernel keeps OSQP's factor reuse).
+ *
+ * Requires Eigen's <Eigen/Dense> and <Eigen/Sparse> (the reference's own dependency) and
+ * linking against intent-mpc_amd/lib/libimpc_qp.so.
+ */
+#ifndef IMPC_OSQPEIGEN_SHIM_H
+#define IMPC_OSQPEIGEN_SHIM_H
+
+#include <Eigen/Dense>
+#include <Eigen/Sparse>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <memory>
+#include <utility>
+#include <vector>
+
+#include "../impc_qp.h"
+
+namespace OsqpEigen {
+
+constexpr double INFTY = 1e30; /* OSQP_INFTY */
+
+enum class Status : int {
+    DualInfeasibleInaccurate = IMPC_DUAL_INFEASIBLE_INACCURATE,
+    PrimalInfeasibleInaccurate = IMPC_PRIMAL_INFEASIBLE_INACCURATE,
+    SolvedInaccurate = IMPC_SOLVED_INACCURATE,
+    Solved = IMPC_SOLVED,
+    MaxIterReached = IMPC_MAX_ITER_REACHED,
+    PrimalInfeasible = IMPC_PRIMAL_INFEASIBLE,
+    DualInfeasible = IMPC_DUAL_INFEASIBLE,
+    Sigint = -5,
+    TimeLimitReached = IMPC_TIME_LIMIT_REACHED,
+    NonCvx = IMPC_NON_CVX,
+    Unsolved = IMPC_UNSOLVED
+};
+
+enum class ErrorExitFlag : int {
+    NoError = 0,
+    DataValidationError = IMPC_DATA_VALIDATION_ERROR,
+    SettingsValidationError = IMPC_SETTINGS_VALIDATION_ERROR,
+    LinsysSolverLoadError = 3,
+    LinsysSolverInitError = IMPC_LINSYS_SOLVER_INIT_ERROR,
+    NonCvxError = IMPC_NONCVX_ERROR,
+    MemAllocError = IMPC_MEM_ALLOC_ERROR,
+    WorkspaceNotInitError = IMPC_WORKSPACE_NOT_INIT_ERROR
+};
+
+namespace detail {
+
+inline void debug(const char *what) { std::fprintf(stderr, "[OsqpEigen/impc] %s\n", what); }
+
+inline void debug_impc(const char *what, int rc) {
+    std::fprintf(stderr, "[OsqpEigen/impc] %s failed (%d): %s\n", what, rc, impc_last_error());
+}
+
+/* Process-wide context, created on first use. */
+inline impc_ctx context() {
+    static impc_ctx ctx = [] {
+        impc_ctx c = nullptr;
+        const char *dev = std::getenv("IMPC_DEVICE");
+        int rc = impc_ctx_create(dev ? std::atoi(dev) : 0, &c);
+        if (rc) debug_impc("impc_ctx_create", rc);
+        return rc ? nullptr : c;
+    }();
+    return ctx;
+}
+
+/* CSC copy of an Eigen sparse matrix (stored entries, explicit zeros kept, rows sorted), optionally
+ * only the upper triangle (OsqpEigen Data.tpp:38, SparseMatrixHelper.tpp:11-58). */
+template <typename Derived>
+void to_csc(const Derived &M, bool upper, std::vector<int64_t> &p, std::vector<int64_t> &i, std::vector<double> &x) {
+    const int64_t cols = (int64_t)M.cols();
+    std::vector<std::vector<std::pair<int64_t, double>>> colv((size_t)cols);
+    for (int64_t k = 0; k < (int64_t)M.outerSize(); ++k)
+        for (typename Derived::InnerIterator it(M, k); it; ++it) {
+            const int64_t r = (int64_t)it.row(), c = (int64_t)it.col();
+            if (upper && r > c) continue;
+            colv[(size_t)c].emplace_back(r, (double)it.value());
+        }
+    p.assign(1, 0);
+    i.clear();
+    x.clear();
+    for (auto &cv : colv) {
+        std::sort(cv.begin(), cv.end(), [](const std::pair<int64_t, double> &a, const std::pair<int64_t, double> &b) {
+            return a.first < b.first;
+        });
+        for (auto &e : cv) {
+            i.push_back(e.first);
+            x.push_back(e.second);
+        }
+        p.push_back((int64_t)i.size());
+    }
+}
+
+template <typename V>
+bool copy_vec(const V &v, int64_t n, std::vector<double> &out) {
+    if ((int64_t)v.size() != n) return false;
+    out.resize((size_t)n);
+    for (int64_t k = 0; k < n; ++k) out[(size_t)k] = (double)v((int)k);
+    return true;
+}
+
+}  // namespace detail
+
+class Settings {
+    impc_settings m_s;
+
+public:
+    Settings() { resetDefaultSettings(); }
+    void resetDefaultSettings() { impc_default_settings(&m_s); }
+    void setRho(const double v) { m_s.rho = v; }
+    void setSigma(const double v) { m_s.sigma = v; }
+    void setScaling(const int v) { m_s.scaling = v; }
+    void setAdaptiveRho(const bool v) { m_s.adaptive_rho = v ? 1 : 0; }
+    void setAdaptiveRhoInterval(const int v) { m_s.adaptive_rho_interval = v; }
+    void setAdaptiveRhoTolerance(const double v) { m_s.adaptive_rho_tolerance = v; }
+    void setAdaptiveRhoFraction(const double v) { m_s.adaptive_rho_fraction = v; }
+    void setMaxIteration(const int v) { m_s.max_iter = v; }
+    void setMaxIteraction(const int v) { m_s.max_iter = v; }
+    void setAbsoluteTolerance(const double v) { m_s.eps_abs = v; }
+    void setRelativeTolerance(const double v) { m_s.eps_rel = v; }
+    void setPrimalInfeasibilityTolerance(const double v) { m_s.eps_prim_inf = v; }
+    void setPrimalInfeasibilityTollerance(const double v) { m_s.eps_prim_inf = v; }
+    void setDualInfeasibilityTolerance(const double v) { m_s.eps_dual_inf = v; }
+    void setDualInfeasibilityTollerance(const double v) { m_s.eps_dual_inf = v; }
+    void setAlpha(const double v) { m_s.alpha = v; }
+    void setLinearSystemSolver(const int v) { m_s.linsys_solver = v; }
+    void setDelta(const double v) { m_s.delta = v; }
+    void setPolish(const bool v) { m_s.polish = v ? 1 : 0; }
+    void setPolishRefineIter(const int v) { m_s.polish_refine_iter = v; }
+    void setVerbosity(const bool v) { m_s.verbose = v ? 1 : 0; }
+    void setScaledTerimination(const bool v) { m_s.scaled_termination = v ? 1 : 0; }
+    void setCheckTermination(const int v) { m_s.check_termination = v; }
+    void setWarmStart(const bool v) { m_s.warm_start = v ? 1 : 0; }
+    void setTimeLimit(const double v) { m_s.time_limit = v; }
+    const impc_settings &getSettings() const { return m_s; }
+};
+
+class Data {
+    int64_t m_n = 0, m_m = 0;
+    bool m_hasP = false, m_hasA = false, m_hasq = false, m_hasl = false, m_hasu = false;
+
+public:
+    std::vector<int64_t> Pp, Pi, Ap, Ai;
+    std::vector<double> Px, Ax, q, l, u;
+
+    Data() = default;
+    Data(int n, int m) : m_n(n), m_m(m) {}
+    void setNumberOfVariables(int n) { m_n = n; }
+    void setNumberOfConstraints(int m) { m_m = m; }
+    int64_t numberOfVariables() const { return m_n; }
+    int64_t numberOfConstraints() const { return m_m; }
+    void clearHessianMatrix() { m_hasP = false; Pp.clear(); Pi.clear(); Px.clear(); }
+    void clearLinearConstraintsMatrix() { m_hasA = false; Ap.clear(); Ai.clear(); Ax.clear(); }
+
+    template <typename Derived>
+    bool setHessianMatrix(const Derived &H) {
+        if (m_hasP) { detail::debug("the Hessian matrix was already set"); return false; }
+        if ((int64_t)H.rows() != m_n || (int64_t)H.cols() != m_n) { detail::debug("the Hessian matrix has to be n x n"); return false; }
+        detail::to_csc(H, true, Pp, Pi, Px);
+        return m_hasP = true;
+    }
+    template <typename Derived>
+    bool setLinearConstraintsMatrix(const Derived &A) {
+        if (m_hasA) { detail::debug("the constraint matrix was already set"); return false; }
+        if ((int64_t)A.rows() != m_m || (int64_t)A.cols() != m_n) { detail::debug("the constraint matrix has to be m x n"); return false; }
+        detail::to_csc(A, false, Ap, Ai, Ax);
+        return m_hasA = true;
+    }
+    template <typename V>
+    bool setGradient(const V &g) {
+        if (!detail::copy_vec(g, m_n, q)) { detail::debug("the gradient has to be n x 1"); return false; }
+        return m_hasq = true;
+    }
+    template <typename V>
+    bool setLowerBound(const V &lb) {
+        if (!detail::copy_vec(lb, m_m, l)) { detail::debug("the lower bound has to be m x 1"); return false; }
+        return m_hasl = true;
+    }
+    template <typename V>
+    bool setUpperBound(const V &ub) {
+        if (!detail::copy_vec(ub, m_m, u)) { detail::debug("the upper bound has to be m x 1"); return false; }
+        return m_hasu = true;
+    }
+    bool isSet() const { return m_n > 0 && m_hasP && m_hasA && m_hasq && m_hasl && m_hasu; }
+};
+
+class Solver {
+    std::unique_ptr<Settings> m_settings;
+    std::unique_ptr<Data> m_data;
+    impc_batch m_batch = nullptr;
+    bool m_solved = false;
+    impc_info m_info{};
+    Eigen::Matrix<double, Eigen::Dynamic, 1> m_x, m_y;
+
+    bool structured() const {
+        impc_batch_stats st{};
+        return m_batch && impc_batch_get_stats(m_batch, &st) == IMPC_OK && st.kernel == IMPC_KERNEL_STRUCTURED;
+    }
+    // restart a structured batch from the current data, warm-started from the last solution
+    bool resetup_from_data() {
+        const Data &d = *m_data;
+        int rc = impc_batch_set_values(m_batch, d.Px.data(), d.q.data(), d.Ax.data(), d.l.data(), d.u.data());
+        if (rc) { detail::debug_impc("impc_batch_set_values", rc); return false; }
+        if (m_solved) {
+            std::vector<double> x((size_t)d.numberOfVariables()), y((size_t)d.numberOfConstraints());
+            for (size_t k = 0; k < x.size(); ++k) x[k] = m_x((int)k);
+            for (size_t k = 0; k < y.size(); ++k) y[k] = m_y((int)k);
+            rc = impc_batch_warm_start(m_batch, x.data(), y.data());
+            if (rc) { detail::debug_impc("impc_batch_warm_start", rc); return false; }
+        }
+        return true;
+    }
+
+public:
+    Solver() : m_settings(new Settings()), m_data(new Data()) {}
+    ~Solver() { clearSolver(); }
+    Solver(const Solver &) = delete;
+    Solver &operator=(const Solver &) = delete;
+
+    const std::unique_ptr<Settings> &settings() const { return m_settings; }
+    const std::unique_ptr<Data> &data() const { return m_data; }
+
+    bool isInitialized() { return m_batch != nullptr; }
+
+    bool initSolver() {
+        if (m_batch) { detail::debug("the solver is already initialized"); return false; }
+        if (!m_data->isSet()) { detail::debug("some data are not set"); return false; }
+        impc_ctx ctx = detail::context();
+        if (!ctx) return false;
+        const Data &d = *m_data;
+        int rc = impc_batch_create(ctx, d.numberOfVariables(), d.numberOfConstraints(), d.Pp.data(), d.Pi.data(),
+                                   d.Ap.data(), d.Ai.data(), 1, &m_batch);
+        if (rc) { detail::debug_impc("impc_batch_create", rc); m_batch = nullptr; return false; }
+        rc = impc_batch_set_settings(m_batch, &m_settings->getSettings());
+        if (!rc) rc = impc_batch_set_values(m_batch, d.Px.data(), d.q.data(), d.Ax.data(), d.l.data(), d.u.data());
+        if (rc) {
+            detail::debug_impc("osqp_setup equivalent", rc);
+            impc_batch_destroy(m_batch);
+            m_batch = nullptr;
+            return false;
+        }
+        m_x.setZero(d.numberOfVariables());
+        m_y.setZero(d.numberOfConstraints());
+        m_solved = false;
+        return true;
+    }
+
+    void clearSolver() {
+        if (m_batch) impc_batch_destroy(m_batch);
+        m_batch = nullptr;
+        m_solved = false;
+    }
+
+    bool clearSolverVariables() {
+        if (!m_batch) return false;
+        return impc_batch_warm_start(m_batch, nullptr, nullptr) == IMPC_OK;
+    }
+
+    template <typename X, typename Y>
+    bool setWarmStart(const X &primalVariable, const Y &dualVariable) {
+        if (!m_batch) { detail::debug("the solver is not initialized"); return false; }
+        std::vector<double> x, y;
+        if (!detail::copy_vec(primalVariable, m_data->numberOfVariables(), x) ||
+            !detail::copy_vec(dualVariable, m_data->numberOfConstraints(), y)) {
+            detail::debug("warm start has the wrong size");
+            return false;
+        }
+        int rc = impc_batch_warm_start(m_batch, x.data(), y.data());
+        if (rc) { detail::debug_impc("impc_batch_warm_start", rc); return false; }
+        return true;
+    }
+
+    template <typename X>
+    bool setPrimalVariable(const X &primalVariable) {
+        Eigen::Matrix<double, Eigen::Dynamic, 1> y;
+        y.setZero(m_data->numberOfConstraints());
+        return setWarmStart(primalVariable, y);
+    }
+
+    ErrorExitFlag solveProblem() {
+        if (!m_batch) return ErrorExitFlag::WorkspaceNotInitError;
+        int rc = impc_batch_set_settings(m_batch, &m_settings->getSettings());
+        if (!rc) rc = impc_batch_solve(m_batch, nullptr);
+        if (rc) {
+            detail::debug_impc("impc_batch_solve", rc);
+            return rc == IMPC_SETTINGS_VALIDATION_ERROR || rc == IMPC_UNSUPPORTED ? ErrorExitFlag::SettingsValidationError
+                                                                                   : ErrorExitFlag::WorkspaceNotInitError;
+        }
+        std::vector<double> x((size_t)m_data->numberOfVariables()), y((size_t)m_data->numberOfConstraints());
+        rc = impc_batch_get(m_batch, x.data(), y.data(), &m_info);
+        if (rc) { detail::debug_impc("impc_batch_get", rc); return ErrorExitFlag::WorkspaceNotInitError; }
+        for (size_t k = 0; k < x.size(); ++k) m_x((int)k) = x[k];
+        for (size_t k = 0; k < y.size(); ++k) m_y((int)k) = y[k];
+        m_solved = true;
+        if (m_info.setup_exitflag == IMPC_NONCVX_ERROR) return ErrorExitFlag::NonCvxError;
+        return ErrorExitFlag::NoError;
+    }
+
+    /* deprecated OsqpEigen API: true when solved to full accuracy */
+    bool solve() { return solveProblem() == ErrorExitFlag::NoError && getStatus() == Status::Solved; }
+
+    Status getStatus() const { return m_solved ? (Status)m_info.status_val : Status::Unsolved; }
+    const Eigen::Matrix<double, Eigen::Dynamic, 1> &getSolution() { return m_x; }
+    const Eigen::Matrix<double, Eigen::Dynamic, 1> &getDualSolution() { return m_y; }
+    double getObjValue() const { return m_info.obj_val; }
+    int64_t getIterations() const { return m_info.iter; }
+
+    template <typename V>
+    bool updateGradient(const V &gradient) {
+        if (!m_batch) return false;
+        if (!detail::copy_vec(gradient, m_data->numberOfVariables(), m_data->q)) return false;
+        if (structured()) return resetup_from_data();
+        return impc_batch_update_lin_cost(m_batch, m_data->q.data()) == IMPC_OK;
+    }
+    template <typename L, typename U>
+    bool updateBounds(const L &lowerBound, const U &upperBound) {
+        if (!m_batch) return false;
+        const int64_t m = m_data->numberOfConstraints();
+        if (!detail::copy_vec(lowerBound, m, m_data->l) || !detail::copy_vec(upperBound, m, m_data->u)) return false;
+        if (structured()) return resetup_from_data();
+        return impc_batch_update_bounds(m_batch, m_data->l.data(), m_data->u.data()) == IMPC_OK;
+    }
+    template <typename L>
+    bool updateLowerBound(const L &lowerBound) {
+        Eigen::Matrix<double, Eigen::Dynamic, 1> u((int)m_data->numberOfConstraints());
+        for (int64_t k = 0; k < m_data->numberOfConstraints(); ++k) u((int)k) = m_data->u[(size_t)k];
+        return updateBounds(lowerBound, u);
+    }
+    template <typename U>
+    bool updateUpperBound(const U &upperBound) {
+        Eigen::Matrix<double, Eigen::Dynamic, 1> l((int)m_data->numberOfConstraints());
+        for (int64_t k = 0; k < m_data->numberOfConstraints(); ++k) l((int)k) = m_data->l[(size_t)k];
+        return updateBounds(l, upperBound);
+    }
+};
+
+}  // namespace OsqpEigen
+
+#endif

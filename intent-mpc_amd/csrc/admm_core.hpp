@@ -595,10 +595,11 @@ IMPC_HD void qp_solve(const DevSym &sy, const DevWork &wk, const DevSettings &st
             IMPC_AT(wk.y, i) = yi;
             IMPC_AT(wk.v, i) = ri * zn - yi;
         }
+        // osqp_solve (PROFILING build): after the ADMM steps, before can_check is recomputed, so
+        // can_check keeps the previous iteration's value when the limit fires
         if (st.time_limit > 0 &&
             (double)(device_clock_100mhz() - t0) * 1e-8 >= st.time_limit) {
-            status = -6;  // OSQP_TIME_LIMIT_REACHED: leave the loop, then the approximate check
-            can_check = 0;
+            status = IMPC_TIME_LIMIT_REACHED;
             break;
         }
         can_check = chk && (iter % chk == 0);
@@ -617,12 +618,8 @@ IMPC_HD void qp_solve(const DevSym &sy, const DevWork &wk, const DevSettings &st
             }
         }
     }
-    const bool time_limited = status == -6;
-    if (time_limited) {
-        update_info(sy, wk, st, inf, iter, cinv, lane);
-        status = IMPC_UNSOLVED;
-        check_termination(sy, wk, st, inf, 0, c, status, obj, lane);
-    } else if (!can_check) {
+    // post-loop update_info / check (may turn TIME_LIMIT_REACHED into SOLVED), as osqp_solve
+    if (!can_check) {
         update_info(sy, wk, st, inf, iter - 1, cinv, lane);
         check_termination(sy, wk, st, inf, 0, c, status, obj, lane);
     }
@@ -645,8 +642,7 @@ IMPC_HD void qp_solve(const DevSym &sy, const DevWork &wk, const DevSettings &st
         if (scaled) obj *= cinv;
     }
     if (status == IMPC_UNSOLVED) {
-        if (!check_termination(sy, wk, st, inf, 1, c, status, obj, lane))
-            status = time_limited ? IMPC_TIME_LIMIT_REACHED : IMPC_MAX_ITER_REACHED;
+        if (!check_termination(sy, wk, st, inf, 1, c, status, obj, lane)) status = IMPC_MAX_ITER_REACHED;
     }
     rho_est = rho_estimate(inf, rho);
     const bool has_sol2 = status != IMPC_PRIMAL_INFEASIBLE && status != IMPC_PRIMAL_INFEASIBLE_INACCURATE &&

@@ -45,8 +45,18 @@ int fail(int code, const std::string &msg) {
 
 constexpr int kBlock = 64;  // generic path: one wavefront per workgroup, one QP per lane
 constexpr int kTile = 64;   // transpose tile edge
-constexpr int kTeam = 128;   // structured path: lanes per QP (two wavefronts)
-constexpr int kWaveVS = 2;  // variable slots per lane (n <= 256)
+// structured path team shape (compile-time; see DESIGN.md for the measured choice)
+#ifndef IMPC_TEAM
+#define IMPC_TEAM 256
+#endif
+#ifndef IMPC_VS
+#define IMPC_VS 1
+#endif
+#ifndef IMPC_WAVES_PER_SIMD
+#define IMPC_WAVES_PER_SIMD 2
+#endif
+constexpr int kTeam = IMPC_TEAM;   // lanes per QP (IMPC_TEAM / 64 wavefronts)
+constexpr int kWaveVS = IMPC_VS;   // variable slots per lane (n <= kTeam * kWaveVS)
 
 // ------------------------------------------------------------------ layout transposes
 // dst[e * S + b] = src[b * len + e]; 64x64 tile through LDS so both sides are coalesced.
@@ -243,7 +253,7 @@ struct GpuTeam {
 };
 
 template <int NL, int VS, int GS>
-__global__ __launch_bounds__(NL, 1) void k_mpc_wave(impc::WaveTables T, impc::WaveIO io, impc::DevSettings st,
+__global__ __launch_bounds__(NL, IMPC_WAVES_PER_SIMD) void k_mpc_wave(impc::WaveTables T, impc::WaveIO io, impc::DevSettings st,
                                                     unsigned *counter) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     using LD = impc::WaveLds<NL, VS, GS>;

@@ -62,14 +62,18 @@ enum {
     kSecSetup, kSecFactor, kSecWarm, kSecRhs, kSecS1, kSecFwd, kSecS3, kSecBwd, kSecS5, kSecUpdate, kSecProducts,
     kSecChecks, kSecOutput, kSecIters = 15, kSecCount = 16
 };
+// The clock is the 20-bit SHADER_CYCLES hardware register (s_getreg, no memory counter
+// involved: an s_memtime SMEM read shares lgkmcnt with the LDS traffic it would be measuring);
+// deltas are taken modulo 2^20, so a section must stay under ~1M cycles.
 #if defined(IMPC_SECTION_PROF) && defined(__HIP_DEVICE_COMPILE__)
-#define IMPC_SEC(X)                                    \
-    do {                                               \
-        uint64_t t_ = __builtin_amdgcn_s_memtime();    \
-        sec_acc[X] += t_ - sec_t0;                     \
-        sec_t0 = t_;                                   \
+#define IMPC_SEC_CLOCK() ((uint32_t)__builtin_amdgcn_s_getreg(29 | (0 << 6) | (19 << 11)))
+#define IMPC_SEC(X)                                          \
+    do {                                                     \
+        uint32_t t_ = IMPC_SEC_CLOCK();                      \
+        sec_acc[X] += (uint64_t)((t_ - sec_t0) & 0xFFFFFu);  \
+        sec_t0 = t_;                                         \
     } while (0)
-#define IMPC_SEC_START() (sec_t0 = __builtin_amdgcn_s_memtime())
+#define IMPC_SEC_START() (sec_t0 = IMPC_SEC_CLOCK())
 #else
 #define IMPC_SEC(X) ((void)0)
 #define IMPC_SEC_START() ((void)0)
@@ -80,7 +84,8 @@ template <int NL, int VS, int GS>
 struct WaveLds {
     static constexpr int NMAX = NL * VS;
     static constexpr int WMAX = (NMAX + 5) / 13 - 1;       // max control stages
-    static constexpr int NP = NMAX + 192;                   // exchange vector length (zero tail)
+    // exchange vector length: zero tail past NMAX, and room for the factorisation scratch
+    static constexpr int NP = (NMAX + 192 > (779 + NL * GS + NMAX + 3) / 4) ? NMAX + 192 : (779 + NL * GS + NMAX + 3) / 4;
     static constexpr int F_OFF = 0;                         // [WMAX][64]
     static constexpr int R_OFF = F_OFF + WMAX * 64;         // rbuf
     static constexpr int T_OFF = R_OFF + NP;                // tbuf
@@ -160,7 +165,8 @@ struct WaveQP {
     WaveRho R;
     double c = 1.0, cinv = 1.0;
 #if defined(IMPC_SECTION_PROF) && defined(__HIP_DEVICE_COMPILE__)
-    uint64_t sec_t0 = 0, sec_acc[kSecCount] = {};
+    uint32_t sec_t0 = 0;
+    uint64_t sec_acc[kSecCount] = {};
 #endif
 
     IMPC_WF WaveQP(WV &w, const WaveTables &t, const WaveIO &i, const DevSettings &s, double *l)
@@ -261,10 +267,8 @@ struct WaveQP {
         for (int t = 0; t < CG4; t += 4) {
             const int i0 = cg[t * LD::NMAX], i1 = cg[(t + 1) * LD::NMAX], i2 = cg[(t + 2) * LD::NMAX],
                       i3 = cg[(t + 3) * LD::NMAX];
-            s += pb[i0];
-            s += pb[i1];
-            s += pb[i2];
-            s += pb[i3];
+            const double p0 = pb[i0], p1 = pb[i1], p2 = pb[i2], p3 = pb[i3];
+            s += (p0 + p1) + (p2 + p3);
         }
         return s;
     }
@@ -503,7 +507,7 @@ struct WaveQP {
         _Pragma("unroll") for (int s = 0; s < VS; s++)
             if (vok[s] && vs_[s] == 0 && vr_[s] < 8)
                 _Pragma("unroll") for (int j = 0; j < 8; j++) cp[s][j] = 0.0;
-        bad = (int)wv.bcast((double)bad, 0);
+        bad = (int)wv.max((double)bad);  // set by lane 0 only: team-wide, so every wavefront agrees
         clear_exchange();
         (void)n;
         return bad;
@@ -1005,27 +1009,33 @@ struct WaveQP {
         write_v_products();
         IMPC_SEC(kSecWarm);
 
-        int64_t status = IMPC_UNSOLVED, rho_updates = 0, iter;
+        int64_t status = IMPC_UNSOLVED, rho_updates = 0;
+        int32_t iter;
         double obj = 0.0, rho_est = R.rho;
         Info inf{};
         int64_t info_iter = 0;
         const int chk = st.check_termination;
         int can_check = 0;
         const uint64_t t0 = device_clock_100mhz();
-        bool time_limited = false;
+        // countdowns instead of iter % interval (no integer division in the loop)
+        int32_t chk_left = chk, rho_left = st.rho_interval;
         for (iter = 1; iter <= st.max_iter; iter++) {
-            const bool need_delta = (chk && iter % chk == 0) || iter == st.max_iter || st.time_limit > 0;
+            const bool chk_now = chk && --chk_left == 0;
+            if (chk_now) chk_left = chk;
+            const bool rho_now = st.adaptive_rho && st.rho_interval && --rho_left == 0;
+            if (rho_now) rho_left = st.rho_interval;
+            const bool need_delta = chk_now || iter == st.max_iter || st.time_limit > 0;
             iterate(need_delta);
+            // osqp_solve (PROFILING build): checked after the ADMM steps, before can_check is
+            // recomputed (so it keeps the previous iteration's value); one team-wide decision
             if (st.time_limit > 0) {
-                double el = (double)(device_clock_100mhz() - t0) * 1e-8;
-                el = wv.bcast(el, 0);
+                const double el = wv.max((double)(device_clock_100mhz() - t0) * 1e-8);
                 if (el >= st.time_limit) {
-                    time_limited = true;
-                    can_check = 0;
+                    status = IMPC_TIME_LIMIT_REACHED;
                     break;
                 }
             }
-            can_check = chk && (iter % chk == 0);
+            can_check = chk_now;
             if (can_check) {
                 IMPC_SEC_START();
                 double D[VS], Eb[VS], Eg[GS];
@@ -1037,7 +1047,7 @@ struct WaveQP {
                 IMPC_SEC(kSecChecks);
                 if (done) break;
             }
-            if (st.adaptive_rho && st.rho_interval && (iter % st.rho_interval == 0)) {
+            if (rho_now) {
                 if (!can_check) {
                     double D[VS], Eb[VS], Eg[GS];
                     load_scal(b, D, Eb, Eg);
@@ -1060,10 +1070,9 @@ struct WaveQP {
         IMPC_SEC_START();
         double D[VS], Eb[VS], Eg[GS];
         load_scal(b, D, Eb, Eg);
-        if (time_limited || !can_check) {
+        if (!can_check) {  // post-loop update_info / check, as osqp_solve
             update_info(inf, D, Eb, Eg);
-            info_iter = time_limited ? iter : iter - 1;
-            status = IMPC_UNSOLVED;
+            info_iter = iter - 1;
             check_termination(inf, 0, status, obj, D, Eb, Eg);
         }
         const bool has_sol = status != IMPC_PRIMAL_INFEASIBLE && status != IMPC_PRIMAL_INFEASIBLE_INACCURATE &&
@@ -1077,8 +1086,7 @@ struct WaveQP {
             if (st.scaling > 0) obj *= cinv;
         }
         if (status == IMPC_UNSOLVED) {
-            if (!check_termination(inf, 1, status, obj, D, Eb, Eg))
-                status = time_limited ? IMPC_TIME_LIMIT_REACHED : IMPC_MAX_ITER_REACHED;
+            if (!check_termination(inf, 1, status, obj, D, Eb, Eg)) status = IMPC_MAX_ITER_REACHED;
         }
         rho_est = rho_estimate(inf);
         const bool has_sol2 = status != IMPC_PRIMAL_INFEASIBLE && status != IMPC_PRIMAL_INFEASIBLE_INACCURATE &&

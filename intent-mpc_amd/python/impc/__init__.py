@@ -14,6 +14,8 @@ _PKG = os.path.dirname(os.path.dirname(_HERE))  # .../intent-mpc_amd
 LIB_PATH = os.path.join(_PKG, "lib", "libimpc_qp.so")
 if os.environ.get("IMPC_SECTION_PROF") == "1":  # profiling variant (tools/section_profile.py only)
     LIB_PATH = os.path.join(_PKG, "lib", "libimpc_qp_prof.so")
+if os.environ.get("IMPC_LIB_VARIANT"):  # kernel-shape experiments (tools/ only): lib/libimpc_qp_<v>.so
+    LIB_PATH = os.path.join(_PKG, "lib", "libimpc_qp_" + os.environ["IMPC_LIB_VARIANT"] + ".so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"libimpc_qp.so not built at {LIB_PATH} (run __graft_entry__.build() or `make lib`)")

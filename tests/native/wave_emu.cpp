@@ -1,7 +1,7 @@
 // wave_emu.cpp -- TEST INFRASTRUCTURE ONLY.
 //
-// Executes the one-QP-per-wavefront kernel body (intent-mpc_amd/csrc/mpc_wave.hpp) on the CPU by
-// running its 64 lanes as 64 threads that meet at a barrier wherever the GPU wave synchronises
+// Executes the one-QP-per-team kernel body (intent-mpc_amd/csrc/mpc_wave.hpp) on the CPU by
+// running its NL lanes as NL threads that meet at a barrier wherever the GPU wave synchronises
 // (LDS exchange, readlane broadcast, wave reductions).  This lets the structured solver be
 // checked against the oracle in the GPU-less container.  Never linked into libimpc_qp.so.
 #include <barrier>
@@ -14,7 +14,7 @@
 
 namespace {
 
-constexpr int NL = 128;
+constexpr int NL = 256;  // the product team shape (impc_qp.hip IMPC_TEAM / IMPC_VS)
 
 struct EmuShared {
     std::barrier<> bar{NL};
@@ -131,10 +131,14 @@ extern "C" int emu_wave_solve_batch(int64_t n, int64_t m, const int64_t *Pp, con
     st.scaled_termination = (int32_t)s->scaled_termination;
     st.check_termination = (int32_t)s->check_termination;
     st.warm_start = (int32_t)s->warm_start;
-    if (ms.n <= 2 * NL && ms.mg <= 3 * NL)
-        run<2, 3>(T, io, st);
-    else if (ms.n <= 2 * NL && ms.mg <= 4 * NL)
-        run<2, 4>(T, io, st);
+    if (ms.n > NL || ms.CG > impc::WaveLds<NL, 1, 2>::CGM)
+        return 2;
+    if (ms.mg <= 2 * NL)
+        run<1, 2>(T, io, st);
+    else if (ms.mg <= 3 * NL)
+        run<1, 3>(T, io, st);
+    else if (ms.mg <= 4 * NL)
+        run<1, 4>(T, io, st);
     else
         return 2;
     return 0;

@@ -69,3 +69,24 @@ def test_auto_selects_structured_for_mpc_patterns(ctx):
             assert st["structured_ok"] == 1 and st["kernel"] == impc.KERNEL_STRUCTURED
         finally:
             b.close()
+
+
+@KERNELS
+def test_nonbinding_time_limit_changes_nothing(ctx, kernel):
+    """time_limit reads the device clock inside the ADMM loop; a limit that never triggers must
+    leave every result bitwise unchanged (the reference passes 0.05 s, mpcPlanner.cpp:440-444)."""
+    cfg = scenarios.static_config(batch=64, identical=False, seed=515)
+    r0 = gpu(ctx, cfg, impc.default_settings(**S25), kernel)
+    r1 = gpu(ctx, cfg, impc.default_settings(time_limit=100.0, **S25), kernel)
+    assert np.array_equal(r0[0], r1[0]) and np.array_equal(r0[2]["iter"], r1[2]["iter"])
+    assert np.array_equal(r0[2]["status_val"], r1[2]["status_val"])
+
+
+@KERNELS
+def test_binding_time_limit_status(ctx, kernel):
+    """A limit far below one solve's duration stops every QP with OSQP_TIME_LIMIT_REACHED (-6)
+    and a primal iterate (x is reported, not NaN), as osqp_solve does (osqp.c time check)."""
+    cfg = scenarios.static_config(batch=32, identical=False, seed=616)
+    x, y, info = gpu(ctx, cfg, impc.default_settings(time_limit=1e-7, **S25), kernel)
+    assert np.all(info["status_val"] == impc.TIME_LIMIT_REACHED)
+    assert np.all(np.isfinite(x)) and not np.any(x == impc.OSQP_NAN)
