@@ -505,14 +505,16 @@ int generic_solve(impc_batch b, hipStream_t st) {
 template <int GS>
 int launch_wave(impc_batch b, hipStream_t st, const impc::WaveIO &io) {
     using LD = impc::WaveLds<kTeam, kWaveVS, GS>;
-    const size_t lds = sizeof(double) * LD::SIZE;
-    static bool attr_set = false;
-    if (!attr_set) {
+    const size_t lds = sizeof(double) * (size_t)LD::size(b->ms->CG);  // products region sized by the pattern
+    static size_t attr_bytes = 0;
+    if (lds > attr_bytes) {
         HIP_OK(hipFuncSetAttribute((const void *)k_mpc_wave<kTeam, kWaveVS, GS>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr_set = true;
+        attr_bytes = lds;
     }
-    const int per_cu = std::max<int>(1, std::min<int>(4, (int)((160 * 1024 - 1024) / lds)));
+    // resident workgroups per CU: the waves-per-SIMD budget of the build, and LDS
+    const int by_waves = (4 * IMPC_WAVES_PER_SIMD) / (kTeam / 64);
+    const int per_cu = std::max<int>(1, std::min<int>(by_waves, (int)((160 * 1024 - 1024) / lds)));
     const int64_t groups = std::min<int64_t>(b->B, (int64_t)b->ctx->num_cu * per_cu);
     hipLaunchKernelGGL((k_mpc_wave<kTeam, kWaveVS, GS>), dim3((unsigned)groups), dim3(kTeam), lds, st, b->wt, io,
                        b->dst, b->d_counter);

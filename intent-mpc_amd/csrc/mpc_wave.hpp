@@ -62,16 +62,16 @@ enum {
     kSecSetup, kSecFactor, kSecWarm, kSecRhs, kSecS1, kSecFwd, kSecS3, kSecBwd, kSecS5, kSecUpdate, kSecProducts,
     kSecChecks, kSecOutput, kSecIters = 15, kSecCount = 16
 };
-// The clock is the 20-bit SHADER_CYCLES hardware register (s_getreg, no memory counter
-// involved: an s_memtime SMEM read shares lgkmcnt with the LDS traffic it would be measuring);
-// deltas are taken modulo 2^20, so a section must stay under ~1M cycles.
+// The clock is the 100 MHz s_memrealtime counter (the one the time-limit path reads; a
+// SHADER_CYCLES s_getreg reads 0 on gfx950, and s_memtime perturbed the LDS wait counts of this
+// kernel's instrumented build).  Units: 10 ns ticks.
 #if defined(IMPC_SECTION_PROF) && defined(__HIP_DEVICE_COMPILE__)
-#define IMPC_SEC_CLOCK() ((uint32_t)__builtin_amdgcn_s_getreg(29 | (0 << 6) | (19 << 11)))
-#define IMPC_SEC(X)                                          \
-    do {                                                     \
-        uint32_t t_ = IMPC_SEC_CLOCK();                      \
-        sec_acc[X] += (uint64_t)((t_ - sec_t0) & 0xFFFFFu);  \
-        sec_t0 = t_;                                         \
+#define IMPC_SEC_CLOCK() ((uint64_t)__builtin_amdgcn_s_memrealtime())
+#define IMPC_SEC(X)                             \
+    do {                                        \
+        uint64_t t_ = IMPC_SEC_CLOCK();         \
+        sec_acc[X] += t_ - sec_t0;              \
+        sec_t0 = t_;                            \
     } while (0)
 #define IMPC_SEC_START() (sec_t0 = IMPC_SEC_CLOCK())
 #else
@@ -91,17 +91,24 @@ struct WaveLds {
     static constexpr int T_OFF = R_OFF + NP;                // tbuf
     static constexpr int E_OFF = T_OFF + NP;                // ebuf
     static constexpr int X_OFF = E_OFF + NP;                // xbuf
-    static constexpr int P_OFF = X_OFF + NP;                // products [4 * NL GS] + zero slot
-    static constexpr int PZ = 4 * NL * GS;                  // zero slot (relative to P_OFF)
-    static constexpr int RED_OFF = P_OFF + PZ + 8;          // team reduction scratch
+    static constexpr int RED_OFF = X_OFF + NP;              // team reduction scratch
     static constexpr int JUNK_OFF = RED_OFF + 64;           // per-lane discard slots [NL]
+    static constexpr int GSLOT_OFF = JUNK_OFF + NL;         // int16 [4 NL GS]: general entry -> product slot
+    static constexpr int P_OFF = GSLOT_OFF + NL * GS;       // products, column-slot layout (size below)
     static constexpr int CGM = 24;                          // max general entries per column
-    static constexpr int CG_OFF = JUNK_OFF + NL;            // int16 column table [CGM][NMAX]
-    static constexpr int SIZE = CG_OFF + NMAX * CGM / 4;
+    // products region: entry t of column v at t * NMAX + v (t < CG rounded up to 4), so a column's
+    // gather is CG4 independent conflict-free reads; it doubles as the factorisation's (4g + e)
+    // scratch.  Sized from the pattern at run time, followed by 8 discard slots (index p_size).
+    static IMPC_WF int cg4(int CG) { return (CG + 3) & ~3; }
+    static IMPC_WF int p_size(int CG) {
+        const int c = cg4(CG) * NMAX, f = 4 * NL * GS;
+        return c > f ? c : f;
+    }
+    static IMPC_WF int size(int CG) { return P_OFF + p_size(CG) + 8; }
     // factorisation aliases (inside R..X region and the products buffer)
     static constexpr int FA = R_OFF, FL = FA + 169, FI = FL + 169, FB = FI + 169, FG = FB + 104, FE = FG + 104,
                          RHOG = FE + 64, DIAGX = RHOG + NL * GS;
-    static_assert(DIAGX + NMAX <= P_OFF, "factorisation scratch does not fit");
+    static_assert(DIAGX + NMAX <= RED_OFF, "factorisation scratch does not fit");
 };
 
 struct WaveRho {
@@ -164,9 +171,9 @@ struct WaveQP {
     bool gok[GS];
     WaveRho R;
     double c = 1.0, cinv = 1.0;
+    int rw = 0;  // the wavefront that runs the stage recursions for this QP
 #if defined(IMPC_SECTION_PROF) && defined(__HIP_DEVICE_COMPILE__)
-    uint32_t sec_t0 = 0;
-    uint64_t sec_acc[kSecCount] = {};
+    uint64_t sec_t0 = 0, sec_acc[kSecCount] = {};
 #endif
 
     IMPC_WF WaveQP(WV &w, const WaveTables &t, const WaveIO &i, const DevSettings &s, double *l)
@@ -224,15 +231,17 @@ struct WaveQP {
             gok[s] = g < T.mg;
             z[s] = y[s] = lg[s] = ug[s] = dyg[s] = 0.0;
             gt[s] = 0;
+            const int16_t *gs = (const int16_t *)(lds + LD::GSLOT_OFF);
+            const int pz = LD::p_size(T.CG);
             _Pragma("unroll") for (int e = 0; e < 4; e++) {
                 a[s][e] = 0.0;
-                gc[s][e] = LD::NMAX;  // zero slot
+                gc[s][e] = (pz << 16) | LD::NMAX;  // discard slot / zero tail of the x exchange
             }
             if (gok[s]) {
                 _Pragma("unroll") for (int e = 0; e < 4; e++) {
                     int col = T.gen_col[4 * g + e], pos = T.gen_pos[4 * g + e];
                     if (col >= 0) {
-                        gc[s][e] = col;
+                        gc[s][e] = ((int)gs[4 * g + e] << 16) | col;
                         a[s][e] = io.Ax[bA + pos];
                     }
                 }
@@ -243,41 +252,51 @@ struct WaveQP {
         }
     }
 
-    // The per-column list of general-row entries (mpc_structure colg) as an int16 table in LDS,
-    // transposed ([t][v]) and padded to a multiple of 4 with the products buffer's zero slot, so
-    // the per-iteration gathers are branch-free LDS reads.  Loaded once per workgroup.
+    // Per-workgroup tables (once per launch): the product slot of every general-row entry
+    // (mpc_structure colg inverted into the column-slot layout, int16 in LDS; padded entries get
+    // the discard slot), and a zeroed products region (slots no entry maps to must read 0).
     static IMPC_WF void load_tables(WV &w, const WaveTables &T, double *lds) {
-        int16_t *cg = (int16_t *)(lds + LD::CG_OFF);
-        const int CG4 = (T.CG + 3) & ~3;
-        for (int e = w.lane(); e < CG4 * LD::NMAX; e += NL) {
-            const int t = e / LD::NMAX, v = e % LD::NMAX;
-            int idx = (v < T.n && t < T.CG) ? T.colg[v * T.CG + t] : -1;
-            cg[e] = (int16_t)(idx >= 0 ? idx : LD::PZ);
+        int16_t *gs = (int16_t *)(lds + LD::GSLOT_OFF);
+        const int pz = LD::p_size(T.CG);
+        for (int e = w.lane(); e < 4 * NL * GS; e += NL) gs[e] = (int16_t)pz;
+        double *pb = lds + LD::P_OFF;
+        for (int e = w.lane(); e < pz + 8; e += NL) pb[e] = 0.0;
+        w.sync();
+        for (int e = w.lane(); e < T.n * T.CG; e += NL) {
+            const int v = e / T.CG, t = e % T.CG, id = T.colg[e];
+            if (id >= 0) gs[id] = (int16_t)(t * LD::NMAX + v);
         }
-        if (w.lane() == 0) lds[LD::P_OFF + LD::PZ] = 0.0;
         w.sync();
     }
 
-    // gather sum over the general entries of this variable's column from the products buffer
+    IMPC_WF void zero_products() {
+        double *pb = pbuf();
+        const int cnt = LD::p_size(T.CG) + 8;
+        for (int i = L; i < cnt; i += NL) pb[i] = 0.0;
+        wv.sync();
+    }
+
+    // column index / product slot of general entry e of slot s (packed: slot << 16 | column)
+    IMPC_WF int gcol(int s, int e) const { return gc[s][e] & 0xFFFF; }
+    IMPC_WF int gdst(int s, int e) const { return gc[s][e] >> 16; }
+
+    // gather sum over the general entries of column v (column-slot layout, independent reads)
     IMPC_WF double col_gather(int v) {
-        const int16_t *cg = (const int16_t *)(lds + LD::CG_OFF) + v;
-        const double *pb = pbuf();
-        const int CG4 = (T.CG + 3) & ~3;
+        const double *pb = pbuf() + v;
+        const int C4 = LD::cg4(T.CG);
         double s = 0.0;
-        for (int t = 0; t < CG4; t += 4) {
-            const int i0 = cg[t * LD::NMAX], i1 = cg[(t + 1) * LD::NMAX], i2 = cg[(t + 2) * LD::NMAX],
-                      i3 = cg[(t + 3) * LD::NMAX];
-            const double p0 = pb[i0], p1 = pb[i1], p2 = pb[i2], p3 = pb[i3];
+        for (int t = 0; t < C4; t += 4) {
+            const double p0 = pb[t * LD::NMAX], p1 = pb[(t + 1) * LD::NMAX], p2 = pb[(t + 2) * LD::NMAX],
+                         p3 = pb[(t + 3) * LD::NMAX];
             s += (p0 + p1) + (p2 + p3);
         }
         return s;
     }
     IMPC_WF double col_gather_max(int v) {
-        const int16_t *cg = (const int16_t *)(lds + LD::CG_OFF) + v;
-        const double *pb = pbuf();
-        const int CG4 = (T.CG + 3) & ~3;
+        const double *pb = pbuf() + v;
+        const int C4 = LD::cg4(T.CG);
         double s = 0.0;
-        for (int t = 0; t < CG4; t++) s = dmax(pb[cg[t * LD::NMAX]], s);
+        for (int t = 0; t < C4; t++) s = dmax(pb[t * LD::NMAX], s);
         return s;
     }
 
@@ -292,9 +311,8 @@ struct WaveQP {
         for (int it = 0; it < st.scaling; it++) {
             // |A| entries of general rows -> products buffer
             _Pragma("unroll") for (int s = 0; s < GS; s++) {
-                int g = NL * s + L;
                 if (gok[s])
-                    _Pragma("unroll") for (int e = 0; e < 4; e++) pb[4 * g + e] = fabs(a[s][e]);
+                    _Pragma("unroll") for (int e = 0; e < 4; e++) pb[gdst(s, e)] = fabs(a[s][e]);
             }
             wv.sync();
             double Dt[VS], Etb[VS], Etg[GS];
@@ -331,7 +349,7 @@ struct WaveQP {
                 Eb[s] = Eb[s] * Etb[s];
             }
             _Pragma("unroll") for (int s = 0; s < GS; s++) {
-                _Pragma("unroll") for (int e = 0; e < 4; e++) a[s][e] = (a[s][e] * Etg[s]) * xb[gc[s][e]];
+                _Pragma("unroll") for (int e = 0; e < 4; e++) a[s][e] = (a[s][e] * Etg[s]) * xb[gcol(s, e)];
                 Eg[s] = Eg[s] * Etg[s];
             }
             // cost normalisation
@@ -509,6 +527,7 @@ struct WaveQP {
                 _Pragma("unroll") for (int j = 0; j < 8; j++) cp[s][j] = 0.0;
         bad = (int)wv.max((double)bad);  // set by lane 0 only: team-wide, so every wavefront agrees
         clear_exchange();
+        zero_products();  // the (4g + e) factorisation scratch shared the products region
         (void)n;
         return bad;
     }
@@ -530,10 +549,9 @@ struct WaveQP {
         const double *Fm = lds + LD::F_OFF;
         const int l = L & 63, i = l >> 3, j = l & 7;
         double *junk = lds + LD::JUNK_OFF + L;
-        const bool wri = L < 64 && j == 0, wrj = L < 64 && i == 0;
+        const bool wri = j == 0, wrj = i == 0;
         // x_W: W = (W-1)+1 has the opposite parity of the first step
         double x = eb[13 * W + (ODD ? i : j)];
-        if (L < 8) xb[13 * W + L] = eb[13 * W + L];
         const int k1 = W - 2 > 0 ? W - 2 : 0;
         double fa = Fm[64 * (W - 1) + l], ea = eb[13 * (W - 1) + (ODD ? j : i)];
         double fb = Fm[64 * k1 + l], ebv = eb[13 * k1 + (ODD ? i : j)];
@@ -555,10 +573,9 @@ struct WaveQP {
     IMPC_WF void write_v_products() {
         double *pb = pbuf();
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
-            int g = NL * s + L;
             if (gok[s]) {
                 double vv = rhog_[s] * z[s] - y[s];
-                _Pragma("unroll") for (int e = 0; e < 4; e++) pb[4 * g + e] = a[s][e] * vv;
+                _Pragma("unroll") for (int e = 0; e < 4; e++) pb[gdst(s, e)] = a[s][e] * vv;
             }
         }
         wv.sync();
@@ -598,15 +615,16 @@ struct WaveQP {
         // wavefront (lane l = 8i + j).  Vectors of even stages sit at index i, of odd stages at
         // index j; F_k is stored as F_k[j][i] (k even) / F_k[i][j] (k odd), so even steps reduce
         // over i (strided: DPP row_ror 8, permlane16/32 swaps) and odd steps over j (contiguous
-        // DPP), all in the VALU, with no transpose.  The next F and t are loaded one step ahead.
-        // Both wavefronts compute it; one lane per element of wavefront 0 writes, the rest write
-        // to discard slots (no divergent branch).
-        {
+        // DPP), all in the VALU, with no transpose.  The next F and t are loaded two steps ahead.
+        // One wavefront of the team (rw) runs it -- the others go straight to the barrier and
+        // leave their SIMD's issue slots to the co-resident team; one lane per element writes,
+        // the rest write to discard slots (no divergent branch).
+        if (L < 8) rb[L] = tb[L];
+        if ((L >> 6) == rw) {
             const int l = L & 63, i = l >> 3, j = l & 7;
             double *junk = lds + LD::JUNK_OFF + L;
-            const bool wri = L < 64 && j == 0, wrj = L < 64 && i == 0;
+            const bool wri = j == 0, wrj = i == 0;
             double a = tb[i];
-            if (L < 8) rb[L] = tb[L];
             // (F, t) of the next even / odd step, loaded two steps ahead (reads past the last
             // stage stay inside the LDS buffers and are never used)
             double fe = Fm[l], te = tb[13 + j], fo = Fm[64 + l], to = tb[26 + i];
@@ -636,10 +654,13 @@ struct WaveQP {
         IMPC_SEC(kSecS3);
         // S4: backward 8-dim recursion x_k[:8] = e_k[:8] - F_k' x_{k+1}[:8] on the same grid and
         // stored layout: even steps reduce over j (contiguous), odd steps over i (strided).
-        if ((W - 1) & 1)
-            bwd_sweep<true>(eb, xb, W);
-        else
-            bwd_sweep<false>(eb, xb, W);
+        if (L < 8) xb[13 * W + L] = eb[13 * W + L];
+        if ((L >> 6) == rw) {
+            if ((W - 1) & 1)
+                bwd_sweep<true>(eb, xb, W);
+            else
+                bwd_sweep<false>(eb, xb, W);
+        }
         wv.sync();
         IMPC_SEC(kSecBwd);
         // S5: controls x_k[8:] = e_k[8:] - G_k[:, 8:]' x_{k+1}[:8]
@@ -671,7 +692,7 @@ struct WaveQP {
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
             if (!gok[s]) continue;
             double zt = 0.0;
-            _Pragma("unroll") for (int e = 0; e < 4; e++) zt += a[s][e] * xb[gc[s][e]];
+            _Pragma("unroll") for (int e = 0; e < 4; e++) zt += a[s][e] * xb[gcol(s, e)];
             double zr = alpha * zt + oma * z[s];
             double zn = dmin(dmax(zr + rhoig_[s] * y[s], lg[s]), ug[s]);
             double dy = rhog_[s] * (zr - zn);
@@ -707,9 +728,8 @@ struct WaveQP {
             if (vok[s]) xb[NL * s + L] = x[s];
         // A'y products of the general rows
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
-            int g = NL * s + L;
             if (gok[s])
-                _Pragma("unroll") for (int e = 0; e < 4; e++) pb[4 * g + e] = a[s][e] * y[s];
+                _Pragma("unroll") for (int e = 0; e < 4; e++) pb[gdst(s, e)] = a[s][e] * y[s];
         }
         wv.sync();
         double pr_u = 0, z_u = 0, ax_u = 0, pr_p = 0, z_p = 0, ax_p = 0;
@@ -726,7 +746,7 @@ struct WaveQP {
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
             if (!gok[s]) continue;
             double ax = 0.0;
-            _Pragma("unroll") for (int e = 0; e < 4; e++) ax += a[s][e] * xb[gc[s][e]];
+            _Pragma("unroll") for (int e = 0; e < 4; e++) ax += a[s][e] * xb[gcol(s, e)];
             double r = ax + -1 * z[s], ei = 1. / Eg[s];
             pr_p = dmax(pr_p, fabs(r));
             z_p = dmax(z_p, fabs(z[s]));
@@ -816,9 +836,8 @@ struct WaveQP {
         if (nrm > kDivTol && lhs < eps * nrm) {
             double *pb = pbuf();
             _Pragma("unroll") for (int s = 0; s < GS; s++) {
-                int g = NL * s + L;
                 if (gok[s])
-                    _Pragma("unroll") for (int e = 0; e < 4; e++) pb[4 * g + e] = a[s][e] * dyg[s];
+                    _Pragma("unroll") for (int e = 0; e < 4; e++) pb[gdst(s, e)] = a[s][e] * dyg[s];
             }
             wv.sync();
             double mx = 0.0;
@@ -872,7 +891,7 @@ struct WaveQP {
                 _Pragma("unroll") for (int s = 0; s < GS; s++) {
                     if (!gok[s]) continue;
                     double t = 0.0;
-                    _Pragma("unroll") for (int e = 0; e < 4; e++) t += a[s][e] * xb[gc[s][e]];
+                    _Pragma("unroll") for (int e = 0; e < 4; e++) t += a[s][e] * xb[gcol(s, e)];
                     if (unsc) t = (1. / Eg[s]) * t;
                     if ((ug[s] < kInf * kMinScaling && t > eps * nrm) || (lg[s] > -kInf * kMinScaling && t < -eps * nrm))
                         viol = 1.0;
@@ -940,6 +959,7 @@ struct WaveQP {
     // not occupy registers across the ADMM loop.
     IMPC_WF void solve(int64_t b) {
         const int n = T.n, m = T.m;
+        rw = (int)(b % (NL / 64));  // spread the serial recursions of co-resident QPs over SIMDs
         IMPC_SEC_START();
         clear_exchange();
         load(b);
@@ -1000,7 +1020,7 @@ struct WaveQP {
                 }
                 y[s] = yv;
                 double zz = 0.0;
-                _Pragma("unroll") for (int e = 0; e < 4; e++) zz += a[s][e] * xb[gc[s][e]];
+                _Pragma("unroll") for (int e = 0; e < 4; e++) zz += a[s][e] * xb[gcol(s, e)];
                 z[s] = zz;
             }
             wv.sync();

@@ -18,38 +18,48 @@ constexpr int NL = 256;  // the product team shape (impc_qp.hip IMPC_TEAM / IMPC
 
 struct EmuShared {
     std::barrier<> bar{NL};
+    std::barrier<> wbar[NL / 64] = {std::barrier<>{64}, std::barrier<>{64}, std::barrier<>{64}, std::barrier<>{64}};
     double scratch[2][NL];
+    double wscratch[2][NL];  // wave-level exchanges (bcast / shfl / 8-lane sums), per-wave regions
 };
+static_assert(NL == 256, "wbar initialiser assumes 4 wavefronts");
 
 struct EmuWave {
     int l;
     EmuShared *sh;
-    int par = 0;
+    int par = 0, wpar = 0;
     int lane() const { return l; }
     void sync() { sh->bar.arrive_and_wait(); }
+    void wsync() { sh->wbar[l >> 6].arrive_and_wait(); }
     double *next_buf() {
         double *b = sh->scratch[par];
         par ^= 1;
         return b;
     }
+    double *next_wbuf() {
+        double *b = sh->wscratch[wpar];
+        wpar ^= 1;
+        return b;
+    }
+    // wave-level operations synchronise only the caller's wavefront (as on the GPU)
     double bcast(double v, int src) {  // lane src of the caller's 64-lane wavefront
-        double *b = next_buf();
+        double *b = next_wbuf();
         b[l] = v;
-        sync();
+        wsync();
         return b[(l & ~63) + src];
     }
     double shfl(double v, int src) { return bcast(v, src); }
     double sum_contig8(double v) {  // the GPU's DPP order: ((v0+v1)+(v2+v3)) + ((v4+v5)+(v6+v7))
-        double *b = next_buf();
+        double *b = next_wbuf();
         b[l] = v;
-        sync();
+        wsync();
         const double *g = b + (l & ~7);
         return ((g[0] + g[1]) + (g[2] + g[3])) + ((g[4] + g[5]) + (g[6] + g[7]));
     }
     double sum_stride8(double v) {  // same shape over lanes j, j+8, .., j+56 of the wavefront
-        double *b = next_buf();
+        double *b = next_wbuf();
         b[l] = v;
-        sync();
+        wsync();
         const double *g = b + (l & ~63) + (l & 7);
         return ((g[0] + g[8]) + (g[16] + g[24])) + ((g[32] + g[40]) + (g[48] + g[56]));
     }
@@ -83,7 +93,7 @@ struct EmuWave {
 template <int VS, int GS>
 void run(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSettings &st) {
     using LD = impc::WaveLds<NL, VS, GS>;
-    std::vector<double> lds(LD::SIZE, 0.0);
+    std::vector<double> lds((size_t)LD::size(T.CG), 0.0);
     EmuShared sh;
     std::vector<std::thread> th;
     for (int l = 0; l < NL; l++)

@@ -2,8 +2,9 @@
 """Per-section cycle breakdown of the structured kernel (profiling build, `make prof`).
 
 usage: IMPC_SECTION_PROF=1 python tools/section_profile.py [instances]
-Runs the bench workload (intent_config, N=20) once and prints, per section, the s_memtime
-cycles of lane 0 of each team summed over QPs, normalised per QP and per ADMM iteration.
+Runs the bench workload (intent_config, N=20) once and prints, per section, the time (100 MHz
+s_memrealtime ticks -> ns) seen by lane 0 of each team, summed over QPs, normalised per QP and per
+ADMM iteration.
 """
 import ctypes as C
 import os
@@ -42,10 +43,11 @@ def main():
         sec = np.array(sec[:], dtype=np.float64)
         iters = sec[15]
         tot = sec[:13].sum()
+        tot_ns, per_ns = 10.0 * tot, 10.0 * sec
         print(f"K={K} B={B} kernel {b.timings()[1]:.1f} ms, mean iter {iters / B:.1f}, "
-              f"cycles/QP {tot / B:.0f}, cycles/iter {tot / iters:.0f}")
+              f"us/QP {tot_ns / B / 1e3:.1f}, ns/iter {tot_ns / iters:.0f}")
         for i, nm in enumerate(NAMES):
-            print(f"  {nm:9s} {100 * sec[i] / tot:5.1f}%  per-iter {sec[i] / iters:8.0f} cyc")
+            print(f"  {nm:9s} {100 * sec[i] / tot:5.1f}%  per-iter {per_ns[i] / iters:8.0f} ns")
         b.close()
     ctx.close()
 
