@@ -90,3 +90,13 @@ def test_binding_time_limit_status(ctx, kernel):
     x, y, info = gpu(ctx, cfg, impc.default_settings(time_limit=1e-7, **S25), kernel)
     assert np.all(info["status_val"] == impc.TIME_LIMIT_REACHED)
     assert np.all(np.isfinite(x)) and not np.any(x == impc.OSQP_NAN)
+
+
+@KERNELS
+@pytest.mark.parametrize("N", [3, 6, 11, 19, 20])
+def test_horizons(ctx, kernel, N):
+    """Stage counts W = N-1 of both parities and short horizons (the structured kernel's paired
+    recursions have single-step heads/tails for odd W)."""
+    cfg = scenarios.static_config(N=N, K=3, batch=24, identical=False, seed=900 + N)
+    s = impc.default_settings(**S25)
+    compare(gpu(ctx, cfg, s, kernel), oracle(cfg, s))

@@ -69,3 +69,10 @@ def test_structured_emulation_odd_stage_count():
     cfg = scenarios.static_config(N=19, K=4, batch=1, identical=False, seed=1919)
     s = impc.default_settings(**S25)
     compare(emulate(cfg, s), oracle(cfg, s))
+
+
+@pytest.mark.parametrize("N", [3, 6])
+def test_structured_emulation_short_horizons(N):
+    cfg = scenarios.static_config(N=N, K=2, batch=1, identical=False, seed=1300 + N)
+    s = impc.default_settings(**S25)
+    compare(emulate(cfg, s), oracle(cfg, s))
