@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/impc_qp.h"
+#include "../../include/impc_select.h"
 #include "admm_core.hpp"
 #include "mpc_structure.hpp"
 #include "mpc_wave.hpp"
@@ -994,3 +995,6 @@ int impc_batch_get_perm(impc_batch b, int64_t *perm) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- candidate scoring / selection
+#include "select.hpp"

@@ -113,6 +113,19 @@ _sig("impc_batch_get_perm", C.c_int, _P, _i64p)
 _sig("impc_batch_set_profiling", C.c_int, _P, C.c_int)
 _sig("impc_batch_get_timings", C.c_int, _P, _dp, _dp, _dp)
 _sig("impc_batch_set_kernel", C.c_int, _P, C.c_int)
+
+
+class SelectParams(C.Structure):
+    """impc_select_params (include/impc_select.h)."""
+    _fields_ = [("horizon", C.c_int32), ("num_candidates", C.c_int32), ("max_dynamic", C.c_int32),
+                ("pred_len", C.c_int32), ("num_static", C.c_int32), ("prev_len", C.c_int32),
+                ("dynamic_safety_dist", C.c_double), ("static_safety_dist", C.c_double)]
+
+
+_sig("impc_select_best", C.c_int, _P, C.POINTER(SelectParams), C.c_int64, _P, _P, _P, _dp, _P, _dp, _dp, _dp, _P,
+     _dp, _dp, _dp, _P, _P, _dp, _dp)
+_sig("impc_select_best_device", C.c_int, _P, C.POINTER(SelectParams), C.c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+     _P, _P, _P, _P, _P, _P, _P, _P)
 _sig("impc_mpc_dims", C.c_int, C.POINTER(MpcParams), C.c_int32, C.c_int32, C.POINTER(Dims))
 _sig("impc_mpc_build_pattern", C.c_int, C.POINTER(MpcParams), C.c_int32, C.c_int32, _i64p, _i64p, _i64p, _i64p)
 _sig("impc_mpc_build_values", C.c_int, C.POINTER(MpcParams), C.c_int64, _dp, _dp, _dp, _dp, C.c_int32, _dp, _dp,
@@ -128,7 +141,7 @@ EXPORTED = [
     "impc_batch_set_values", "impc_batch_set_values_device", "impc_batch_warm_start", "impc_batch_setup",
     "impc_batch_solve", "impc_batch_get", "impc_batch_device_results", "impc_batch_update_lin_cost",
     "impc_batch_update_bounds", "impc_batch_get_stats", "impc_batch_get_perm", "impc_batch_set_profiling",
-    "impc_batch_get_timings", "impc_batch_set_kernel", "impc_mpc_dims",
+    "impc_batch_get_timings", "impc_batch_set_kernel", "impc_select_best", "impc_select_best_device", "impc_mpc_dims",
     "impc_mpc_build_pattern", "impc_mpc_build_values", "impc_mpc_warm_start",
 ]
 
@@ -335,3 +348,31 @@ def mpc_values(params, curr_pos, curr_vel, xref, lin_states=None, st_centroid=No
                                    _d(out["Px"]), _d(out["q"]), _d(out["Ax"]), _d(out["l"]), _d(out["u"]))
     _check(rc, "impc_mpc_build_values")
     return out
+
+
+# ------------------------------------------------------------------ candidate selection
+def select_best(ctx, params, x_ptrs, valid, first_time, prev_states, prev_count, xref, st_centroid, st_size,
+                dyn_count, dyn_pos, dyn_size, prob):
+    """impc_select_best: scoring + evaluateTraj for I instances x C candidates on the device.
+
+    params: dict of impc_select_params fields; x_ptrs: [I*C] device addresses of the candidates'
+    QP solutions (e.g. Batch.device_results()[0] + row * n * 8).  Returns dict(best_cand,
+    best_pos, scores [I][C][3], weighted [I][C])."""
+    sp = SelectParams(**params)
+    I, Cn = np.asarray(valid).shape
+    xp = np.ascontiguousarray(x_ptrs, dtype=np.uint64)
+    arr = lambda a, t: np.ascontiguousarray(a, dtype=t)  # noqa: E731
+    keep = dict(valid=arr(valid, np.int8), first=arr(first_time, np.int8), prev=arr(prev_states, np.float64),
+                pc=arr(prev_count, np.int32), xref=arr(xref, np.float64), sc=arr(st_centroid, np.float64),
+                ss=arr(st_size, np.float64), dc=arr(dyn_count, np.int32), dp=arr(dyn_pos, np.float64),
+                ds=arr(dyn_size, np.float64), prob=arr(prob, np.float64))
+    best = np.empty(I, np.int32)
+    pos = np.empty(I, np.int32)
+    scores = np.empty((I, Cn, 3))
+    weighted = np.empty((I, Cn))
+    v = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    _check(lib.impc_select_best(ctx.h, C.byref(sp), I, v(xp), v(keep["valid"]), v(keep["first"]), _d(keep["prev"]),
+                                v(keep["pc"]), _d(keep["xref"]), _d(keep["sc"]), _d(keep["ss"]), v(keep["dc"]),
+                                _d(keep["dp"]), _d(keep["ds"]), _d(keep["prob"]), v(best), v(pos), _d(scores),
+                                _d(weighted)), "impc_select_best")
+    return dict(best_cand=best, best_pos=pos, scores=scores, weighted=weighted)

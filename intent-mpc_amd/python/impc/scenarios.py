@@ -156,6 +156,8 @@ def intent_config(N=20, K=8, instances=8192, hyps=8, seed=3000, params=None):
             buckets[kk]["dyn_pos"].append(np.stack(sets))
             buckets[kk]["inst"].append(i)
             buckets[kk]["hyp"].append(h)
+    # per-instance inputs of the candidate selection (makePlanWithPred / evaluateTraj)
+    inst_data = dict(prev=prev, xref=xref, prob=prob[np.arange(I), ob], closest=ob)
     out = {}
     for kk, bk in buckets.items():
         if not bk["inst"]:
@@ -170,7 +172,7 @@ def intent_config(N=20, K=8, instances=8192, hyps=8, seed=3000, params=None):
         x_ws = np.zeros((nb, n))
         x_ws[:, : 8 * N] = prev[inst].reshape(nb, -1)          # solveTraj warm start (:489-498)
         out[kk] = dict(pattern=pat, values=vals, x_ws=x_ws, inst=inst, hyp=np.array(bk["hyp"]), K=kk, N=N,
-                       params=pd)
+                       params=pd, dyn_pos=dp, dyn_size=ds, instances=inst_data)
     return out
 
 
