@@ -123,6 +123,10 @@ def main():
         recs.append(D.make_records(rank, bk["inst"], bk["hyp"], info))
     iters_all = np.concatenate(iters_all)
     status_all = np.concatenate(status_all)
+
+    # device-side candidate scoring + selection of every instance's replan (SURVEY.md 8f row 1,
+    # mpcPlanner.cpp:771-887), on the solutions still in HBM; timed on its own
+    sel = select_candidates(impc, scenarios, ctx, buckets, batches, pd_params=settings_params(buckets))
     if not args.no_allgather:
         D.gather_records(dist, np.concatenate(recs))  # hypothesis costs to every rank
 
@@ -197,6 +201,7 @@ def main():
         "fp64": {"achieved_tflops": alg_flops / ((solve_ms + setup_ms) * 1e-3) / 1e12 if solve_ms else None,
                  "peak_tflops": PEAK_FP64_TFLOPS},
         "cpu_baseline": cpu,
+        "selection": sel,
         "gen_seconds": t_gen,
     }
     if rank == 0:
@@ -206,6 +211,31 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def settings_params(buckets):
+    return next(iter(buckets.values()))["params"]
+
+
+def select_candidates(impc, scenarios, ctx, buckets, batches, pd_params):
+    """impc_select_best over all instances (6 candidates each, all solved QPs count as solveTraj
+    successes, as OSQP's exitflag is 0 for every status); returns timing and the pick histogram."""
+    ptrs = {K: b.device_results()[0] for K, _, b in batches}
+    d = scenarios.selection_arrays(buckets, ptrs)
+    I, C, N = d["I"], d["C"], d["N"]
+    params = dict(horizon=N, num_candidates=C, max_dynamic=d["kmax"], pred_len=d["L"], num_static=0, prev_len=N,
+                  dynamic_safety_dist=pd_params["dynamic_safety_dist"],
+                  static_safety_dist=pd_params["static_safety_dist"])
+    args = (ctx, params, d["x_ptrs"], np.ones((I, C), np.int8), np.zeros(I, np.int8), d["prev"],
+            np.full(I, N, np.int32), d["xref"], np.zeros((I, 0, 3)), np.zeros((I, 0, 3)), d["dyn_count"],
+            d["dyn_pos"], d["dyn_size"], d["prob"])
+    impc.select_best(*args)  # warm-up (module load)
+    t = time.perf_counter()
+    out = impc.select_best(*args)
+    t = time.perf_counter() - t
+    picks = np.bincount(out["best_cand"][out["best_cand"] >= 0], minlength=C)
+    return {"instances": int(I), "candidates": int(C), "ms_incl_transfers": 1000.0 * t,
+            "picked_histogram": [int(v) for v in picks]}
 
 
 def cpu_baseline(buckets, settings, sample, threads):

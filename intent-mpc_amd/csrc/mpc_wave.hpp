@@ -86,9 +86,8 @@ struct WaveLds {
     static constexpr int WMAX = (NMAX + 5) / 13 - 1;       // max control stages
     // exchange vector length: zero tail past NMAX, and room for the factorisation scratch
     static constexpr int NP = (NMAX + 192 > (779 + NL * GS + NMAX + 3) / 4) ? NMAX + 192 : (779 + NL * GS + NMAX + 3) / 4;
-    static constexpr int F_OFF = 0;                         // [WMAX][64] F_k, recursion layout
-    static constexpr int F2_OFF = F_OFF + WMAX * 64;        // [WMAX/2 + 1][64] F_{2p+1} F_{2p}
-    static constexpr int R_OFF = F2_OFF + (WMAX / 2 + 1) * 64;  // rbuf
+    static constexpr int F_OFF = 0;                         // [WMAX][64]
+    static constexpr int R_OFF = F_OFF + WMAX * 64;         // rbuf
     static constexpr int T_OFF = R_OFF + NP;                // tbuf
     static constexpr int E_OFF = T_OFF + NP;                // ebuf
     static constexpr int X_OFF = E_OFF + NP;                // xbuf
@@ -150,35 +149,6 @@ IMPC_WF double prod_nc(double a, double b) {
 #endif
     return p;
 }
-
-// a lane-local value made opaque to the optimiser (no fusion into the reduction that follows)
-IMPC_WF double lane_opaque(double v) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    asm volatile("" : "+v"(v));
-#endif
-    return v;
-}
-
-// Measurement builds only (-DIMPC_DUP_<phase>=2): run one idempotent phase of the ADMM iteration
-// twice to read its marginal cost off the bench; 1 (no repetition) in the product.
-#ifndef IMPC_DUP_RHS
-#define IMPC_DUP_RHS 1
-#endif
-#ifndef IMPC_DUP_S1
-#define IMPC_DUP_S1 1
-#endif
-#ifndef IMPC_DUP_FWD
-#define IMPC_DUP_FWD 1
-#endif
-#ifndef IMPC_DUP_S3
-#define IMPC_DUP_S3 1
-#endif
-#ifndef IMPC_DUP_BWD
-#define IMPC_DUP_BWD 1
-#endif
-#ifndef IMPC_DUP_S5
-#define IMPC_DUP_S5 1
-#endif
 
 template <class WV, int NL, int VS, int GS>
 struct WaveQP {
@@ -539,16 +509,8 @@ struct WaveQP {
                     double s = 0.0;
                     for (int t = 0; t < 13; t++) s += G[13 * i + t] * Bb[13 * j + t];
                     E[8 * i + j] = s;
-                    // recursion layout (pair p = k / 2): lane (i,j) holds F_k[j][i] for p even,
-                    // F_k[i][j] for p odd; the pair product F2_p = F_{2p+1} F_{2p} likewise
-                    const bool podd = (k >> 1) & 1;
-                    Fm[64 * k + 8 * i + j] = podd ? G[13 * i + j] : G[13 * j + i];
-                    if (k & 1) {
-                        double f2 = 0.0;
-                        for (int t = 0; t < 8; t++)
-                            f2 += G[13 * i + t] * Fm[64 * (k - 1) + (podd ? 8 * t + j : 8 * j + t)];
-                        lds[LD::F2_OFF + 64 * (k >> 1) + (podd ? 8 * i + j : 8 * j + i)] = f2;
-                    }
+                    // recursion layout: lane (i,j) of step k reads F_k[j][i] (k even) / F_k[i][j]
+                    Fm[64 * k + 8 * i + j] = (k & 1) ? G[13 * i + j] : G[13 * j + i];
                 }
                 _Pragma("unroll") for (int s = 0; s < VS; s++) {
                     if (!vok[s]) continue;
@@ -570,86 +532,40 @@ struct WaveQP {
         return bad;
     }
 
-    // 8-lane reduction of pair parity: strided (over i) for even pairs, contiguous (over j) for odd
-    IMPC_WF double red(bool stride, double v) { return stride ? wv.sum_stride8(v) : wv.sum_contig8(v); }
-
-    IMPC_WF void fwd_sweep(const double *tb, double *rb, int W) {
-        const double *Fm = lds + LD::F_OFF, *F2 = lds + LD::F2_OFF;
-        const int l = L & 63, i = l >> 3, j = l & 7, P = W >> 1;
-        double *junk = lds + LD::JUNK_OFF + L;
-        double a = tb[i];  // a_0 = t_0, pair 0 input index i
-        // operands of pair p (loaded one pair ahead; reads past the last stage stay in LDS)
-        double s0 = Fm[l], s1 = Fm[64 + l], s2 = F2[l], t1in = tb[13 + i], t1out = tb[13 + j], t2out = tb[26 + j];
-        for (int p = 0; p < P; p++) {
-            const bool ev = (p & 1) == 0;
-            const int k = 2 * p, in = ev ? j : i, out = ev ? i : j;  // next pair: in/out swap
-            const double c0 = s0, c1 = s1, c2 = s2, u1 = t1in, o1 = t1out, o2 = t2out;
-            s0 = Fm[64 * (k + 2) + l];
-            s1 = Fm[64 * (k + 3) + l];
-            s2 = F2[64 * (p + 1) + l];
-            t1in = tb[13 * (k + 3) + in];
-            t1out = tb[13 * (k + 3) + out];
-            t2out = tb[13 * (k + 4) + out];
-            const double chain = lane_opaque(c2 * a - c1 * u1);
-            const double side = prod_nc(c0, a);
-            const double a2 = o2 + red(ev, chain);
-            const double a1 = o1 - red(ev, side);
-            const bool wr = ev ? i == 0 : j == 0;  // one writer per output element (index in)
-            *(wr ? rb + 13 * (k + 1) + in : junk) = a1;
-            *(wr ? rb + 13 * (k + 2) + in : junk) = a2;
-            a = a2;
-        }
-        if (W & 1) {  // last single step a_W = t_W - F_{W-1} a_{W-1}
-            const bool ev = (P & 1) == 0;
-            const int out = ev ? j : i;
-            const double aw = tb[13 * W + out] - red(ev, prod_nc(Fm[64 * (W - 1) + l], a));
-            *((ev ? i == 0 : j == 0) ? rb + 13 * W + out : junk) = aw;
-        }
+    // One step of a stage recursion on the 8x8 lane grid: returns c - R(F v), R the strided
+    // (STRIDE) or contiguous 8-lane sum, and stores it at dst (a discard slot for non-writers).
+    template <bool STRIDE>
+    IMPC_WF double rstep(double f, double c, double v, double *dst) {
+        const double p = prod_nc(f, v);
+        const double r = c - (STRIDE ? wv.sum_stride8(p) : wv.sum_contig8(p));
+        *dst = r;
+        return r;
     }
 
+    // S4 body for a first step k = W-1 of parity ODD: steps alternate strided (odd k) and
+    // contiguous (even k) reductions; x_k sits at index j (odd k) / i (even k).
+    template <bool ODD>
     IMPC_WF void bwd_sweep(const double *eb, double *xb, int W) {
-        const double *Fm = lds + LD::F_OFF, *F2 = lds + LD::F2_OFF;
-        const int l = L & 63, i = l >> 3, j = l & 7, P = W >> 1;
+        const double *Fm = lds + LD::F_OFF;
+        const int l = L & 63, i = l >> 3, j = l & 7;
         double *junk = lds + LD::JUNK_OFF + L;
-        double x;  // input of pair P-1: x_{2P}, at index j if P-1 is even, i if odd
-        if (W & 1) {  // first single step x_{2P} = e_{2P} - F_{2P}' x_W
-            const bool ev = (P & 1) == 0;  // stored like pair P: read transposed, reduce over j if even
-            const int in = ev ? j : i, out = ev ? i : j;
-            x = eb[13 * (2 * P) + out] - red(!ev, prod_nc(Fm[64 * (2 * P) + l], eb[13 * W + in]));
-            *((ev ? j == 0 : i == 0) ? xb + 13 * (2 * P) + out : junk) = x;
-        } else {
-            x = eb[13 * W + (((P - 1) & 1) ? i : j)];
-        }
-        if (P == 0) return;
-        int p = P - 1;
-        double s0 = Fm[64 * (2 * p) + l], s1 = Fm[64 * (2 * p + 1) + l], s2 = F2[64 * p + l];
-        double e1in, e1out, e0out;
-        {
-            const bool ev = (p & 1) == 0;
-            const int in = ev ? j : i, out = ev ? i : j;
-            e1in = eb[13 * (2 * p + 1) + in];
-            e1out = eb[13 * (2 * p + 1) + out];
-            e0out = eb[13 * (2 * p) + out];
-        }
-        for (; p >= 0; p--) {
-            const bool ev = (p & 1) == 0;
-            const int k = 2 * p, in = ev ? j : i, out = ev ? i : j;
-            const double c0 = s0, c1 = s1, c2 = s2, u1 = e1in, o1 = e1out, o0 = e0out;
-            const int q = p > 0 ? p - 1 : 0;  // next pair (in/out swap)
-            s0 = Fm[64 * (2 * q) + l];
-            s1 = Fm[64 * (2 * q + 1) + l];
-            s2 = F2[64 * q + l];
-            e1in = eb[13 * (2 * q + 1) + out];
-            e1out = eb[13 * (2 * q + 1) + in];
-            e0out = eb[13 * (2 * q) + in];
-            const double chain = lane_opaque(c2 * x - c0 * u1);
-            const double side = prod_nc(c1, x);
-            const double x0 = o0 + red(!ev, chain);
-            const double x1 = o1 - red(!ev, side);
-            const bool wr = ev ? j == 0 : i == 0;  // outputs at index out
-            *(wr ? xb + 13 * (k + 1) + out : junk) = x1;
-            *(wr ? xb + 13 * k + out : junk) = x0;
-            x = x0;
+        const bool wri = j == 0, wrj = i == 0;
+        // x_W: W = (W-1)+1 has the opposite parity of the first step
+        double x = eb[13 * W + (ODD ? i : j)];
+        const int k1 = W - 2 > 0 ? W - 2 : 0;
+        double fa = Fm[64 * (W - 1) + l], ea = eb[13 * (W - 1) + (ODD ? j : i)];
+        double fb = Fm[64 * k1 + l], ebv = eb[13 * k1 + (ODD ? i : j)];
+        for (int k = W - 1; k >= 0; k -= 2) {
+            const int k2 = k - 2 > 0 ? k - 2 : 0, k3 = k - 3 > 0 ? k - 3 : 0;
+            const double f0 = fa, e0 = ea;
+            fa = Fm[64 * k2 + l];
+            ea = eb[13 * k2 + (ODD ? j : i)];
+            x = rstep<ODD>(f0, e0, x, ODD ? (wrj ? xb + 13 * k + j : junk) : (wri ? xb + 13 * k + i : junk));
+            if (k - 1 < 0) break;
+            const double f1 = fb, e1 = ebv;
+            fb = Fm[64 * k3 + l];
+            ebv = eb[13 * k3 + (ODD ? i : j)];
+            x = rstep<!ODD>(f1, e1, x, ODD ? (wri ? xb + 13 * (k - 1) + i : junk) : (wrj ? xb + 13 * (k - 1) + j : junk));
         }
     }
 
@@ -668,9 +584,8 @@ struct WaveQP {
     // --------------------------------------------------------------- one ADMM iteration
     IMPC_WF void iterate(bool need_delta) {
         const int n = T.n, W = T.W;
-        double *rb = rbuf(), *tb = tbuf(), *eb = ebuf(), *xb = xbuf();
+        double *rb = rbuf(), *tb = tbuf(), *eb = ebuf(), *xb = xbuf(), *Fm = F();
         const double sigma = st.sigma, alpha = st.alpha, oma = (double)1.0 - st.alpha;
-        for (int dup_ = 0; dup_ < IMPC_DUP_RHS; dup_++) {  // measurement builds only
         // rhs = sigma x - q + A' v   (stage order)
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (!vok[s]) continue;
@@ -683,8 +598,6 @@ struct WaveQP {
         }
         wv.sync();
         IMPC_SEC(kSecRhs);
-        }  // IMPC_DUP_RHS
-        for (int dup_ = 0; dup_ < IMPC_DUP_S1; dup_++) {  // measurement builds only
         // S1: t_k = r_k[:8] - G_{k-1}[:, 8:] r_{k-1}[8:]
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (!vok[s] || vr_[s] >= 8) continue;
@@ -698,24 +611,37 @@ struct WaveQP {
         }
         wv.sync();
         IMPC_SEC(kSecS1);
-        }  // IMPC_DUP_S1
-        for (int dup_ = 0; dup_ < IMPC_DUP_FWD; dup_++) {  // measurement builds only
-        // S2: forward 8-dim recursion a_{k+1} = t_{k+1} - F_k a_k, two stages per dependent step:
-        //   a_{2p+2} = t_{2p+2} + R(F2_p a_{2p} - F_{2p+1} t_{2p+1})   (F2_p = F_{2p+1} F_{2p})
-        //   a_{2p+1} = t_{2p+1} - R(F_{2p} a_{2p})                      (side, off the chain)
-        // on the 8x8 lane grid (lane l = 8i + j) of one wavefront (rw).  Pair p's input sits at
-        // index i (p even) / j (p odd) and its matrices are stored so that every product of the
-        // pair reduces over that index: strided sum (DPP row_ror 8 + permlane16/32 swaps) for
-        // p even, contiguous (DPP quad_perm + row_half_mirror) for p odd; outputs land at the
-        // other index, which is the next pair's input -- no transposes, no LDS in the chain.  The
-        // next pair's operands are loaded one step ahead.  The other wavefronts go straight to
-        // the barrier (their SIMDs' issue slots go to the co-resident team).
+        // S2: forward 8-dim recursion a_{k+1} = t_{k+1} - F_k a_k on the 8x8 lane grid of each
+        // wavefront (lane l = 8i + j).  Vectors of even stages sit at index i, of odd stages at
+        // index j; F_k is stored as F_k[j][i] (k even) / F_k[i][j] (k odd), so even steps reduce
+        // over i (strided: DPP row_ror 8, permlane16/32 swaps) and odd steps over j (contiguous
+        // DPP), all in the VALU, with no transpose.  The next F and t are loaded two steps ahead.
+        // One wavefront of the team (rw) runs it -- the others go straight to the barrier and
+        // leave their SIMD's issue slots to the co-resident team; one lane per element writes,
+        // the rest write to discard slots (no divergent branch).
         if (L < 8) rb[L] = tb[L];
-        if ((L >> 6) == rw) fwd_sweep(tb, rb, W);
+        if ((L >> 6) == rw) {
+            const int l = L & 63, i = l >> 3, j = l & 7;
+            double *junk = lds + LD::JUNK_OFF + L;
+            const bool wri = j == 0, wrj = i == 0;
+            double a = tb[i];
+            // (F, t) of the next even / odd step, loaded two steps ahead (reads past the last
+            // stage stay inside the LDS buffers and are never used)
+            double fe = Fm[l], te = tb[13 + j], fo = Fm[64 + l], to = tb[26 + i];
+            for (int k = 0; k < W; k += 2) {
+                const double f0 = fe, t0 = te;
+                fe = Fm[64 * (k + 2) + l];
+                te = tb[13 * (k + 3) + j];
+                a = rstep<true>(f0, t0, a, wrj ? rb + 13 * (k + 1) + j : junk);
+                if (k + 1 >= W) break;
+                const double f1 = fo, t1 = to;
+                fo = Fm[64 * (k + 3) + l];
+                to = tb[13 * (k + 4) + i];
+                a = rstep<false>(f1, t1, a, wri ? rb + 13 * (k + 2) + i : junk);
+            }
+        }
         wv.sync();
         IMPC_SEC(kSecFwd);
-        }  // IMPC_DUP_FWD
-        for (int dup_ = 0; dup_ < IMPC_DUP_S3; dup_++) {  // measurement builds only
         // S3: e_k = Ahat_k^{-1} rhat_k
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (!vok[s]) continue;
@@ -726,18 +652,17 @@ struct WaveQP {
         }
         wv.sync();
         IMPC_SEC(kSecS3);
-        }  // IMPC_DUP_S3
-        for (int dup_ = 0; dup_ < IMPC_DUP_BWD; dup_++) {  // measurement builds only
-        // S4: backward recursion x_k = e_k - F_k' x_{k+1}, two stages per dependent step:
-        //   x_{2p}   = e_{2p} + R(F2_p' x_{2p+2} - F_{2p}' e_{2p+1})
-        //   x_{2p+1} = e_{2p+1} - R(F_{2p+1}' x_{2p+2})                 (side)
-        // same grid and stored matrices (read transposed: pair p reduces over j for p even).
+        // S4: backward 8-dim recursion x_k[:8] = e_k[:8] - F_k' x_{k+1}[:8] on the same grid and
+        // stored layout: even steps reduce over j (contiguous), odd steps over i (strided).
         if (L < 8) xb[13 * W + L] = eb[13 * W + L];
-        if ((L >> 6) == rw) bwd_sweep(eb, xb, W);
+        if ((L >> 6) == rw) {
+            if ((W - 1) & 1)
+                bwd_sweep<true>(eb, xb, W);
+            else
+                bwd_sweep<false>(eb, xb, W);
+        }
         wv.sync();
         IMPC_SEC(kSecBwd);
-        }  // IMPC_DUP_BWD
-        for (int dup_ = 0; dup_ < IMPC_DUP_S5; dup_++) {  // measurement builds only
         // S5: controls x_k[8:] = e_k[8:] - G_k[:, 8:]' x_{k+1}[:8]
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (!vok[s] || vr_[s] < 8) continue;
@@ -748,7 +673,6 @@ struct WaveQP {
         }
         wv.sync();
         IMPC_SEC(kSecS5);
-        }  // IMPC_DUP_S5
         // update_x and the box rows (update_z / project / update_y)
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (!vok[s]) continue;

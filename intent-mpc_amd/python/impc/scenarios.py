@@ -185,3 +185,32 @@ def first_call_config(N=20, batch=1, seed=1000, params=None):
     pat = mpc_pattern(p, 0, 0)
     vals = mpc_values(p, pos, vel, xref, None)
     return dict(pattern=pat, values=vals, x_ws=None, params=pd, K=0, N=N)
+
+
+def selection_arrays(buckets, ptr_by_bucket, C=6):
+    """Inputs of impc.select_best for the intent_config buckets: hypotheses 0..C-1 of every
+    instance are mpcPlanner's getIntentComb candidates.  ptr_by_bucket[K] is the device address
+    of bucket K's QP-major solution array (Batch.device_results()[0])."""
+    any_bk = next(iter(buckets.values()))
+    inst = any_bk["instances"]
+    I = inst["prev"].shape[0]
+    N = any_bk["N"]
+    kmax = max(buckets)
+    L = any_bk["dyn_pos"].shape[2]
+    x_ptrs = np.zeros(I * C, np.uint64)
+    dyn_pos = np.zeros((I, C, kmax, L, 3))
+    dyn_size = np.zeros((I, C, kmax, L, 3))
+    dyn_count = np.zeros((I, C), np.int32)
+    rows = {}
+    for K, bk in buckets.items():
+        n = bk["pattern"]["n"]
+        sel = bk["hyp"] < C
+        r = np.nonzero(sel)[0]
+        i, h = bk["inst"][sel], bk["hyp"][sel]
+        x_ptrs[i * C + h] = np.uint64(ptr_by_bucket[K]) + (r * n * 8).astype(np.uint64)
+        dyn_pos[i, h, :K] = bk["dyn_pos"][r]
+        dyn_size[i, h, :K] = bk["dyn_size"][r]
+        dyn_count[i, h] = K
+        rows[K] = (i, h, r)
+    return dict(I=I, N=N, C=C, kmax=kmax, L=L, x_ptrs=x_ptrs, dyn_pos=dyn_pos, dyn_size=dyn_size,
+                dyn_count=dyn_count, prev=inst["prev"], xref=inst["xref"], prob=inst["prob"], rows=rows)

@@ -69,30 +69,29 @@ def test_evaluate_weights_by_candidate_position_and_first_max():
 
 
 def selection_inputs(buckets, x_by_bucket, ptr_by_bucket, C=6):
-    """Assemble per (instance, candidate) inputs for hypotheses 0..C-1 of intent_config buckets."""
-    any_bk = next(iter(buckets.values()))
-    inst = any_bk["instances"]
-    I = inst["prev"].shape[0]
-    N = any_bk["N"]
-    kmax = max(buckets)
-    L = any_bk["dyn_pos"].shape[2]
-    x_ptrs = np.zeros(I * C, np.uint64)
-    states = [[None] * C for _ in range(I)]
-    dyn_pos = np.zeros((I, C, kmax, L, 3))
-    dyn_size = np.zeros((I, C, kmax, L, 3))
-    dyn_count = np.zeros((I, C), np.int32)
-    for K, bk in buckets.items():
-        n = bk["pattern"]["n"]
-        for r, (i, h) in enumerate(zip(bk["inst"], bk["hyp"])):
-            if h >= C:
-                continue
-            x_ptrs[i * C + h] = ptr_by_bucket[K] + r * n * 8
+    """impc.scenarios.selection_arrays plus the candidates' state trajectories on the host."""
+    d = scenarios.selection_arrays(buckets, ptr_by_bucket, C)
+    N = d["N"]
+    states = [[None] * C for _ in range(d["I"])]
+    for K, (inst, hyp, rows) in d["rows"].items():
+        for i, h, r in zip(inst, hyp, rows):
             states[i][h] = x_by_bucket[K][r, :8 * N].reshape(N, 8)
-            dyn_pos[i, h, :K] = bk["dyn_pos"][r]
-            dyn_size[i, h, :K] = bk["dyn_size"][r]
-            dyn_count[i, h] = K
-    return dict(I=I, N=N, C=C, kmax=kmax, L=L, x_ptrs=x_ptrs, states=states, dyn_pos=dyn_pos, dyn_size=dyn_size,
-                dyn_count=dyn_count, prev=inst["prev"], xref=inst["xref"], prob=inst["prob"])
+    d["states"] = states
+    return d
+
+
+def test_selection_arrays_layout():
+    """Every instance gets its 6 candidates, each pointing at its own bucket row."""
+    buckets = scenarios.intent_config(instances=5, seed=99)
+    ptrs = {K: 1 << 40 for K in buckets}
+    d = scenarios.selection_arrays(buckets, ptrs)
+    assert d["x_ptrs"].shape == (5 * 6,) and np.all(d["x_ptrs"] >= (1 << 40))
+    assert set(np.unique(d["dyn_count"])) <= set(buckets)
+    for K, bk in buckets.items():
+        i, h, r = d["rows"][K]
+        n = bk["pattern"]["n"]
+        assert np.all(d["x_ptrs"][i * 6 + h] == (1 << 40) + r * n * 8)
+        assert np.array_equal(d["dyn_pos"][i, h, :K], bk["dyn_pos"][r])
 
 
 @pytest.mark.gpu
