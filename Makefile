@@ -32,14 +32,16 @@ oracle: $(ORACLE)
 harness: $(HARNESS) $(EMU) $(SHIMT)
 
 $(LIBDIR)/impc_qp.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symbolic.hpp $(CSRC)/mpc_wave.hpp \
-		$(CSRC)/mpc_structure.hpp $(CSRC)/select.hpp $(ROOT)/include/impc_qp.h $(ROOT)/include/impc_select.h
+		$(CSRC)/mpc_structure.hpp $(CSRC)/select.hpp $(CSRC)/mpc_build.hpp $(CSRC)/mpc_qp_internal.hpp \
+		$(ROOT)/include/impc_qp.h $(ROOT)/include/impc_select.h $(ROOT)/include/impc_mpc.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 # section-profiling variant of the library (tools/section_profile.py; never the product)
 prof: $(PROFLIB)
 $(LIBDIR)/impc_qp_prof.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symbolic.hpp $(CSRC)/mpc_wave.hpp \
-		$(CSRC)/mpc_structure.hpp $(CSRC)/select.hpp $(ROOT)/include/impc_qp.h $(ROOT)/include/impc_select.h
+		$(CSRC)/mpc_structure.hpp $(CSRC)/select.hpp $(CSRC)/mpc_build.hpp $(CSRC)/mpc_qp_internal.hpp \
+		$(ROOT)/include/impc_qp.h $(ROOT)/include/impc_select.h $(ROOT)/include/impc_mpc.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -DIMPC_SECTION_PROF -c $< -o $@
 $(PROFLIB): $(LIBDIR)/impc_qp_prof.o $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o
@@ -49,7 +51,7 @@ $(LIBDIR)/symbolic.o: $(CSRC)/symbolic.cpp $(CSRC)/symbolic.hpp
 	@mkdir -p $(LIBDIR)
 	$(CXX) $(HOSTFLAGS) -c $< -o $@
 
-$(LIBDIR)/mpc_qp.o: $(CSRC)/mpc_qp.cpp $(ROOT)/include/impc_mpc.h
+$(LIBDIR)/mpc_qp.o: $(CSRC)/mpc_qp.cpp $(CSRC)/mpc_qp_internal.hpp $(ROOT)/include/impc_mpc.h
 	@mkdir -p $(LIBDIR)
 	$(CXX) $(HOSTFLAGS) -c $< -o $@
 

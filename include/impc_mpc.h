@@ -23,6 +23,7 @@
 #ifndef IMPC_MPC_H
 #define IMPC_MPC_H
 #include <stdint.h>
+#include "impc_qp.h"
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -70,6 +71,26 @@ int impc_mpc_build_values(const impc_mpc_params *p, int64_t nb, const double *cu
 
 /* Warm-start primal vector of solveTraj (mpcPlanner.cpp:487-509): previous states/controls,
  * zero when absent.  prev_states [nb][N][8] / prev_controls [nb][N-1][5] may be NULL. */
+/* ---- On-device assembly: the same values, built on the GPU.
+ * A builder holds, on the device, the instance-independent part of one (horizon, #static,
+ * #dynamic) shape -- P, the dynamics/box/half-space entries of A, the bound templates -- and the
+ * CSC slots of the obstacle-row entries; impc_mpc_build_values_device then fills q, the x0 rows
+ * and the obstacle rows of nb instances (one workgroup per QP, same expressions as
+ * castMPCToQPConstraintMatrix/Vectors).  Dynamic-obstacle entries are bit-identical to
+ * impc_mpc_build_values; static obstacles with yaw go through the device cos/sin (a few ulp). */
+typedef struct impc_mpc_builder_s *impc_mpc_builder;
+int impc_mpc_builder_create(impc_ctx ctx, const impc_mpc_params *p, int32_t num_static, int32_t num_dynamic,
+                            int32_t pred_len, impc_mpc_builder *out);
+int impc_mpc_builder_destroy(impc_mpc_builder b);
+/* DEVICE pointers, layouts as impc_mpc_build_values; lin_states may be NULL (first call).
+ * Outputs QP-major (ready for impc_batch_set_values_device).  Asynchronous on `stream`
+ * (NULL = the context's stream). */
+int impc_mpc_build_values_device(impc_mpc_builder b, int64_t nb, const double *curr_pos, const double *curr_vel,
+                                 const double *xref, const double *lin_states, const double *st_centroid,
+                                 const double *st_size, const double *st_yaw, const double *dyn_pos,
+                                 const double *dyn_size, double *Px, double *q, double *Ax, double *l, double *u,
+                                 void *stream);
+
 int impc_mpc_warm_start(const impc_mpc_params *p, int64_t nb, const double *prev_states, const double *prev_controls,
                         double *x_ws);
 

@@ -168,6 +168,13 @@ int impc_batch_update_bounds(impc_batch b, const double *l, const double *u);
 #define IMPC_KERNEL_STRUCTURED 2
 int impc_batch_set_kernel(impc_batch b, int kernel);
 
+/* Device memory utilities for callers without their own HIP plumbing (FFI bindings, tests):
+ * allocation on the context's device and synchronous copies. */
+int impc_device_alloc(impc_ctx ctx, int64_t bytes, void **out);
+int impc_device_free(impc_ctx ctx, void *ptr);
+int impc_copy_to_device(impc_ctx ctx, void *dst, const void *src, int64_t bytes);
+int impc_copy_to_host(impc_ctx ctx, void *dst, const void *src, int64_t bytes);
+
 /* Problem / analysis facts (for tests and roofline accounting). */
 typedef struct {
     int64_t n, m, nnzP, nnzA, batch, batch_stride;

@@ -21,6 +21,8 @@
 
 #include "../../include/impc_qp.h"
 #include "../../include/impc_select.h"
+#include "../../include/impc_mpc.h"
+#include "mpc_qp_internal.hpp"
 #include "admm_core.hpp"
 #include "mpc_structure.hpp"
 #include "mpc_wave.hpp"
@@ -996,5 +998,38 @@ int impc_batch_get_perm(impc_batch b, int64_t *perm) {
 
 }  // extern "C"
 
+// ---------------------------------------------------------------- device memory utilities
+int impc_device_alloc(impc_ctx ctx, int64_t bytes, void **out) {
+    if (!ctx || !out || bytes < 0) return fail(IMPC_INVALID_ARGUMENT, "invalid argument");
+    *out = nullptr;
+    HIP_OK(hipSetDevice(ctx->device));
+    HIP_OK(hipMalloc(out, (size_t)std::max<int64_t>(bytes, 1)));
+    return IMPC_OK;
+}
+int impc_device_free(impc_ctx ctx, void *ptr) {
+    if (!ctx) return fail(IMPC_INVALID_ARGUMENT, "null context");
+    if (!ptr) return IMPC_OK;
+    HIP_OK(hipSetDevice(ctx->device));
+    HIP_OK(hipFree(ptr));
+    return IMPC_OK;
+}
+int impc_copy_to_device(impc_ctx ctx, void *dst, const void *src, int64_t bytes) {
+    if (!ctx || (bytes > 0 && (!dst || !src)) || bytes < 0) return fail(IMPC_INVALID_ARGUMENT, "invalid argument");
+    HIP_OK(hipSetDevice(ctx->device));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    if (bytes) HIP_OK(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyHostToDevice));
+    return IMPC_OK;
+}
+int impc_copy_to_host(impc_ctx ctx, void *dst, const void *src, int64_t bytes) {
+    if (!ctx || (bytes > 0 && (!dst || !src)) || bytes < 0) return fail(IMPC_INVALID_ARGUMENT, "invalid argument");
+    HIP_OK(hipSetDevice(ctx->device));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    if (bytes) HIP_OK(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyDeviceToHost));
+    return IMPC_OK;
+}
+
 // ---------------------------------------------------------------- candidate scoring / selection
 #include "select.hpp"
+
+// ---------------------------------------------------------------- on-device MPC -> QP assembly
+#include "mpc_build.hpp"

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/impc_mpc.h"
+#include "mpc_qp_internal.hpp"
 
 namespace {
 
@@ -363,6 +364,20 @@ extern "C" int impc_mpc_build_values(const impc_mpc_params *p, int64_t nb, const
                 }
         }
     }
+    return 0;
+}
+
+int impc_mpc_obstacle_layout(const impc_mpc_params *p, int32_t num_static, int32_t num_dynamic,
+                             std::vector<int64_t> &slots, int64_t &obs_row_off) {
+    Shape s;
+    if (!make_shape(p, num_static, num_dynamic, &s)) return 1;
+    std::vector<Trip> t;
+    a_insertions(p, s, t);
+    std::vector<int64_t> slot;
+    csc_from_insertions(s.n, t, nullptr, nullptr, slot);
+    const int64_t nob = (int64_t)4 * s.W * s.K, base = (int64_t)t.size() - nob;
+    slots.assign(slot.begin() + base, slot.end());
+    obs_row_off = s.off_obs;
     return 0;
 }
 

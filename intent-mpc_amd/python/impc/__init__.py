@@ -113,6 +113,10 @@ _sig("impc_batch_get_perm", C.c_int, _P, _i64p)
 _sig("impc_batch_set_profiling", C.c_int, _P, C.c_int)
 _sig("impc_batch_get_timings", C.c_int, _P, _dp, _dp, _dp)
 _sig("impc_batch_set_kernel", C.c_int, _P, C.c_int)
+_sig("impc_device_alloc", C.c_int, _P, C.c_int64, C.POINTER(_P))
+_sig("impc_device_free", C.c_int, _P, _P)
+_sig("impc_copy_to_device", C.c_int, _P, _P, _P, C.c_int64)
+_sig("impc_copy_to_host", C.c_int, _P, _P, _P, C.c_int64)
 
 
 class SelectParams(C.Structure):
@@ -130,6 +134,9 @@ _sig("impc_mpc_dims", C.c_int, C.POINTER(MpcParams), C.c_int32, C.c_int32, C.POI
 _sig("impc_mpc_build_pattern", C.c_int, C.POINTER(MpcParams), C.c_int32, C.c_int32, _i64p, _i64p, _i64p, _i64p)
 _sig("impc_mpc_build_values", C.c_int, C.POINTER(MpcParams), C.c_int64, _dp, _dp, _dp, _dp, C.c_int32, _dp, _dp,
      _dp, C.c_int32, C.c_int32, _dp, _dp, _dp, _dp, _dp, _dp, _dp)
+_sig("impc_mpc_builder_create", C.c_int, _P, C.POINTER(MpcParams), C.c_int32, C.c_int32, C.c_int32, C.POINTER(_P))
+_sig("impc_mpc_builder_destroy", C.c_int, _P)
+_sig("impc_mpc_build_values_device", C.c_int, _P, C.c_int64, *([_P] * 14), _P)
 _sig("impc_mpc_warm_start", C.c_int, C.POINTER(MpcParams), C.c_int64, _dp, _dp, _dp)
 
 # every symbol declared in include/*.h (checked by tests/test_abi.py)
@@ -141,8 +148,10 @@ EXPORTED = [
     "impc_batch_set_values", "impc_batch_set_values_device", "impc_batch_warm_start", "impc_batch_setup",
     "impc_batch_solve", "impc_batch_get", "impc_batch_device_results", "impc_batch_update_lin_cost",
     "impc_batch_update_bounds", "impc_batch_get_stats", "impc_batch_get_perm", "impc_batch_set_profiling",
-    "impc_batch_get_timings", "impc_batch_set_kernel", "impc_select_best", "impc_select_best_device", "impc_mpc_dims",
-    "impc_mpc_build_pattern", "impc_mpc_build_values", "impc_mpc_warm_start",
+    "impc_batch_get_timings", "impc_batch_set_kernel", "impc_device_alloc", "impc_device_free",
+    "impc_copy_to_device", "impc_copy_to_host", "impc_select_best", "impc_select_best_device", "impc_mpc_dims",
+    "impc_mpc_build_pattern", "impc_mpc_build_values", "impc_mpc_warm_start", "impc_mpc_builder_create",
+    "impc_mpc_builder_destroy", "impc_mpc_build_values_device",
 ]
 
 
@@ -376,3 +385,63 @@ def select_best(ctx, params, x_ptrs, valid, first_time, prev_states, prev_count,
                                 _d(keep["dp"]), _d(keep["ds"]), _d(keep["prob"]), v(best), v(pos), _d(scores),
                                 _d(weighted)), "impc_select_best")
     return dict(best_cand=best, best_pos=pos, scores=scores, weighted=weighted)
+
+
+class MpcBuilder:
+    """impc_mpc_builder: on-device castMPCToQP* for one (horizon, #static, #dynamic) shape.
+    build() takes device addresses (ints, e.g. torch tensor data_ptr()) and fills device output
+    arrays, asynchronously on the context stream."""
+
+    def __init__(self, ctx, params, num_static, num_dynamic, pred_len):
+        self.ctx, self.params = ctx, params
+        self.h = _P()
+        _check(lib.impc_mpc_builder_create(ctx.h, C.byref(params), num_static, num_dynamic, pred_len,
+                                           C.byref(self.h)), "impc_mpc_builder_create")
+
+    def build(self, nb, curr_pos, curr_vel, xref, lin_states, st_centroid, st_size, st_yaw, dyn_pos, dyn_size,
+              Px, q, Ax, l, u):
+        ptrs = [curr_pos, curr_vel, xref, lin_states, st_centroid, st_size, st_yaw, dyn_pos, dyn_size, Px, q, Ax, l, u]
+        _check(lib.impc_mpc_build_values_device(self.h, nb, *[_P(p) if p else None for p in ptrs], None),
+               "impc_mpc_build_values_device")
+
+    def close(self):
+        if self.h:
+            lib.impc_mpc_builder_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceArray:
+    """A device allocation of the library (impc_device_alloc) holding one numpy array's bytes."""
+
+    def __init__(self, ctx, shape_or_array, dtype=np.float64):
+        self.ctx = ctx
+        if isinstance(shape_or_array, np.ndarray):
+            host = np.ascontiguousarray(shape_or_array)
+            self.shape, self.dtype = host.shape, host.dtype
+        else:
+            host = None
+            self.shape, self.dtype = tuple(shape_or_array), np.dtype(dtype)
+        self.nbytes = int(np.prod(self.shape, dtype=np.int64)) * self.dtype.itemsize
+        p = _P()
+        _check(lib.impc_device_alloc(ctx.h, self.nbytes, C.byref(p)), "impc_device_alloc")
+        self.ptr = p.value
+        if host is not None:
+            _check(lib.impc_copy_to_device(ctx.h, _P(self.ptr), host.ctypes.data_as(_P), self.nbytes),
+                   "impc_copy_to_device")
+
+    def get(self):
+        out = np.empty(self.shape, self.dtype)
+        _check(lib.impc_copy_to_host(self.ctx.h, out.ctypes.data_as(_P), _P(self.ptr), self.nbytes),
+               "impc_copy_to_host")
+        return out
+
+    def free(self):
+        if self.ptr:
+            lib.impc_device_free(self.ctx.h, _P(self.ptr))
+            self.ptr = None
