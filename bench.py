@@ -85,7 +85,12 @@ def main():
         batches.append((K, bk, b))
     total_qps = sum(b.B for _, _, b in batches)
 
+    grouped = all(b.stats()["kernel"] == impc.KERNEL_STRUCTURED for _, _, b in batches) and len(batches) > 1
+
     def step():
+        if grouped:  # one persistent launch over all pattern buckets (impc_batch_solve_group)
+            impc.solve_group([b for _, _, b in batches])
+            return
         for _, _, b in batches:
             b.setup()
             b.solve()
@@ -133,8 +138,8 @@ def main():
     value = throughput(world, total_qps, args.steps, elapsed)
 
     # roofline of the dominant kernel, SURVEY.md 8(d) algorithmic bytes
-    kernel_name = "k_mpc_wave" if all(b.stats()["kernel"] == impc.KERNEL_STRUCTURED for _, _, b in batches) \
-        else "k_solve"
+    kernel_name = ("k_mpc_wave_group" if grouped else "k_mpc_wave") \
+        if all(b.stats()["kernel"] == impc.KERNEL_STRUCTURED for _, _, b in batches) else "k_solve"
     solve_ms = sum(kt[K][1] for K in kt)
     setup_ms = sum(kt[K][0] for K in kt)
     alg_bytes = 0.0

@@ -148,6 +148,14 @@ int impc_batch_setup(impc_batch b, void *stream);
  * setup.  Asynchronous on `stream`. */
 int impc_batch_solve(impc_batch b, void *stream);
 
+/* One persistent launch for several structured batches (e.g. the pattern buckets of a replan:
+ * candidates with K and K+1 obstacles): a single work queue over all their QPs, so the slow QPs
+ * at the end of one batch overlap the others' work.  The batches must share the context and the
+ * structured kernel's team shape (impc_batch_stats.kernel == IMPC_KERNEL_STRUCTURED; n <= 256, i.e.
+ * N <= 20, or 256 < n <= 768).  Results land in each batch as after impc_batch_solve.  With profiling
+ * on for bs[0], its impc_batch_get_timings reports the grouped kernel. */
+int impc_batch_solve_group(impc_batch *bs, int count, void *stream);
+
 /* Synchronise and copy results to host (any pointer may be NULL): x [B][n], y [B][m], info [B]. */
 int impc_batch_get(impc_batch b, double *x, double *y, impc_info *info);
 

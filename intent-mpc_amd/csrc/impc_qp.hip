@@ -60,6 +60,9 @@ constexpr int kTile = 64;   // transpose tile edge
 #endif
 constexpr int kTeam = IMPC_TEAM;   // lanes per QP (IMPC_TEAM / 64 wavefronts)
 constexpr int kWaveVS = IMPC_VS;   // variable slots per lane (n <= kTeam * kWaveVS)
+// long-horizon shape (e.g. N = 40, n = 515): three variable slots per lane, one wave per SIMD
+// (the per-QP LDS then allows one team per CU anyway)
+constexpr int kWaveVSLong = 3;
 
 // ------------------------------------------------------------------ layout transposes
 // dst[e * S + b] = src[b * len + e]; 64x64 tile through LDS so both sides are coalesced.
@@ -255,9 +258,9 @@ struct GpuTeam {
     }
 };
 
-template <int NL, int VS, int GS>
-__global__ __launch_bounds__(NL, IMPC_WAVES_PER_SIMD) void k_mpc_wave(impc::WaveTables T, impc::WaveIO io, impc::DevSettings st,
-                                                    unsigned *counter) {
+template <int NL, int VS, int GS, int WPS>
+__global__ __launch_bounds__(NL, WPS) void k_mpc_wave(impc::WaveTables T, impc::WaveIO io, impc::DevSettings st,
+                                                      unsigned *counter) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     using LD = impc::WaveLds<NL, VS, GS>;
     GpuTeam<NL> wv{smem + LD::RED_OFF};
@@ -274,12 +277,53 @@ __global__ __launch_bounds__(NL, IMPC_WAVES_PER_SIMD) void k_mpc_wave(impc::Wave
     }
 }
 
+// One batch of a grouped launch (impc_batch_solve_group): its tables, I/O, settings and the
+// index of its first QP in the group's work queue.
+struct GroupEntry {
+    impc::WaveTables T;
+    impc::WaveIO io;
+    impc::DevSettings st;
+    int64_t first;
+};
+
+// Several structured batches in one persistent launch: one work queue over all their QPs, so
+// the long-running QPs at the end of one batch overlap the next batch's work instead of leaving
+// CUs idle between launches.  A workgroup reloads the pattern tables when it crosses batches.
+template <int NL, int VS, int GS, int WPS>
+__global__ __launch_bounds__(NL, WPS) void k_mpc_wave_group(const GroupEntry *__restrict__ g, int count,
+                                                            int64_t total, unsigned *counter) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    using LD = impc::WaveLds<NL, VS, GS>;
+    GpuTeam<NL> wv{smem + LD::RED_OFF};
+    __shared__ unsigned next;
+    int cur = -1;
+    for (;;) {
+        if (threadIdx.x == 0) next = atomicAdd(counter, 1u);
+        __syncthreads();
+        const unsigned b = next;
+        __syncthreads();
+        if ((int64_t)b >= total) break;
+        int e = 0;
+        while (e + 1 < count && (int64_t)b >= g[e + 1].first) e++;
+        if (e != cur) {
+            impc::WaveQP<GpuTeam<NL>, NL, VS, GS>::load_tables(wv, g[e].T, smem);
+            cur = e;
+        }
+        impc::WaveQP<GpuTeam<NL>, NL, VS, GS> qp(wv, g[e].T, g[e].io, g[e].st, smem);
+        qp.solve((int64_t)b - g[e].first);
+    }
+}
+
 }  // namespace
 
 struct impc_ctx_s {
     int device = 0;
     int num_cu = 256;
     hipStream_t stream = nullptr;
+    // grouped launches: device copy of the entries (grow-only) and its host staging buffer
+    GroupEntry *d_group = nullptr;
+    int group_cap = 0;
+    std::vector<GroupEntry> h_group;
 };
 
 struct impc_batch_s {
@@ -301,7 +345,8 @@ struct impc_batch_s {
     // ---- structured path
     std::unique_ptr<impc::MpcStructure> ms;
     bool structured_ok = false;
-    int gs = 0;
+    int gs = 0;  // general-row slots per lane of the structured kernel
+    int vs = 1;  // variable slots per lane (kWaveVS, or kWaveVSLong for long horizons)
     void *d_tables = nullptr;
     double *d_scal = nullptr;
     unsigned *d_counter = nullptr;
@@ -505,21 +550,22 @@ int generic_solve(impc_batch b, hipStream_t st) {
 }
 
 // ---- structured path
-template <int GS>
+template <int VS, int GS>
 int launch_wave(impc_batch b, hipStream_t st, const impc::WaveIO &io) {
-    using LD = impc::WaveLds<kTeam, kWaveVS, GS>;
-    const size_t lds = sizeof(double) * (size_t)LD::size(b->ms->CG);  // products region sized by the pattern
+    constexpr int WPS = VS == kWaveVS ? IMPC_WAVES_PER_SIMD : 1;
+    using LD = impc::WaveLds<kTeam, VS, GS>;
+    const size_t lds = sizeof(double) * (size_t)LD::size(b->ms->CG, b->ms->n);  // products sized by the pattern
     static size_t attr_bytes = 0;
     if (lds > attr_bytes) {
-        HIP_OK(hipFuncSetAttribute((const void *)k_mpc_wave<kTeam, kWaveVS, GS>,
+        HIP_OK(hipFuncSetAttribute((const void *)k_mpc_wave<kTeam, VS, GS, WPS>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         attr_bytes = lds;
     }
-    // resident workgroups per CU: the waves-per-SIMD budget of the build, and LDS
-    const int by_waves = (4 * IMPC_WAVES_PER_SIMD) / (kTeam / 64);
+    // resident workgroups per CU: the waves-per-SIMD budget of the shape, and LDS
+    const int by_waves = std::max(1, (4 * WPS) / (kTeam / 64));
     const int per_cu = std::max<int>(1, std::min<int>(by_waves, (int)((160 * 1024 - 1024) / lds)));
     const int64_t groups = std::min<int64_t>(b->B, (int64_t)b->ctx->num_cu * per_cu);
-    hipLaunchKernelGGL((k_mpc_wave<kTeam, kWaveVS, GS>), dim3((unsigned)groups), dim3(kTeam), lds, st, b->wt, io,
+    hipLaunchKernelGGL((k_mpc_wave<kTeam, VS, GS, WPS>), dim3((unsigned)groups), dim3(kTeam), lds, st, b->wt, io,
                        b->dst, b->d_counter);
     HIP_OK(hipGetLastError());
     return IMPC_OK;
@@ -538,10 +584,13 @@ int structured_solve(impc_batch b, hipStream_t st) {
 #endif
     if (b->profile) HIP_OK(hipEventRecord(b->ev[2], st));
     int rc;
-    switch (b->gs) {
-        case 2: rc = launch_wave<2>(b, st, io); break;
-        case 3: rc = launch_wave<3>(b, st, io); break;
-        case 4: rc = launch_wave<4>(b, st, io); break;
+    switch (b->vs * 8 + b->gs) {
+        case kWaveVS * 8 + 2: rc = launch_wave<kWaveVS, 2>(b, st, io); break;
+        case kWaveVS * 8 + 3: rc = launch_wave<kWaveVS, 3>(b, st, io); break;
+        case kWaveVS * 8 + 4: rc = launch_wave<kWaveVS, 4>(b, st, io); break;
+        case kWaveVSLong * 8 + 2: rc = launch_wave<kWaveVSLong, 2>(b, st, io); break;
+        case kWaveVSLong * 8 + 3: rc = launch_wave<kWaveVSLong, 3>(b, st, io); break;
+        case kWaveVSLong * 8 + 4: rc = launch_wave<kWaveVSLong, 4>(b, st, io); break;
         default: return fail(IMPC_UNSUPPORTED, "no structured kernel for this size");
     }
     if (rc) return rc;
@@ -554,17 +603,48 @@ int structured_solve(impc_batch b, hipStream_t st) {
     return IMPC_OK;
 }
 
+template <int VS, int GS>
+int launch_group(impc_ctx ctx, hipStream_t st, int count, int64_t total, int maxCG, int maxN, unsigned *counter) {
+    constexpr int WPS = VS == kWaveVS ? IMPC_WAVES_PER_SIMD : 1;
+    using LD = impc::WaveLds<kTeam, VS, GS>;
+    const size_t lds = sizeof(double) * (size_t)LD::size(maxCG, maxN);
+    static size_t attr_bytes = 0;
+    if (lds > attr_bytes) {
+        HIP_OK(hipFuncSetAttribute((const void *)k_mpc_wave_group<kTeam, VS, GS, WPS>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr_bytes = lds;
+    }
+    const int by_waves = std::max(1, (4 * WPS) / (kTeam / 64));
+    const int per_cu = std::max<int>(1, std::min<int>(by_waves, (int)((160 * 1024 - 1024) / lds)));
+    const int64_t groups = std::min<int64_t>(total, (int64_t)ctx->num_cu * per_cu);
+    hipLaunchKernelGGL((k_mpc_wave_group<kTeam, VS, GS, WPS>), dim3((unsigned)groups), dim3(kTeam), lds, st,
+                       ctx->d_group, count, total, counter);
+    HIP_OK(hipGetLastError());
+    return IMPC_OK;
+}
+
+// dynamic LDS bytes of the structured kernel for a shape (team VS, GS) and pattern (CG, n)
+size_t wave_lds_bytes(int vs, int gs, int CG, int n) {
+    auto sz = [&](auto ld) { return sizeof(double) * (size_t)decltype(ld)::size(CG, n); };
+    if (vs == kWaveVS)
+        return gs == 2 ? sz(impc::WaveLds<kTeam, kWaveVS, 2>{}) : gs == 3 ? sz(impc::WaveLds<kTeam, kWaveVS, 3>{})
+                                                                          : sz(impc::WaveLds<kTeam, kWaveVS, 4>{});
+    return gs == 2 ? sz(impc::WaveLds<kTeam, kWaveVSLong, 2>{}) : gs == 3 ? sz(impc::WaveLds<kTeam, kWaveVSLong, 3>{})
+                                                                          : sz(impc::WaveLds<kTeam, kWaveVSLong, 4>{});
+}
+
 int prepare_structured(impc_batch b) {
     b->ms.reset(new impc::MpcStructure());
     std::string why = b->ms->analyse(b->n, b->m, b->Pp.data(), b->Pi.data(), b->Ap.data(), b->Ai.data());
-    if (!why.empty() || b->ms->n > kTeam * kWaveVS || b->ms->CG > impc::WaveLds<kTeam, kWaveVS, 2>::CGM) {
+    if (!why.empty() || b->ms->n > kTeam * kWaveVSLong || b->ms->CG > impc::WaveLds<kTeam, kWaveVS, 2>::CGM) {
         b->structured_ok = false;
         return IMPC_OK;
     }
+    b->vs = b->ms->n <= kTeam * kWaveVS ? kWaveVS : kWaveVSLong;
     const int mg = b->ms->mg;
     b->gs = mg <= 2 * kTeam ? 2 : mg <= 3 * kTeam ? 3 : mg <= 4 * kTeam ? 4 : 0;
-    if (!b->gs) {
-        b->structured_ok = false;
+    if (!b->gs || wave_lds_bytes(b->vs, b->gs, b->ms->CG, b->ms->n) > 160 * 1024 - 1024) {
+        b->structured_ok = false;  // the generic kernel takes it
         return IMPC_OK;
     }
     const impc::MpcStructure &s = *b->ms;
@@ -663,6 +743,7 @@ int impc_ctx_destroy(impc_ctx ctx) {
     if (!ctx) return IMPC_OK;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->d_group) (void)hipFree(ctx->d_group);
     delete ctx;
     return IMPC_OK;
 }
@@ -854,6 +935,76 @@ int impc_batch_solve(impc_batch b, void *stream) {
     hipStream_t st = pick(b, stream);
     if (use_structured(b)) return structured_solve(b, st);
     return generic_solve(b, st);
+}
+
+int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
+    if (!bs || count < 1) return fail(IMPC_INVALID_ARGUMENT, "empty group");
+    impc_batch b0 = bs[0];
+    if (!b0) return fail(IMPC_INVALID_ARGUMENT, "null batch");
+    impc_ctx ctx = b0->ctx;
+    int gs = 0, maxCG = 1, maxN = 1;
+    for (int k = 0; k < count; k++) {
+        impc_batch b = bs[k];
+        if (!b || b->ctx != ctx) return fail(IMPC_INVALID_ARGUMENT, "group batches must share a context");
+        if (!b->values_set) return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "values not set");
+        if (!use_structured(b) || b->vs != b0->vs)
+            return fail(IMPC_UNSUPPORTED, "grouped solves need structured batches of one team shape");
+        gs = std::max(gs, b->gs);
+        maxCG = std::max(maxCG, b->ms->CG);
+        maxN = std::max(maxN, b->ms->n);
+    }
+    HIP_OK(hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    std::vector<GroupEntry> entries((size_t)count);
+    std::memset((void *)entries.data(), 0, sizeof(GroupEntry) * (size_t)count);  // comparable bytes
+    int64_t total = 0;
+    for (int k = 0; k < count; k++) {
+        impc_batch b = bs[k];
+        GroupEntry &e = entries[(size_t)k];
+        e.T = b->wt;
+        e.io = impc::WaveIO{b->B,        b->in_Px,  b->in_q,  b->in_Ax,  b->in_l,  b->in_u, b->in_xws, b->in_yws,
+                            b->has_ws ? 1 : 0, b->d_xout, b->d_yout, b->d_scal, b->d_info};
+        e.st = b->dst;
+        e.first = total;
+        total += b->B;
+        b->ev_solve = false;
+        b->ev_setup = false;
+    }
+    if (total == 0) return IMPC_OK;
+    // upload the entries only when they change (repeated solves of one group launch back to back);
+    // the device copy must not change under an in-flight kernel, so an update waits for the stream
+    const bool same = ctx->h_group.size() == entries.size() &&
+                      std::memcmp(ctx->h_group.data(), entries.data(), sizeof(GroupEntry) * (size_t)count) == 0;
+    if (!same) {
+        HIP_OK(hipStreamSynchronize(st));
+        if (count > ctx->group_cap) {
+            if (ctx->d_group) HIP_OK(hipFree(ctx->d_group));
+            ctx->d_group = nullptr;
+            HIP_OK(hipMalloc((void **)&ctx->d_group, sizeof(GroupEntry) * (size_t)count));
+            ctx->group_cap = count;
+        }
+        HIP_OK(hipMemcpy(ctx->d_group, entries.data(), sizeof(GroupEntry) * (size_t)count, hipMemcpyHostToDevice));
+        ctx->h_group = entries;
+    }
+    HIP_OK(hipMemsetAsync(b0->d_counter, 0, 256, st));
+    if (b0->profile) HIP_OK(hipEventRecord(b0->ev[2], st));
+    int rc;
+    switch (b0->vs * 8 + gs) {
+        case kWaveVS * 8 + 2: rc = launch_group<kWaveVS, 2>(ctx, st, count, total, maxCG, maxN, b0->d_counter); break;
+        case kWaveVS * 8 + 3: rc = launch_group<kWaveVS, 3>(ctx, st, count, total, maxCG, maxN, b0->d_counter); break;
+        case kWaveVS * 8 + 4: rc = launch_group<kWaveVS, 4>(ctx, st, count, total, maxCG, maxN, b0->d_counter); break;
+        case kWaveVSLong * 8 + 2: rc = launch_group<kWaveVSLong, 2>(ctx, st, count, total, maxCG, maxN, b0->d_counter); break;
+        case kWaveVSLong * 8 + 3: rc = launch_group<kWaveVSLong, 3>(ctx, st, count, total, maxCG, maxN, b0->d_counter); break;
+        case kWaveVSLong * 8 + 4: rc = launch_group<kWaveVSLong, 4>(ctx, st, count, total, maxCG, maxN, b0->d_counter); break;
+        default: return fail(IMPC_UNSUPPORTED, "no structured kernel for this size");
+    }
+    if (rc) return rc;
+    if (b0->profile) {
+        HIP_OK(hipEventRecord(b0->ev[3], st));
+        HIP_OK(hipEventRecord(b0->ev[4], st));
+        b0->ev_solve = true;
+    }
+    return IMPC_OK;
 }
 
 int impc_batch_get(impc_batch b, double *x, double *y, impc_info *info) {

@@ -96,15 +96,17 @@ struct WaveLds {
     static constexpr int GSLOT_OFF = JUNK_OFF + NL;         // int16 [4 NL GS]: general entry -> product slot
     static constexpr int P_OFF = GSLOT_OFF + NL * GS;       // products, column-slot layout (size below)
     static constexpr int CGM = 24;                          // max general entries per column
-    // products region: entry t of column v at t * NMAX + v (t < CG rounded up to 4), so a column's
-    // gather is CG4 independent conflict-free reads; it doubles as the factorisation's (4g + e)
-    // scratch.  Sized from the pattern at run time, followed by 8 discard slots (index p_size).
+    // products region: entry t of column v at t * stride(n) + v (stride = n rounded up to 64), so a
+    // column's gather is CG4 independent conflict-free reads; it doubles as the factorisation's
+    // (4g + e) scratch.  Sized from the pattern at run time, followed by 8 discard slots (index
+    // p_size).
     static IMPC_WF int cg4(int CG) { return (CG + 3) & ~3; }
-    static IMPC_WF int p_size(int CG) {
-        const int c = cg4(CG) * NMAX, f = 4 * NL * GS;
+    static IMPC_WF int stride(int n) { return (n + 63) & ~63; }
+    static IMPC_WF int p_size(int CG, int n) {
+        const int c = cg4(CG) * stride(n), f = 4 * NL * GS;
         return c > f ? c : f;
     }
-    static IMPC_WF int size(int CG) { return P_OFF + p_size(CG) + 8; }
+    static IMPC_WF int size(int CG, int n) { return P_OFF + p_size(CG, n) + 8; }
     // factorisation aliases (inside R..X region and the products buffer)
     static constexpr int FA = R_OFF, FL = FA + 169, FI = FL + 169, FB = FI + 169, FG = FB + 104, FE = FG + 104,
                          RHOG = FE + 64, DIAGX = RHOG + NL * GS;
@@ -232,7 +234,7 @@ struct WaveQP {
             z[s] = y[s] = lg[s] = ug[s] = dyg[s] = 0.0;
             gt[s] = 0;
             const int16_t *gs = (const int16_t *)(lds + LD::GSLOT_OFF);
-            const int pz = LD::p_size(T.CG);
+            const int pz = LD::p_size(T.CG, T.n);
             _Pragma("unroll") for (int e = 0; e < 4; e++) {
                 a[s][e] = 0.0;
                 gc[s][e] = (pz << 16) | LD::NMAX;  // discard slot / zero tail of the x exchange
@@ -257,21 +259,21 @@ struct WaveQP {
     // the discard slot), and a zeroed products region (slots no entry maps to must read 0).
     static IMPC_WF void load_tables(WV &w, const WaveTables &T, double *lds) {
         int16_t *gs = (int16_t *)(lds + LD::GSLOT_OFF);
-        const int pz = LD::p_size(T.CG);
+        const int pz = LD::p_size(T.CG, T.n);
         for (int e = w.lane(); e < 4 * NL * GS; e += NL) gs[e] = (int16_t)pz;
         double *pb = lds + LD::P_OFF;
         for (int e = w.lane(); e < pz + 8; e += NL) pb[e] = 0.0;
         w.sync();
         for (int e = w.lane(); e < T.n * T.CG; e += NL) {
             const int v = e / T.CG, t = e % T.CG, id = T.colg[e];
-            if (id >= 0) gs[id] = (int16_t)(t * LD::NMAX + v);
+            if (id >= 0) gs[id] = (int16_t)(t * LD::stride(T.n) + v);
         }
         w.sync();
     }
 
     IMPC_WF void zero_products() {
         double *pb = pbuf();
-        const int cnt = LD::p_size(T.CG) + 8;
+        const int cnt = LD::p_size(T.CG, T.n) + 8;
         for (int i = L; i < cnt; i += NL) pb[i] = 0.0;
         wv.sync();
     }
@@ -283,20 +285,19 @@ struct WaveQP {
     // gather sum over the general entries of column v (column-slot layout, independent reads)
     IMPC_WF double col_gather(int v) {
         const double *pb = pbuf() + v;
-        const int C4 = LD::cg4(T.CG);
+        const int C4 = LD::cg4(T.CG), sd = LD::stride(T.n);
         double s = 0.0;
         for (int t = 0; t < C4; t += 4) {
-            const double p0 = pb[t * LD::NMAX], p1 = pb[(t + 1) * LD::NMAX], p2 = pb[(t + 2) * LD::NMAX],
-                         p3 = pb[(t + 3) * LD::NMAX];
+            const double p0 = pb[t * sd], p1 = pb[(t + 1) * sd], p2 = pb[(t + 2) * sd], p3 = pb[(t + 3) * sd];
             s += (p0 + p1) + (p2 + p3);
         }
         return s;
     }
     IMPC_WF double col_gather_max(int v) {
         const double *pb = pbuf() + v;
-        const int C4 = LD::cg4(T.CG);
+        const int C4 = LD::cg4(T.CG), sd = LD::stride(T.n);
         double s = 0.0;
-        for (int t = 0; t < C4; t++) s = dmax(pb[t * LD::NMAX], s);
+        for (int t = 0; t < C4; t++) s = dmax(pb[t * sd], s);
         return s;
     }
 

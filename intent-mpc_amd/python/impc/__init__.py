@@ -113,6 +113,7 @@ _sig("impc_batch_get_perm", C.c_int, _P, _i64p)
 _sig("impc_batch_set_profiling", C.c_int, _P, C.c_int)
 _sig("impc_batch_get_timings", C.c_int, _P, _dp, _dp, _dp)
 _sig("impc_batch_set_kernel", C.c_int, _P, C.c_int)
+_sig("impc_batch_solve_group", C.c_int, C.POINTER(_P), C.c_int, _P)
 _sig("impc_device_alloc", C.c_int, _P, C.c_int64, C.POINTER(_P))
 _sig("impc_device_free", C.c_int, _P, _P)
 _sig("impc_copy_to_device", C.c_int, _P, _P, _P, C.c_int64)
@@ -148,7 +149,7 @@ EXPORTED = [
     "impc_batch_set_values", "impc_batch_set_values_device", "impc_batch_warm_start", "impc_batch_setup",
     "impc_batch_solve", "impc_batch_get", "impc_batch_device_results", "impc_batch_update_lin_cost",
     "impc_batch_update_bounds", "impc_batch_get_stats", "impc_batch_get_perm", "impc_batch_set_profiling",
-    "impc_batch_get_timings", "impc_batch_set_kernel", "impc_device_alloc", "impc_device_free",
+    "impc_batch_get_timings", "impc_batch_set_kernel", "impc_batch_solve_group", "impc_device_alloc", "impc_device_free",
     "impc_copy_to_device", "impc_copy_to_host", "impc_select_best", "impc_select_best_device", "impc_mpc_dims",
     "impc_mpc_build_pattern", "impc_mpc_build_values", "impc_mpc_warm_start", "impc_mpc_builder_create",
     "impc_mpc_builder_destroy", "impc_mpc_build_values_device",
@@ -445,3 +446,9 @@ class DeviceArray:
         if self.ptr:
             lib.impc_device_free(self.ctx.h, _P(self.ptr))
             self.ptr = None
+
+
+def solve_group(batches, stream=None):
+    """impc_batch_solve_group: one persistent launch over several structured batches."""
+    arr = (_P * len(batches))(*[b.h for b in batches])
+    _check(lib.impc_batch_solve_group(arr, len(batches), _P(stream) if stream else None), "impc_batch_solve_group")

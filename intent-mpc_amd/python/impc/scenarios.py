@@ -116,7 +116,8 @@ def intent_config(N=20, K=8, instances=8192, hyps=8, seed=3000, params=None):
     clear = 0.4 + pd["dynamic_safety_dist"]
     for _ in range(64):
         am = np.argmax(prob, axis=2)
-        track = np.take_along_axis(pred, am[:, :, None, None, None], axis=2)[:, :, 0, :N]   # [I, K, N, 3]
+        steps = np.minimum(np.arange(N), pred.shape[3] - 1)  # prediction clamped to .back() (:1165-1184)
+        track = np.take_along_axis(pred, am[:, :, None, None, None], axis=2)[:, :, 0][:, :, steps]  # [I, K, N, 3]
         bad = (np.linalg.norm(track - prev[:, None, :, :3], axis=3) < clear).any(axis=2)   # [I, K]
         if not bad.any():
             break

@@ -93,7 +93,7 @@ struct EmuWave {
 template <int VS, int GS>
 void run(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSettings &st) {
     using LD = impc::WaveLds<NL, VS, GS>;
-    std::vector<double> lds((size_t)LD::size(T.CG), 0.0);
+    std::vector<double> lds((size_t)LD::size(T.CG, T.n), 0.0);
     EmuShared sh;
     std::vector<std::thread> th;
     for (int l = 0; l < NL; l++)
@@ -141,15 +141,16 @@ extern "C" int emu_wave_solve_batch(int64_t n, int64_t m, const int64_t *Pp, con
     st.scaled_termination = (int32_t)s->scaled_termination;
     st.check_termination = (int32_t)s->check_termination;
     st.warm_start = (int32_t)s->warm_start;
-    if (ms.n > NL || ms.CG > impc::WaveLds<NL, 1, 2>::CGM)
-        return 2;
-    if (ms.mg <= 2 * NL)
-        run<1, 2>(T, io, st);
-    else if (ms.mg <= 3 * NL)
-        run<1, 3>(T, io, st);
-    else if (ms.mg <= 4 * NL)
-        run<1, 4>(T, io, st);
-    else
-        return 2;
+    if (ms.n > 3 * NL || ms.CG > impc::WaveLds<NL, 1, 2>::CGM || ms.mg > 4 * NL) return 2;
+    const int gs = ms.mg <= 2 * NL ? 2 : ms.mg <= 3 * NL ? 3 : 4;
+    if (ms.n <= NL) {  // the product's shapes (impc_qp.hip kWaveVS / kWaveVSLong)
+        if (gs == 2) run<1, 2>(T, io, st);
+        else if (gs == 3) run<1, 3>(T, io, st);
+        else run<1, 4>(T, io, st);
+    } else {
+        if (gs == 2) run<3, 2>(T, io, st);
+        else if (gs == 3) run<3, 3>(T, io, st);
+        else run<3, 4>(T, io, st);
+    }
     return 0;
 }

@@ -76,3 +76,10 @@ def test_structured_emulation_short_horizons(N):
     cfg = scenarios.static_config(N=N, K=2, batch=1, identical=False, seed=1300 + N)
     s = impc.default_settings(**S25)
     compare(emulate(cfg, s), oracle(cfg, s))
+
+
+def test_structured_emulation_long_horizon():
+    """N=40 (n=515): the three-slot team shape of the structured kernel."""
+    cfg = take(scenarios.intent_config(N=40, K=10, instances=1, seed=4040)[10], 1)
+    s = impc.default_settings(**S25)
+    compare(emulate(cfg, s), oracle(cfg, s))
