@@ -36,7 +36,13 @@ def run(ctx, name, cfgs, steps, settings):
         batches.append(b)
     total = sum(b.B for b in batches)
 
+    shapes = {b.stats()["kernel"] for b in batches}
+    grouped = len(batches) > 1 and shapes == {impc.KERNEL_STRUCTURED} and len({b.n > 256 for b in batches}) == 1
+
     def step():
+        if grouped:  # one persistent launch over all pattern buckets
+            impc.solve_group(batches)
+            return
         for b in batches:
             b.setup()
             b.solve()
@@ -53,7 +59,8 @@ def run(ctx, name, cfgs, steps, settings):
     for b in batches:
         b.close()
     return {"config": name, "qps": total, "steps": steps, "ms_per_step": 1000 * el / steps,
-            "qp_solves_per_s": total * steps / el, "mean_iter": float(iters.mean()), "kernels": kernels}
+            "qp_solves_per_s": total * steps / el, "mean_iter": float(iters.mean()), "kernels": kernels,
+            "launch": "grouped" if grouped else "per batch"}
 
 
 def main():
@@ -76,7 +83,7 @@ def main():
         if K == 0:
             cfg4.append(scenarios.first_call_config(batch=cnt, seed=4100))
         else:
-            b = scenarios.intent_config(N=20, K=K, instances=(cnt + 7) // 8, hyps=8, seed=4200 + K)
+            b = scenarios.intent_config(N=20, K=K, instances=cnt // 6 + 1, hyps=8, seed=4200 + K)
             bk = b[K]
             take = min(cnt, bk["values"]["q"].shape[0])
             cfg4.append(dict(pattern=bk["pattern"], values={k: v[:take] for k, v in bk["values"].items()},

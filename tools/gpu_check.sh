@@ -28,3 +28,9 @@ if [ -n "${PMC:-}" ]; then
   timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/gpurun_out/pmc_write" -o pmc -- python3 "$R/bench.py" --steps 1 --warmup 0 --cpu-sample 0 > "$R/gpurun_out/pmc_write.log" 2>&1 || { tail -30 "$R/gpurun_out/pmc_write.log"; exit 1; }
   python3 "$R/tools/pmc_summary.py" "$R/gpurun_out/pmc_fetch" "$R/gpurun_out/pmc_write" k_mpc_wave_group 65536 > "$R/gpurun_out/pmc_k_solve.json" && cat "$R/gpurun_out/pmc_k_solve.json"
 fi
+if [ -n "${CONFIGS:-}" ]; then
+  step configs
+  cd "$R" || exit 1
+  timeout -k 10 600 python3 tools/bench_configs.py --steps 3 > gpurun_out/configs.log 2>&1 || { tail -30 gpurun_out/configs.log; exit 1; }
+  cat gpurun_out/configs.log
+fi
