@@ -197,8 +197,9 @@ struct GpuTeam {
     }
     template <int CTRL>
     __device__ static double dpp(double v) {
-        int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-        int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+        // every control used reads a valid lane of the same row: no "old" operand to initialise
+        int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+        int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
         return __hiloint2double(hi, lo);
     }
     // sum over lanes {8i, .., 8i+7}: quad_perm xor 1, quad_perm xor 2, row_half_mirror.  Every

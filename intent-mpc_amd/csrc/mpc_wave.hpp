@@ -84,6 +84,9 @@ template <int NL, int VS, int GS>
 struct WaveLds {
     static constexpr int NMAX = NL * VS;
     static constexpr int WMAX = (NMAX + 5) / 13 - 1;       // max control stages
+    // stage count whose recursions are fully unrolled (the reference's default horizon N = 20
+    // for the one-variable-per-lane shape, N = 40 for the long-horizon shape)
+    static constexpr int WSPEC = VS == 1 ? 19 : 39;
     // exchange vector length: zero tail past NMAX, and room for the factorisation scratch
     static constexpr int NP = (NMAX + 192 > (779 + NL * GS + NMAX + 3) / 4) ? NMAX + 192 : (779 + NL * GS + NMAX + 3) / 4;
     static constexpr int F_OFF = 0;                         // [WMAX][64]
@@ -534,39 +537,132 @@ struct WaveQP {
     }
 
     // One step of a stage recursion on the 8x8 lane grid: returns c - R(F v), R the strided
-    // (STRIDE) or contiguous 8-lane sum, and stores it at dst (a discard slot for non-writers).
+    // (STRIDE) or contiguous 8-lane sum.
     template <bool STRIDE>
-    IMPC_WF double rstep(double f, double c, double v, double *dst) {
+    IMPC_WF double rstep(double f, double c, double v) {
         const double p = prod_nc(f, v);
-        const double r = c - (STRIDE ? wv.sum_stride8(p) : wv.sum_contig8(p));
-        *dst = r;
-        return r;
+        return c - (STRIDE ? wv.sum_stride8(p) : wv.sum_contig8(p));
+    }
+
+    // Sweeps with a compile-time step count WC (= WSPEC) are fully unrolled: every LDS wait is
+    // exact and the step results stay in registers until the sweep ends, instead of an LDS store
+    // per step whose completion the next step's wait would include (measured 195 -> 157 cycles
+    // per step, tools/probe/recur_probe.hip).  Step m's result sits in the 8 lanes sharing its
+    // output index; of those the lane whose other index is (m/2) mod 8 keeps it, in slot m/16 of
+    // the even- or odd-step array (a compile-time lane mask, one v_cndmask pair per step).
+    static constexpr int CQ = LD::WSPEC / 16 + 1;
+    IMPC_WF static void cap(double (&c)[CQ], double r, int m, int other) {
+        if (((m >> 1) & 7) == other) c[m >> 4] = r;
+    }
+    // Store a sweep's W captured steps: even steps' outputs sit at index j (EJ) or i, odd steps'
+    // at the other; step m is stage m + 1 (forward) or W - 1 - m (backward).
+    template <bool EJ>
+    IMPC_WF static void cap_store(const double (&c0)[CQ], const double (&c1)[CQ], double *buf, int W, bool fwd,
+                                  int i, int j) {
+        const int o0 = EJ ? i : j, e0 = EJ ? j : i;
+        _Pragma("unroll") for (int q = 0; q < CQ; q++) {
+            const int m0 = 16 * q + 2 * o0, m1 = 16 * q + 2 * e0 + 1;
+            if (m0 < W) buf[13 * (fwd ? m0 + 1 : W - 1 - m0) + e0] = c0[q];
+            if (m1 < W) buf[13 * (fwd ? m1 + 1 : W - 1 - m1) + o0] = c1[q];
+        }
+    }
+
+    // S2 body: a_{k+1} = t_{k+1} - F_k a_k for k = 0..W-1 (WC = W, or 0 for a runtime W).
+    template <int WC>
+    IMPC_WF void fwd_sweep(const double *tb, double *rb, int W) {
+        const double *Fm = lds + LD::F_OFF;
+        const int l = L & 63, i = l >> 3, j = l & 7;
+        double a = tb[i];
+        // (F, t) of the next even / odd step, loaded two steps ahead (reads past the last stage
+        // stay inside the LDS buffers and are never used)
+        double fe = Fm[l], te = tb[13 + j], fo = Fm[64 + l], to = tb[26 + i];
+        if constexpr (WC > 0) {
+            double c0[CQ], c1[CQ];
+            _Pragma("unroll") for (int q = 0; q < CQ; q++) c0[q] = c1[q] = 0.0;
+            _Pragma("unroll") for (int k = 0; k < WC; k += 2) {
+                const double f0 = fe, t0 = te;
+                fe = Fm[64 * (k + 2) + l];
+                te = tb[13 * (k + 3) + j];
+                a = rstep<true>(f0, t0, a);
+                cap(c0, a, k, i);
+                if (k + 1 < WC) {
+                    const double f1 = fo, t1 = to;
+                    fo = Fm[64 * (k + 3) + l];
+                    to = tb[13 * (k + 4) + i];
+                    a = rstep<false>(f1, t1, a);
+                    cap(c1, a, k + 1, j);
+                }
+            }
+            cap_store<true>(c0, c1, rb, WC, true, i, j);
+        } else {
+            // one lane per element writes, the rest write to discard slots (no divergent branch)
+            double *junk = lds + LD::JUNK_OFF + L;
+            const bool wri = j == 0, wrj = i == 0;
+            for (int k = 0; k < W; k += 2) {
+                const double f0 = fe, t0 = te;
+                fe = Fm[64 * (k + 2) + l];
+                te = tb[13 * (k + 3) + j];
+                a = rstep<true>(f0, t0, a);
+                *(wrj ? rb + 13 * (k + 1) + j : junk) = a;
+                if (k + 1 >= W) break;
+                const double f1 = fo, t1 = to;
+                fo = Fm[64 * (k + 3) + l];
+                to = tb[13 * (k + 4) + i];
+                a = rstep<false>(f1, t1, a);
+                *(wri ? rb + 13 * (k + 2) + i : junk) = a;
+            }
+        }
     }
 
     // S4 body for a first step k = W-1 of parity ODD: steps alternate strided (odd k) and
-    // contiguous (even k) reductions; x_k sits at index j (odd k) / i (even k).
-    template <bool ODD>
+    // contiguous (even k) reductions; x_k sits at index j (odd k) / i (even k).  WC as above.
+    template <bool ODD, int WC>
     IMPC_WF void bwd_sweep(const double *eb, double *xb, int W) {
         const double *Fm = lds + LD::F_OFF;
         const int l = L & 63, i = l >> 3, j = l & 7;
-        double *junk = lds + LD::JUNK_OFF + L;
-        const bool wri = j == 0, wrj = i == 0;
+        if constexpr (WC > 0) W = WC;
         // x_W: W = (W-1)+1 has the opposite parity of the first step
         double x = eb[13 * W + (ODD ? i : j)];
         const int k1 = W - 2 > 0 ? W - 2 : 0;
         double fa = Fm[64 * (W - 1) + l], ea = eb[13 * (W - 1) + (ODD ? j : i)];
         double fb = Fm[64 * k1 + l], ebv = eb[13 * k1 + (ODD ? i : j)];
-        for (int k = W - 1; k >= 0; k -= 2) {
-            const int k2 = k - 2 > 0 ? k - 2 : 0, k3 = k - 3 > 0 ? k - 3 : 0;
-            const double f0 = fa, e0 = ea;
-            fa = Fm[64 * k2 + l];
-            ea = eb[13 * k2 + (ODD ? j : i)];
-            x = rstep<ODD>(f0, e0, x, ODD ? (wrj ? xb + 13 * k + j : junk) : (wri ? xb + 13 * k + i : junk));
-            if (k - 1 < 0) break;
-            const double f1 = fb, e1 = ebv;
-            fb = Fm[64 * k3 + l];
-            ebv = eb[13 * k3 + (ODD ? i : j)];
-            x = rstep<!ODD>(f1, e1, x, ODD ? (wri ? xb + 13 * (k - 1) + i : junk) : (wrj ? xb + 13 * (k - 1) + j : junk));
+        if constexpr (WC > 0) {
+            double c0[CQ], c1[CQ];
+            _Pragma("unroll") for (int q = 0; q < CQ; q++) c0[q] = c1[q] = 0.0;
+            _Pragma("unroll") for (int m = 0; m < WC; m += 2) {
+                const int k = WC - 1 - m;
+                const int k2 = k - 2 > 0 ? k - 2 : 0, k3 = k - 3 > 0 ? k - 3 : 0;
+                const double f0 = fa, e0 = ea;
+                fa = Fm[64 * k2 + l];
+                ea = eb[13 * k2 + (ODD ? j : i)];
+                x = rstep<ODD>(f0, e0, x);
+                cap(c0, x, m, ODD ? i : j);
+                if (m + 1 < WC) {
+                    const double f1 = fb, e1 = ebv;
+                    fb = Fm[64 * k3 + l];
+                    ebv = eb[13 * k3 + (ODD ? i : j)];
+                    x = rstep<!ODD>(f1, e1, x);
+                    cap(c1, x, m + 1, ODD ? j : i);
+                }
+            }
+            cap_store<ODD>(c0, c1, xb, WC, false, i, j);
+        } else {
+            double *junk = lds + LD::JUNK_OFF + L;
+            const bool wri = j == 0, wrj = i == 0;
+            for (int k = W - 1; k >= 0; k -= 2) {
+                const int k2 = k - 2 > 0 ? k - 2 : 0, k3 = k - 3 > 0 ? k - 3 : 0;
+                const double f0 = fa, e0 = ea;
+                fa = Fm[64 * k2 + l];
+                ea = eb[13 * k2 + (ODD ? j : i)];
+                x = rstep<ODD>(f0, e0, x);
+                *(ODD ? (wrj ? xb + 13 * k + j : junk) : (wri ? xb + 13 * k + i : junk)) = x;
+                if (k - 1 < 0) break;
+                const double f1 = fb, e1 = ebv;
+                fb = Fm[64 * k3 + l];
+                ebv = eb[13 * k3 + (ODD ? i : j)];
+                x = rstep<!ODD>(f1, e1, x);
+                *(ODD ? (wri ? xb + 13 * (k - 1) + i : junk) : (wrj ? xb + 13 * (k - 1) + j : junk)) = x;
+            }
         }
     }
 
@@ -585,7 +681,7 @@ struct WaveQP {
     // --------------------------------------------------------------- one ADMM iteration
     IMPC_WF void iterate(bool need_delta) {
         const int n = T.n, W = T.W;
-        double *rb = rbuf(), *tb = tbuf(), *eb = ebuf(), *xb = xbuf(), *Fm = F();
+        double *rb = rbuf(), *tb = tbuf(), *eb = ebuf(), *xb = xbuf();
         const double sigma = st.sigma, alpha = st.alpha, oma = (double)1.0 - st.alpha;
         // rhs = sigma x - q + A' v   (stage order)
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
@@ -618,28 +714,13 @@ struct WaveQP {
         // over i (strided: DPP row_ror 8, permlane16/32 swaps) and odd steps over j (contiguous
         // DPP), all in the VALU, with no transpose.  The next F and t are loaded two steps ahead.
         // One wavefront of the team (rw) runs it -- the others go straight to the barrier and
-        // leave their SIMD's issue slots to the co-resident team; one lane per element writes,
-        // the rest write to discard slots (no divergent branch).
+        // leave their SIMD's issue slots to the co-resident team.
         if (L < 8) rb[L] = tb[L];
         if ((L >> 6) == rw) {
-            const int l = L & 63, i = l >> 3, j = l & 7;
-            double *junk = lds + LD::JUNK_OFF + L;
-            const bool wri = j == 0, wrj = i == 0;
-            double a = tb[i];
-            // (F, t) of the next even / odd step, loaded two steps ahead (reads past the last
-            // stage stay inside the LDS buffers and are never used)
-            double fe = Fm[l], te = tb[13 + j], fo = Fm[64 + l], to = tb[26 + i];
-            for (int k = 0; k < W; k += 2) {
-                const double f0 = fe, t0 = te;
-                fe = Fm[64 * (k + 2) + l];
-                te = tb[13 * (k + 3) + j];
-                a = rstep<true>(f0, t0, a, wrj ? rb + 13 * (k + 1) + j : junk);
-                if (k + 1 >= W) break;
-                const double f1 = fo, t1 = to;
-                fo = Fm[64 * (k + 3) + l];
-                to = tb[13 * (k + 4) + i];
-                a = rstep<false>(f1, t1, a, wri ? rb + 13 * (k + 2) + i : junk);
-            }
+            if (W == LD::WSPEC)
+                fwd_sweep<LD::WSPEC>(tb, rb, W);
+            else
+                fwd_sweep<0>(tb, rb, W);
         }
         wv.sync();
         IMPC_SEC(kSecFwd);
@@ -657,10 +738,12 @@ struct WaveQP {
         // stored layout: even steps reduce over j (contiguous), odd steps over i (strided).
         if (L < 8) xb[13 * W + L] = eb[13 * W + L];
         if ((L >> 6) == rw) {
-            if ((W - 1) & 1)
-                bwd_sweep<true>(eb, xb, W);
+            if (W == LD::WSPEC)
+                bwd_sweep<((LD::WSPEC - 1) & 1) != 0, LD::WSPEC>(eb, xb, W);
+            else if ((W - 1) & 1)
+                bwd_sweep<true, 0>(eb, xb, W);
             else
-                bwd_sweep<false>(eb, xb, W);
+                bwd_sweep<false, 0>(eb, xb, W);
         }
         wv.sync();
         IMPC_SEC(kSecBwd);
