@@ -25,7 +25,7 @@ HARNESS := $(HARNDIR)/libimpc_core_cpu.so
 EMU     := $(HARNDIR)/libwave_emu.so
 SHIMT   := $(HARNDIR)/shim_test
 
-.PHONY: all lib oracle harness prof clean
+.PHONY: all lib oracle harness prof variant clean
 all: lib oracle harness
 lib: $(LIB)
 oracle: $(ORACLE)
@@ -82,6 +82,12 @@ $(SHIMT): $(ROOT)/tests/native/shim_test.cpp $(ROOT)/include/OsqpEigen/OsqpEigen
 	@mkdir -p $(HARNDIR)
 	$(CXX) -O2 -std=c++17 -Wall -I$(ROOT)/tests/native/mock_eigen -I$(ROOT)/include $< -L$(LIBDIR) -limpc_qp \
 		-Wl,-rpath,'$$ORIGIN/../../../intent-mpc_amd/lib' -o $@
+
+# kernel experiments (tools/ only): make variant V=name DEFS="-DX=1" -> lib/libimpc_qp_<name>.so,
+# selected at run time with IMPC_LIB_VARIANT=<name>
+variant: $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(CSRC)/impc_qp.hip -o $(LIBDIR)/impc_qp_$(V).o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(LIBDIR)/impc_qp_$(V).o $^ -o $(LIBDIR)/libimpc_qp_$(V).so
 
 clean:
 	rm -rf $(LIBDIR) $(ORADIR) $(HARNDIR)

@@ -40,6 +40,17 @@ namespace impc {
 
 #define IMPC_WF __host__ __device__ __forceinline__
 
+// Phase-cost experiments (tools/exp.sh only): IMPC_DUP=<section id> runs that idempotent phase of
+// the ADMM iteration twice; the bench's time difference is the phase's marginal cost.
+#ifndef IMPC_DUP
+#define IMPC_DUP -1
+#endif
+#define IMPC_REP(X) for (int rep_ = 0; rep_ < (IMPC_DUP == (X) ? 2 : 1); rep_++)
+
+#ifndef IMPC_PSTRIDE_PAD
+#define IMPC_PSTRIDE_PAD 1
+#endif
+
 struct WaveTables {
     int32_t n, m, mg, N, W, CG, nnzP, nnzA;
     const int32_t *var_orig, *var_pdiag, *var_boxrow, *var_boxpos;
@@ -104,7 +115,10 @@ struct WaveLds {
     // (4g + e) scratch.  Sized from the pattern at run time, followed by 8 discard slots (index
     // p_size).
     static IMPC_WF int cg4(int CG) { return (CG + 3) & ~3; }
-    static IMPC_WF int stride(int n) { return (n + 63) & ~63; }
+    // +PAD: the obstacle rows of one stage write their products to the same column in different
+    // entry slots; a stride that is not a multiple of 16 doubles puts those ds_write_b64 (bank =
+    // dword mod 32, 16-lane groups) on distinct banks.  Reads stay lane-contiguous.
+    static IMPC_WF int stride(int n) { return ((n + 63) & ~63) + IMPC_PSTRIDE_PAD; }
     static IMPC_WF int p_size(int CG, int n) {
         const int c = cg4(CG) * stride(n), f = 4 * NL * GS;
         return c > f ? c : f;
@@ -683,79 +697,91 @@ struct WaveQP {
         const int n = T.n, W = T.W;
         double *rb = rbuf(), *tb = tbuf(), *eb = ebuf(), *xb = xbuf();
         const double sigma = st.sigma, alpha = st.alpha, oma = (double)1.0 - st.alpha;
-        // rhs = sigma x - q + A' v   (stage order)
-        _Pragma("unroll") for (int s = 0; s < VS; s++) {
-            if (!vok[s]) continue;
-            int v = NL * s + L;
-            double vb = rhob[s] * zb[s] - yb[s];
-            double r = sigma * x[s] - q[s];
-            r += ab[s] * vb;
-            r += col_gather(v);
-            rb[v] = r;
-        }
-        wv.sync();
-        IMPC_SEC(kSecRhs);
-        // S1: t_k = r_k[:8] - G_{k-1}[:, 8:] r_{k-1}[8:]
-        _Pragma("unroll") for (int s = 0; s < VS; s++) {
-            if (!vok[s] || vr_[s] >= 8) continue;
-            int v = NL * s + L;
-            double t = rb[v];
-            if (vs_[s] > 0) {
-                const double *rp = rb + 13 * (vs_[s] - 1) + 8;
-                _Pragma("unroll") for (int cc = 0; cc < 5; cc++) t -= cp[s][cc] * rp[cc];
+        IMPC_REP(kSecRhs) {
+            // rhs = sigma x - q + A' v   (stage order)
+            _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                if (!vok[s]) continue;
+                int v = NL * s + L;
+                double vb = rhob[s] * zb[s] - yb[s];
+                double r = sigma * x[s] - q[s];
+                r += ab[s] * vb;
+                r += col_gather(v);
+                rb[v] = r;
             }
-            tb[v] = t;
+            wv.sync();
         }
-        wv.sync();
+        IMPC_SEC(kSecRhs);
+        IMPC_REP(kSecS1) {
+            // S1: t_k = r_k[:8] - G_{k-1}[:, 8:] r_{k-1}[8:]
+            _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                if (!vok[s] || vr_[s] >= 8) continue;
+                int v = NL * s + L;
+                double t = rb[v];
+                if (vs_[s] > 0) {
+                    const double *rp = rb + 13 * (vs_[s] - 1) + 8;
+                    _Pragma("unroll") for (int cc = 0; cc < 5; cc++) t -= cp[s][cc] * rp[cc];
+                }
+                tb[v] = t;
+            }
+            wv.sync();
+        }
         IMPC_SEC(kSecS1);
-        // S2: forward 8-dim recursion a_{k+1} = t_{k+1} - F_k a_k on the 8x8 lane grid of each
-        // wavefront (lane l = 8i + j).  Vectors of even stages sit at index i, of odd stages at
-        // index j; F_k is stored as F_k[j][i] (k even) / F_k[i][j] (k odd), so even steps reduce
-        // over i (strided: DPP row_ror 8, permlane16/32 swaps) and odd steps over j (contiguous
-        // DPP), all in the VALU, with no transpose.  The next F and t are loaded two steps ahead.
-        // One wavefront of the team (rw) runs it -- the others go straight to the barrier and
-        // leave their SIMD's issue slots to the co-resident team.
-        if (L < 8) rb[L] = tb[L];
-        if ((L >> 6) == rw) {
-            if (W == LD::WSPEC)
-                fwd_sweep<LD::WSPEC>(tb, rb, W);
-            else
-                fwd_sweep<0>(tb, rb, W);
+        IMPC_REP(kSecFwd) {
+            // S2: forward 8-dim recursion a_{k+1} = t_{k+1} - F_k a_k on the 8x8 lane grid of each
+            // wavefront (lane l = 8i + j).  Vectors of even stages sit at index i, of odd stages at
+            // index j; F_k is stored as F_k[j][i] (k even) / F_k[i][j] (k odd), so even steps reduce
+            // over i (strided: DPP row_ror 8, permlane16/32 swaps) and odd steps over j (contiguous
+            // DPP), all in the VALU, with no transpose.  The next F and t are loaded two steps ahead.
+            // One wavefront of the team (rw) runs it -- the others go straight to the barrier and
+            // leave their SIMD's issue slots to the co-resident team.
+            if (L < 8) rb[L] = tb[L];
+            if ((L >> 6) == rw) {
+                if (W == LD::WSPEC)
+                    fwd_sweep<LD::WSPEC>(tb, rb, W);
+                else
+                    fwd_sweep<0>(tb, rb, W);
+            }
+            wv.sync();
         }
-        wv.sync();
         IMPC_SEC(kSecFwd);
-        // S3: e_k = Ahat_k^{-1} rhat_k
-        _Pragma("unroll") for (int s = 0; s < VS; s++) {
-            if (!vok[s]) continue;
-            const double *rk = rb + 13 * vs_[s];
-            double e = 0.0;
-            _Pragma("unroll") for (int cc = 0; cc < 13; cc++) e += ainv[s][cc] * rk[cc];
-            eb[NL * s + L] = e;
+        IMPC_REP(kSecS3) {
+            // S3: e_k = Ahat_k^{-1} rhat_k
+            _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                if (!vok[s]) continue;
+                const double *rk = rb + 13 * vs_[s];
+                double e = 0.0;
+                _Pragma("unroll") for (int cc = 0; cc < 13; cc++) e += ainv[s][cc] * rk[cc];
+                eb[NL * s + L] = e;
+            }
+            wv.sync();
         }
-        wv.sync();
         IMPC_SEC(kSecS3);
-        // S4: backward 8-dim recursion x_k[:8] = e_k[:8] - F_k' x_{k+1}[:8] on the same grid and
-        // stored layout: even steps reduce over j (contiguous), odd steps over i (strided).
-        if (L < 8) xb[13 * W + L] = eb[13 * W + L];
-        if ((L >> 6) == rw) {
-            if (W == LD::WSPEC)
-                bwd_sweep<((LD::WSPEC - 1) & 1) != 0, LD::WSPEC>(eb, xb, W);
-            else if ((W - 1) & 1)
-                bwd_sweep<true, 0>(eb, xb, W);
-            else
-                bwd_sweep<false, 0>(eb, xb, W);
+        IMPC_REP(kSecBwd) {
+            // S4: backward 8-dim recursion x_k[:8] = e_k[:8] - F_k' x_{k+1}[:8] on the same grid and
+            // stored layout: even steps reduce over j (contiguous), odd steps over i (strided).
+            if (L < 8) xb[13 * W + L] = eb[13 * W + L];
+            if ((L >> 6) == rw) {
+                if (W == LD::WSPEC)
+                    bwd_sweep<((LD::WSPEC - 1) & 1) != 0, LD::WSPEC>(eb, xb, W);
+                else if ((W - 1) & 1)
+                    bwd_sweep<true, 0>(eb, xb, W);
+                else
+                    bwd_sweep<false, 0>(eb, xb, W);
+            }
+            wv.sync();
         }
-        wv.sync();
         IMPC_SEC(kSecBwd);
-        // S5: controls x_k[8:] = e_k[8:] - G_k[:, 8:]' x_{k+1}[:8]
-        _Pragma("unroll") for (int s = 0; s < VS; s++) {
-            if (!vok[s] || vr_[s] < 8) continue;
-            const double *xn = xb + 13 * (vs_[s] + 1);
-            double t = eb[NL * s + L];
-            _Pragma("unroll") for (int j = 0; j < 8; j++) t -= cp[s][j] * xn[j];
-            xb[NL * s + L] = t;
+        IMPC_REP(kSecS5) {
+            // S5: controls x_k[8:] = e_k[8:] - G_k[:, 8:]' x_{k+1}[:8]
+            _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                if (!vok[s] || vr_[s] < 8) continue;
+                const double *xn = xb + 13 * (vs_[s] + 1);
+                double t = eb[NL * s + L];
+                _Pragma("unroll") for (int j = 0; j < 8; j++) t -= cp[s][j] * xn[j];
+                xb[NL * s + L] = t;
+            }
+            wv.sync();
         }
-        wv.sync();
         IMPC_SEC(kSecS5);
         // update_x and the box rows (update_z / project / update_y)
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
@@ -786,7 +812,7 @@ struct WaveQP {
         }
         wv.sync();
         IMPC_SEC(kSecUpdate);
-        write_v_products();
+        IMPC_REP(kSecProducts) write_v_products();
         IMPC_SEC(kSecProducts);
         (void)n;
     }

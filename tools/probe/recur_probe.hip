@@ -13,6 +13,10 @@
 //   6  as 1, recursion fully unrolled up to the maximum W (runtime W, break past it): exact
 //      waitcnts, exec-masked store of each stage
 //   7  as 6, stages captured in registers with compile-time lane masks, stored after the sweep
+//   8  row-broadcast form: lane l holds row (l & 7) of F_k (8 copies per wave), a_k lane i;
+//      the 8 operands by v_mov_b64_dpp row_newbcast, 4 mul + 4 fma + depth-2 adds in the lane;
+//      fully unrolled, captured in registers (copy l >> 3 keeps step m when m % 8 == l >> 3)
+//   9  as 8 with an LDS store of each stage by lanes 0..7 (runtime loop)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
@@ -54,6 +58,13 @@ __device__ double strided(double v) {
     v = pair_sum<false>(v);
     return pair_sum<true>(v);
 }
+template <int N>
+__device__ double nbc(double v) { return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + N, 0xF, 0xF, false); }
+__device__ double rowdot(const double (&f)[8], double a) {
+    const double s0 = fma(f[1], nbc<1>(a), f[0] * nbc<0>(a)), s1 = fma(f[3], nbc<3>(a), f[2] * nbc<2>(a));
+    const double s2 = fma(f[5], nbc<5>(a), f[4] * nbc<4>(a)), s3 = fma(f[7], nbc<7>(a), f[6] * nbc<6>(a));
+    return (s0 + s1) + (s2 + s3);
+}
 __device__ double prod_nc(double a, double b) {
     double p = a * b;
     asm volatile("" : "+v"(p));
@@ -79,7 +90,36 @@ __global__ void kr(double *o, unsigned long long *cyc, int Wr) {
     unsigned long long c0 = 0;
     for (int rep = -1; rep < REP; rep++) {
         if (rep == 0) c0 = __builtin_amdgcn_s_memtime();
-        if (MODE <= 3) {
+        if (MODE >= 8) {
+            const int r = l & 7, cp = l >> 3;
+            double a = tb[r], f[8], fn[8], tn = tb[13 + r];
+            double cap[3] = {0, 0, 0};
+            _Pragma("unroll") for (int q = 0; q < 8; q++) f[q] = Fm[8 * r + q];
+            if (MODE == 8) {
+                _Pragma("unroll") for (int k = 0; k < W; k++) {
+                    _Pragma("unroll") for (int q = 0; q < 8; q++) fn[q] = Fm[64 * (k + 1) + 8 * r + q];
+                    const double tc = tn;
+                    tn = tb[13 * (k + 2) + r];
+                    a = tc - rowdot(f, a);
+                    if ((k & 7) == cp) cap[k >> 3] = a;
+                    _Pragma("unroll") for (int q = 0; q < 8; q++) f[q] = fn[q];
+                }
+                _Pragma("unroll") for (int qq = 0; qq < 3; qq++) {
+                    const int k = 8 * qq + cp;
+                    if (k < W) rb[13 * (k + 1) + r] = cap[qq];
+                }
+            } else {
+                for (int k = 0; k < Wr; k++) {
+                    _Pragma("unroll") for (int q = 0; q < 8; q++) fn[q] = Fm[64 * (k + 1) + 8 * r + q];
+                    const double tc = tn;
+                    tn = tb[13 * (k + 2) + r];
+                    a = tc - rowdot(f, a);
+                    *(l < 8 ? rb + 13 * (k + 1) + r : jk) = a;
+                    _Pragma("unroll") for (int q = 0; q < 8; q++) f[q] = fn[q];
+                }
+            }
+            acc += a;
+        } else if (MODE <= 3) {
             constexpr bool BC = MODE >= 1;
             double co0 = 0, co1 = 0, ce0 = 0, ce1 = 0;
             double a = tb[i];
@@ -172,11 +212,11 @@ __global__ void kr(double *o, unsigned long long *cyc, int Wr) {
 
 int main() {
     double *o;
-    unsigned long long *c, h[8] = {};
+    unsigned long long *c, h[10] = {};
     if (hipMalloc(&o, 512 * sizeof(double)) || hipMalloc(&c, sizeof(h))) return 1;
     const char *nm[] = {"grid, update_dpp, store", "grid, mov_dpp, store", "grid, mov_dpp, capture",
                         "grid, mov_dpp, bare", "broadcast, store", "broadcast, bare", "unrolled, masked store",
-                        "unrolled, const-mask capture"};
+                        "unrolled, const-mask capture", "row-bcast, unrolled capture", "row-bcast, store"};
     for (int threads : {64, 512}) {
         for (int it = 0; it < 2; it++) {
             hipLaunchKernelGGL(kr<0>, 1, threads, 0, 0, o, c, W);
@@ -187,10 +227,12 @@ int main() {
             hipLaunchKernelGGL(kr<5>, 1, threads, 0, 0, o, c, W);
             hipLaunchKernelGGL(kr<6>, 1, threads, 0, 0, o, c, W);
             hipLaunchKernelGGL(kr<7>, 1, threads, 0, 0, o, c, W);
+            hipLaunchKernelGGL(kr<8>, 1, threads, 0, 0, o, c, W);
+            hipLaunchKernelGGL(kr<9>, 1, threads, 0, 0, o, c, W);
         }
         if (hipMemcpy(h, c, sizeof(h), hipMemcpyDeviceToHost)) return 1;
         printf("-- %d lanes (%d wave(s) per SIMD)\n", threads, threads > 256 ? 2 : 1);
-        for (int m = 0; m < 8; m++) printf("%-28s %llu cyc/step\n", nm[m], h[m]);
+        for (int m = 0; m < 10; m++) printf("%-28s %llu cyc/step\n", nm[m], h[m]);
     }
     return 0;
 }
