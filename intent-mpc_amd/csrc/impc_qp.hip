@@ -188,6 +188,12 @@ struct GpuTeam {
         int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
         return __hiloint2double(hi, lo);
     }
+    // a value every lane holds identically, moved to scalar registers
+    __device__ static double uniform(double v) {
+        int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
+        int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
+        return __hiloint2double(hi, lo);
+    }
     // v of lane src (per-lane) of the caller's wavefront: ds_bpermute on both halves
     __device__ double shfl(double v, int src) {
         const int addr = src << 2;
@@ -259,21 +265,21 @@ struct GpuTeam {
     }
 };
 
-template <int NL, int VS, int GS, int WPS>
+template <int NL, int VS, int GS, int WPS, int WF>
 __global__ __launch_bounds__(NL, WPS) void k_mpc_wave(impc::WaveTables T, impc::WaveIO io, impc::DevSettings st,
                                                       unsigned *counter) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     using LD = impc::WaveLds<NL, VS, GS>;
     GpuTeam<NL> wv{smem + LD::RED_OFF};
     __shared__ unsigned next;
-    impc::WaveQP<GpuTeam<NL>, NL, VS, GS>::load_tables(wv, T, smem);
+    impc::WaveQP<GpuTeam<NL>, NL, VS, GS, WF>::load_tables(wv, T, smem);
     for (;;) {
         if (threadIdx.x == 0) next = atomicAdd(counter, 1u);
         __syncthreads();
         const unsigned b = next;
         __syncthreads();
         if ((int64_t)b >= io.B) break;
-        impc::WaveQP<GpuTeam<NL>, NL, VS, GS> qp(wv, T, io, st, smem);
+        impc::WaveQP<GpuTeam<NL>, NL, VS, GS, WF> qp(wv, T, io, st, smem);
         qp.solve((int64_t)b);
     }
 }
@@ -290,7 +296,7 @@ struct GroupEntry {
 // Several structured batches in one persistent launch: one work queue over all their QPs, so
 // the long-running QPs at the end of one batch overlap the next batch's work instead of leaving
 // CUs idle between launches.  A workgroup reloads the pattern tables when it crosses batches.
-template <int NL, int VS, int GS, int WPS>
+template <int NL, int VS, int GS, int WPS, int WF>
 __global__ __launch_bounds__(NL, WPS) void k_mpc_wave_group(const GroupEntry *__restrict__ g, int count,
                                                             int64_t total, unsigned *counter) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -307,10 +313,10 @@ __global__ __launch_bounds__(NL, WPS) void k_mpc_wave_group(const GroupEntry *__
         int e = 0;
         while (e + 1 < count && (int64_t)b >= g[e + 1].first) e++;
         if (e != cur) {
-            impc::WaveQP<GpuTeam<NL>, NL, VS, GS>::load_tables(wv, g[e].T, smem);
+            impc::WaveQP<GpuTeam<NL>, NL, VS, GS, WF>::load_tables(wv, g[e].T, smem);
             cur = e;
         }
-        impc::WaveQP<GpuTeam<NL>, NL, VS, GS> qp(wv, g[e].T, g[e].io, g[e].st, smem);
+        impc::WaveQP<GpuTeam<NL>, NL, VS, GS, WF> qp(wv, g[e].T, g[e].io, g[e].st, smem);
         qp.solve((int64_t)b - g[e].first);
     }
 }
@@ -551,25 +557,43 @@ int generic_solve(impc_batch b, hipStream_t st) {
 }
 
 // ---- structured path
-template <int VS, int GS>
-int launch_wave(impc_batch b, hipStream_t st, const impc::WaveIO &io) {
+// The raised dynamic-LDS limit is set once per kernel instantiation (grow-only).
+template <class K>
+int ensure_lds_attr(K kernel, size_t lds) {
+    static size_t attr_bytes = 0;
+    if (lds > attr_bytes) {
+        HIP_OK(hipFuncSetAttribute((const void *)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr_bytes = lds;
+    }
+    return IMPC_OK;
+}
+
+// resident workgroups per CU: the waves-per-SIMD budget of the shape, and LDS
+template <int VS>
+int64_t resident_groups(int num_cu, size_t lds, int64_t work) {
+    constexpr int WPS = VS == kWaveVS ? IMPC_WAVES_PER_SIMD : 1;
+    const int by_waves = std::max(1, (4 * WPS) / (kTeam / 64));
+    const int per_cu = std::max<int>(1, std::min<int>(by_waves, (int)((160 * 1024 - 1024) / lds)));
+    return std::min<int64_t>(work, (int64_t)num_cu * per_cu);
+}
+
+// ---- structured path
+template <int VS, int GS, int WF>
+int launch_wave_w(impc_batch b, hipStream_t st, const impc::WaveIO &io) {
     constexpr int WPS = VS == kWaveVS ? IMPC_WAVES_PER_SIMD : 1;
     using LD = impc::WaveLds<kTeam, VS, GS>;
     const size_t lds = sizeof(double) * (size_t)LD::size(b->ms->CG, b->ms->n);  // products sized by the pattern
-    static size_t attr_bytes = 0;
-    if (lds > attr_bytes) {
-        HIP_OK(hipFuncSetAttribute((const void *)k_mpc_wave<kTeam, VS, GS, WPS>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr_bytes = lds;
-    }
-    // resident workgroups per CU: the waves-per-SIMD budget of the shape, and LDS
-    const int by_waves = std::max(1, (4 * WPS) / (kTeam / 64));
-    const int per_cu = std::max<int>(1, std::min<int>(by_waves, (int)((160 * 1024 - 1024) / lds)));
-    const int64_t groups = std::min<int64_t>(b->B, (int64_t)b->ctx->num_cu * per_cu);
-    hipLaunchKernelGGL((k_mpc_wave<kTeam, VS, GS, WPS>), dim3((unsigned)groups), dim3(kTeam), lds, st, b->wt, io,
+    if (int rc = ensure_lds_attr(k_mpc_wave<kTeam, VS, GS, WPS, WF>, lds)) return rc;
+    const int64_t groups = resident_groups<VS>(b->ctx->num_cu, lds, b->B);
+    hipLaunchKernelGGL((k_mpc_wave<kTeam, VS, GS, WPS, WF>), dim3((unsigned)groups), dim3(kTeam), lds, st, b->wt, io,
                        b->dst, b->d_counter);
     HIP_OK(hipGetLastError());
     return IMPC_OK;
+}
+template <int VS, int GS>
+int launch_wave(impc_batch b, hipStream_t st, const impc::WaveIO &io) {
+    constexpr int WS = impc::WaveLds<kTeam, VS, GS>::WSPEC;
+    return b->ms->W == WS ? launch_wave_w<VS, GS, WS>(b, st, io) : launch_wave_w<VS, GS, 0>(b, st, io);
 }
 
 int structured_solve(impc_batch b, hipStream_t st) {
@@ -604,24 +628,25 @@ int structured_solve(impc_batch b, hipStream_t st) {
     return IMPC_OK;
 }
 
-template <int VS, int GS>
-int launch_group(impc_ctx ctx, hipStream_t st, int count, int64_t total, int maxCG, int maxN, unsigned *counter) {
+template <int VS, int GS, int WF>
+int launch_group_w(impc_ctx ctx, hipStream_t st, int count, int64_t total, int maxCG, int maxN, unsigned *counter) {
     constexpr int WPS = VS == kWaveVS ? IMPC_WAVES_PER_SIMD : 1;
     using LD = impc::WaveLds<kTeam, VS, GS>;
     const size_t lds = sizeof(double) * (size_t)LD::size(maxCG, maxN);
-    static size_t attr_bytes = 0;
-    if (lds > attr_bytes) {
-        HIP_OK(hipFuncSetAttribute((const void *)k_mpc_wave_group<kTeam, VS, GS, WPS>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr_bytes = lds;
-    }
-    const int by_waves = std::max(1, (4 * WPS) / (kTeam / 64));
-    const int per_cu = std::max<int>(1, std::min<int>(by_waves, (int)((160 * 1024 - 1024) / lds)));
-    const int64_t groups = std::min<int64_t>(total, (int64_t)ctx->num_cu * per_cu);
-    hipLaunchKernelGGL((k_mpc_wave_group<kTeam, VS, GS, WPS>), dim3((unsigned)groups), dim3(kTeam), lds, st,
+    if (int rc = ensure_lds_attr(k_mpc_wave_group<kTeam, VS, GS, WPS, WF>, lds)) return rc;
+    const int64_t groups = resident_groups<VS>(ctx->num_cu, lds, total);
+    hipLaunchKernelGGL((k_mpc_wave_group<kTeam, VS, GS, WPS, WF>), dim3((unsigned)groups), dim3(kTeam), lds, st,
                        ctx->d_group, count, total, counter);
     HIP_OK(hipGetLastError());
     return IMPC_OK;
+}
+// spec: every batch of the group has the shape's default horizon
+template <int VS, int GS>
+int launch_group(impc_ctx ctx, hipStream_t st, int count, int64_t total, int maxCG, int maxN, unsigned *counter,
+                 bool spec) {
+    constexpr int WS = impc::WaveLds<kTeam, VS, GS>::WSPEC;
+    return spec ? launch_group_w<VS, GS, WS>(ctx, st, count, total, maxCG, maxN, counter)
+                : launch_group_w<VS, GS, 0>(ctx, st, count, total, maxCG, maxN, counter);
 }
 
 // dynamic LDS bytes of the structured kernel for a shape (team VS, GS) and pattern (CG, n)
@@ -676,8 +701,11 @@ int prepare_structured(impc_batch b) {
     const int32_t **dst_ptrs[] = {&t.var_orig, &t.var_pdiag, &t.var_boxrow, &t.var_boxpos, &t.gen_row,
                                   &t.gen_col,  &t.gen_pos,   &t.colg,       &t.term_ptr,   &t.term};
     for (size_t k = 0; k < arrs.size(); k++) *dst_ptrs[k] = base + offs[k];
-    const size_t scal_bytes = sizeof(double) * (size_t)b->B * (size_t)(2 * s.n + s.mg);
-    HIP_OK(hipMalloc((void **)&b->d_scal, scal_bytes));
+    // per-QP HBM scratch for the scaling vectors: long-horizon shape only (the default shape keeps
+    // them in LDS, mpc_wave.hpp WaveLds::ONCHIP)
+    const size_t scal_bytes =
+        b->vs == kWaveVS ? 0 : sizeof(double) * (size_t)b->B * (size_t)(2 * s.n + s.mg);
+    if (scal_bytes) HIP_OK(hipMalloc((void **)&b->d_scal, scal_bytes));
     HIP_OK(hipMalloc((void **)&b->d_counter, 256));
     b->device_bytes += (int64_t)(scal_bytes + h.size() * 4 + 256);
     b->structured_ok = true;
@@ -944,6 +972,7 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
     if (!b0) return fail(IMPC_INVALID_ARGUMENT, "null batch");
     impc_ctx ctx = b0->ctx;
     int gs = 0, maxCG = 1, maxN = 1;
+    bool spec = true;
     for (int k = 0; k < count; k++) {
         impc_batch b = bs[k];
         if (!b || b->ctx != ctx) return fail(IMPC_INVALID_ARGUMENT, "group batches must share a context");
@@ -953,6 +982,8 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
         gs = std::max(gs, b->gs);
         maxCG = std::max(maxCG, b->ms->CG);
         maxN = std::max(maxN, b->ms->n);
+        spec = spec && b->ms->W == (b->vs == kWaveVS ? impc::WaveLds<kTeam, kWaveVS, 2>::WSPEC
+                                                     : impc::WaveLds<kTeam, kWaveVSLong, 2>::WSPEC);
     }
     HIP_OK(hipSetDevice(ctx->device));
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
@@ -991,12 +1022,12 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
     if (b0->profile) HIP_OK(hipEventRecord(b0->ev[2], st));
     int rc;
     switch (b0->vs * 8 + gs) {
-        case kWaveVS * 8 + 2: rc = launch_group<kWaveVS, 2>(ctx, st, count, total, maxCG, maxN, b0->d_counter); break;
-        case kWaveVS * 8 + 3: rc = launch_group<kWaveVS, 3>(ctx, st, count, total, maxCG, maxN, b0->d_counter); break;
-        case kWaveVS * 8 + 4: rc = launch_group<kWaveVS, 4>(ctx, st, count, total, maxCG, maxN, b0->d_counter); break;
-        case kWaveVSLong * 8 + 2: rc = launch_group<kWaveVSLong, 2>(ctx, st, count, total, maxCG, maxN, b0->d_counter); break;
-        case kWaveVSLong * 8 + 3: rc = launch_group<kWaveVSLong, 3>(ctx, st, count, total, maxCG, maxN, b0->d_counter); break;
-        case kWaveVSLong * 8 + 4: rc = launch_group<kWaveVSLong, 4>(ctx, st, count, total, maxCG, maxN, b0->d_counter); break;
+        case kWaveVS * 8 + 2: rc = launch_group<kWaveVS, 2>(ctx, st, count, total, maxCG, maxN, b0->d_counter, spec); break;
+        case kWaveVS * 8 + 3: rc = launch_group<kWaveVS, 3>(ctx, st, count, total, maxCG, maxN, b0->d_counter, spec); break;
+        case kWaveVS * 8 + 4: rc = launch_group<kWaveVS, 4>(ctx, st, count, total, maxCG, maxN, b0->d_counter, spec); break;
+        case kWaveVSLong * 8 + 2: rc = launch_group<kWaveVSLong, 2>(ctx, st, count, total, maxCG, maxN, b0->d_counter, spec); break;
+        case kWaveVSLong * 8 + 3: rc = launch_group<kWaveVSLong, 3>(ctx, st, count, total, maxCG, maxN, b0->d_counter, spec); break;
+        case kWaveVSLong * 8 + 4: rc = launch_group<kWaveVSLong, 4>(ctx, st, count, total, maxCG, maxN, b0->d_counter, spec); break;
         default: return fail(IMPC_UNSUPPORTED, "no structured kernel for this size");
     }
     if (rc) return rc;

@@ -47,6 +47,10 @@ namespace impc {
 #endif
 #define IMPC_REP(X) for (int rep_ = 0; rep_ < (IMPC_DUP == (X) ? 2 : 1); rep_++)
 
+#ifndef IMPC_NOCHUNK
+#define IMPC_NOCHUNK 1
+#endif
+
 #ifndef IMPC_PSTRIDE_PAD
 #define IMPC_PSTRIDE_PAD 1
 #endif
@@ -108,7 +112,25 @@ struct WaveLds {
     static constexpr int RED_OFF = X_OFF + NP;              // team reduction scratch
     static constexpr int JUNK_OFF = RED_OFF + 64;           // per-lane discard slots [NL]
     static constexpr int GSLOT_OFF = JUNK_OFF + NL;         // int16 [4 NL GS]: general entry -> product slot
-    static constexpr int P_OFF = GSLOT_OFF + NL * GS;       // products, column-slot layout (size below)
+    // Chunked stage recursions (default horizon of the one-variable-per-lane shape): the W + 1
+    // stages split into 4 chunks [S(c), S(c+1)), one per wavefront; the chunk-entry operators
+    // Psi_k (forward) / Phi_k (backward) and two cross-chunk products live here.
+    static constexpr bool CHUNK = VS == 1 && NL == 256 && !IMPC_NOCHUNK;
+    static IMPC_WF constexpr int S(int c) { return (c * (WSPEC + 1) + 2) / 4; }
+    static constexpr int NPF = WSPEC + 1 - S(1), NPB = S(3);   // Psi_k, k in [S1, W]; Phi_k, k in [0, S3)
+    static constexpr int PSI_OFF = GSLOT_OFF + NL * GS;     // [NPF + NPB + 2][64], row-major 8x8
+    static constexpr int PSI_N = CHUNK ? 64 * (NPF + NPB + 2) : 0;
+    // One-variable-per-lane shape: the Ruiz scaling vectors D, E and the ADMM deltas of the
+    // termination checks live here (the long-horizon shape keeps them in HBM / registers: its LDS
+    // is full).  Layout of each: [var slots NMAX][box rows NMAX][general slots NL GS].
+    static constexpr bool ONCHIP = VS == 1;
+    static constexpr int VEC_N = 2 * NMAX + NL * GS;
+    static constexpr int SCL_OFF = PSI_OFF + PSI_N;         // D, E (scaling)
+    static constexpr int DLT_OFF = SCL_OFF + (ONCHIP ? VEC_N : 0);  // dx, dy (check iterations)
+    static constexpr int P_OFF = DLT_OFF + (ONCHIP ? VEC_N : 0);    // products, column-slot layout (size below)
+    // chunk-boundary exchange of the recursions (inside the team reduction scratch, past red[0..3])
+    static constexpr int XF_OFF = RED_OFF + 8;              // forward: a^_{S(c+1)-1}, c = 0..2
+    static constexpr int XB_OFF = RED_OFF + 32;             // backward: x^_{S(c)}, c = 1..3
     static constexpr int CGM = 24;                          // max general entries per column
     // products region: entry t of column v at t * stride(n) + v (stride = n rounded up to 64), so a
     // column's gather is CG4 independent conflict-free reads; it doubles as the factorisation's
@@ -162,16 +184,20 @@ IMPC_WF int row_type(double l, double u) {  // set_rho_vec (auxil.h:34)
 // a * b rounded on its own (never contracted into a following add), so the symmetric
 // cross-lane sums that consume it give bitwise-identical results in every lane of a group
 IMPC_WF double prod_nc(double a, double b) {
-    double p = a * b;
-#if defined(__HIP_DEVICE_COMPILE__)
-    asm volatile("" : "+v"(p));
-#endif
-    return p;
+    // contract(off) drops the multiply's contraction flag, so it never fuses into the add that
+    // consumes it (an empty volatile asm would do the same but also pin the instruction order)
+#pragma clang fp contract(off)
+    return a * b;
 }
 
-template <class WV, int NL, int VS, int GS>
+// WF: the stage count W fixed at compile time (LD::WSPEC, the default horizon: every stage loop
+// and LDS offset becomes a constant and no runtime-W code path shares the kernel's registers), or 0
+// for any W read from the tables.
+template <class WV, int NL, int VS, int GS, int WF = 0>
 struct WaveQP {
     using LD = WaveLds<NL, VS, GS>;
+    static_assert(WF == 0 || WF == LD::WSPEC, "WF is 0 or the shape's default horizon");
+    IMPC_WF int Wst() const { return WF ? WF : T.W; }
     WV &wv;
     const WaveTables &T;
     const WaveIO &io;
@@ -179,13 +205,12 @@ struct WaveQP {
     double *lds;
     int L;
     // ---- variable slots
-    double x[VS], q[VS], pd[VS], ab[VS], zb[VS], yb[VS], lb[VS], ub[VS], dxv[VS], dyb[VS];
+    double x[VS], q[VS], pd[VS], ab[VS], zb[VS], yb[VS], lb[VS], ub[VS], dxv_[VS], dyb_[VS];
     double ainv[VS][13], cp[VS][8];
-    double rhob[VS], rhoib[VS];  // rho and 1/rho of each variable's box row
     int bt[VS], vs_[VS], vr_[VS];
     bool vok[VS];
     // ---- general-row slots
-    double a[GS][4], z[GS], y[GS], lg[GS], ug[GS], dyg[GS], rhog_[GS], rhoig_[GS];
+    double a[GS][4], z[GS], y[GS], lg[GS], ug[GS], dyg_[GS];
     int gc[GS][4], gt[GS];
     bool gok[GS];
     WaveRho R;
@@ -198,16 +223,38 @@ struct WaveQP {
     IMPC_WF WaveQP(WV &w, const WaveTables &t, const WaveIO &i, const DevSettings &s, double *l)
         : wv(w), T(t), io(i), st(s), lds(l), L(w.lane()) {}
 
-    IMPC_WF void set_rho(double r) {
-        R.set(r);
-        _Pragma("unroll") for (int s = 0; s < VS; s++) {
-            rhob[s] = R.of(bt[s]);
-            rhoib[s] = R.inv(bt[s]);
-        }
-        _Pragma("unroll") for (int s = 0; s < GS; s++) {
-            rhog_[s] = R.of(gt[s]);
-            rhoig_[s] = R.inv(gt[s]);
-        }
+    // the lane index, opaque to the optimiser: per-lane LDS addresses derived from it are formed
+    // where they are used instead of being hoisted out of the ADMM loop (dozens of loop-invariant
+    // address registers otherwise spill and come back as scratch loads inside the recursions)
+    IMPC_WF int lane_o() const {
+        int l = L;
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("" : "+v"(l));
+#endif
+        return l;
+    }
+
+    // team-uniform: R stays in scalar registers, and each row's rho / 1/rho is selected from it
+    // by the row type where used instead of occupying 4 VGPRs per row slot
+    IMPC_WF void set_rho(double r) { R.set(wv.uniform(r)); }
+    IMPC_WF double rhob(int s) const { return R.of(bt[s]); }
+    IMPC_WF double rhoib(int s) const { return R.inv(bt[s]); }
+    IMPC_WF double rhog_(int s) const { return R.of(gt[s]); }
+    IMPC_WF double rhoig_(int s) const { return R.inv(gt[s]); }
+
+    // ADMM deltas of the last iteration (termination checks only): LDS or registers
+    IMPC_WF double &dxv(int s) { if constexpr (LD::ONCHIP) return lds[LD::DLT_OFF + NL * s + L]; else return dxv_[s]; }
+    IMPC_WF double &dyb(int s) {
+        if constexpr (LD::ONCHIP) return lds[LD::DLT_OFF + LD::NMAX + NL * s + L]; else return dyb_[s];
+    }
+    IMPC_WF double &dyg(int s) {
+        if constexpr (LD::ONCHIP) return lds[LD::DLT_OFF + 2 * LD::NMAX + NL * s + L]; else return dyg_[s];
+    }
+    // scaling vectors D, E (set by scale(), read at warm start, checks and unscaling): layout
+    // [D n][E box n][E general mg], in LDS or in the per-QP HBM scratch
+    IMPC_WF double *scal(int64_t b) {
+        if constexpr (LD::ONCHIP) return lds + LD::SCL_OFF;
+        else return io.scal + b * (int64_t)(2 * T.n + T.mg);
     }
 
     IMPC_WF double *F() { return lds + LD::F_OFF; }
@@ -232,7 +279,7 @@ struct WaveQP {
             vok[s] = v < n;
             vs_[s] = vok[s] ? v / 13 : 0;
             vr_[s] = vok[s] ? v % 13 : 0;
-            x[s] = q[s] = pd[s] = ab[s] = zb[s] = yb[s] = lb[s] = ub[s] = dxv[s] = dyb[s] = 0.0;
+            x[s] = q[s] = pd[s] = ab[s] = zb[s] = yb[s] = lb[s] = ub[s] = dxv_[s] = dyb_[s] = 0.0;
             bt[s] = 0;
             if (vok[s]) {
                 int ov = T.var_orig[v];
@@ -248,7 +295,7 @@ struct WaveQP {
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
             int g = NL * s + L;
             gok[s] = g < T.mg;
-            z[s] = y[s] = lg[s] = ug[s] = dyg[s] = 0.0;
+            z[s] = y[s] = lg[s] = ug[s] = dyg_[s] = 0.0;
             gt[s] = 0;
             const int16_t *gs = (const int16_t *)(lds + LD::GSLOT_OFF);
             const int pz = LD::p_size(T.CG, T.n);
@@ -268,6 +315,10 @@ struct WaveQP {
                 lg[s] = dmin(dmax(io.l[bm + row], -kInf), kInf);
                 ug[s] = dmin(dmax(io.u[bm + row], -kInf), kInf);
             }
+        }
+        if constexpr (LD::ONCHIP) {  // deltas read by a check before any ADMM step (max_iter = 0)
+            _Pragma("unroll") for (int s = 0; s < VS; s++) dxv(s) = dyb(s) = 0.0;
+            _Pragma("unroll") for (int s = 0; s < GS; s++) dyg(s) = 0.0;
         }
     }
 
@@ -393,6 +444,7 @@ struct WaveQP {
             c *= ct;
             wv.sync();
         }
+        c = wv.uniform(c);
         cinv = 1. / c;
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             lb[s] = Eb[s] * lb[s];
@@ -404,7 +456,7 @@ struct WaveQP {
             ug[s] = Eg[s] * ug[s];
             gt[s] = row_type(lg[s], ug[s]);
         }
-        double *sc = io.scal + b * (int64_t)(2 * T.n + T.mg);
+        double *sc = scal(b);
         _Pragma("unroll") for (int s = 0; s < VS; s++)
             if (vok[s]) {
                 sc[NL * s + L] = D[s];
@@ -417,7 +469,7 @@ struct WaveQP {
     // ------------------------------------------------------------ block factorisation
     // Returns 1 if a pivot is not positive (OSQP_NONCVX_ERROR).
     IMPC_WF int factorize() {
-        const int n = T.n, N = T.N, W = T.W;
+        const int n = T.n, W = Wst(), N = W + 1;
         double *w = pbuf(), *rhog = lds + LD::RHOG, *diagx = lds + LD::DIAGX;
         double *A = lds + LD::FA, *Li = lds + LD::FL, *Ai = lds + LD::FI, *Bb = lds + LD::FB, *G = lds + LD::FG,
                *E = lds + LD::FE, *Fm = F();
@@ -425,12 +477,12 @@ struct WaveQP {
             int g = NL * s + L;
             if (gok[s]) {
                 _Pragma("unroll") for (int e = 0; e < 4; e++) w[4 * g + e] = a[s][e];
-                rhog[g] = rhog_[s];
+                rhog[g] = rhog_(s);
             }
         }
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (vok[s]) {
-                double rb = rhob[s];
+                double rb = rhob(s);
                 diagx[NL * s + L] = (pd[s] + st.sigma) + rb * ab[s] * ab[s];
             }
         }
@@ -543,11 +595,211 @@ struct WaveQP {
         _Pragma("unroll") for (int s = 0; s < VS; s++)
             if (vok[s] && vs_[s] == 0 && vr_[s] < 8)
                 _Pragma("unroll") for (int j = 0; j < 8; j++) cp[s][j] = 0.0;
+        if constexpr (LD::CHUNK)
+            if (W == LD::WSPEC) chunk_operators();
         bad = (int)wv.max((double)bad);  // set by lane 0 only: team-wide, so every wavefront agrees
         clear_exchange();
         zero_products();  // the (4g + e) factorisation scratch shared the products region
         (void)n;
         return bad;
+    }
+
+    // ------------------------------------------------------- chunked stage recursions
+    // The forward recursion a_{k+1} = t_{k+1} - F_k a_k is linear in the chunk's entry value: for a
+    // chunk [S, E] entered from a_{S-1}, a_k = a^_k + Psi_k a_{S-1} with a^ the recursion started
+    // from a^_S = t_S, Psi_S = -F_{S-1}, Psi_{k+1} = -F_k Psi_k.  Likewise backward, x_k = x^_k +
+    // Phi_k x_{E+1} with x^_E = e_E, Phi_E = -F_E', Phi_k = -F_k' Phi_{k+1}.  Each wavefront runs
+    // its chunk's local recursion (phase A, S(c+1) - S(c) - 1 dependent steps), the boundary values
+    // meet in LDS, then every wavefront forms its entry value from the earlier chunks' boundary
+    // values (at most two independent 8x8 products, with the precomputed Psi_{S3-1} Psi_{S2-1} /
+    // Phi_{S1} Phi_{S2}) and corrects its stages with independent 8x8 products (phase B).  The
+    // dependent chain drops from W steps to 4 + 2.  Psi / Phi depend only on the factorisation.
+    IMPC_WF static double Fget(const double *Fm, int k, int r, int c) {  // F_k[r][c] (parity layout)
+        return (k & 1) ? Fm[64 * k + 8 * r + c] : Fm[64 * k + 8 * c + r];
+    }
+    IMPC_WF double *PF(int k) { return lds + LD::PSI_OFF + 64 * (k - LD::S(1)); }  // Psi_k, row-major
+    IMPC_WF double *PB(int k) { return lds + LD::PSI_OFF + 64 * (LD::NPF + k); }   // Phi_k
+    IMPC_WF double *PIF() { return lds + LD::PSI_OFF + 64 * (LD::NPF + LD::NPB); }
+    IMPC_WF double *PIB() { return PIF() + 64; }
+
+    IMPC_WF void chunk_operators() {
+        const double *Fm = F();
+        constexpr int CL = LD::S(4) - LD::S(3) > LD::S(1) ? LD::S(4) - LD::S(3) : LD::S(1);
+        static_assert(LD::S(2) - LD::S(1) <= CL && LD::S(3) - LD::S(2) <= CL, "chunk length");
+        for (int st = 0; st < CL; st++) {
+            for (int p = L; p < 6 * 64; p += NL) {
+                const int mtx = p >> 6, e = p & 63, r = e >> 3, cc = e & 7;
+                if (mtx < 3) {  // Psi_k of chunk c = mtx + 1
+                    const int c = mtx + 1, k = LD::S(c) + st;
+                    if (k >= LD::S(c + 1)) continue;
+                    double v;
+                    if (st == 0) {
+                        v = -Fget(Fm, k - 1, r, cc);
+                    } else {
+                        const double *Pp = PF(k - 1);
+                        double a = 0.0;
+                        for (int q = 0; q < 8; q++) a += Fget(Fm, k - 1, r, q) * Pp[8 * q + cc];
+                        v = -a;
+                    }
+                    PF(k)[e] = v;
+                } else {  // Phi_k of chunk c = mtx - 3
+                    const int c = mtx - 3, k = LD::S(c + 1) - 1 - st;
+                    if (k < LD::S(c)) continue;
+                    double v;
+                    if (st == 0) {
+                        v = -Fget(Fm, k, cc, r);
+                    } else {
+                        const double *Pn = PB(k + 1);
+                        double a = 0.0;
+                        for (int q = 0; q < 8; q++) a += Fget(Fm, k, q, r) * Pn[8 * q + cc];
+                        v = -a;
+                    }
+                    PB(k)[e] = v;
+                }
+            }
+            wv.sync();
+        }
+        for (int p = L; p < 128; p += NL) {
+            const int e = p & 63, r = e >> 3, cc = e & 7;
+            const double *X = p < 64 ? PF(LD::S(3) - 1) : PB(LD::S(1));
+            const double *Y = p < 64 ? PF(LD::S(2) - 1) : PB(LD::S(2));
+            double a = 0.0;
+            for (int q = 0; q < 8; q++) a += X[8 * r + q] * Y[8 * q + cc];
+            (p < 64 ? PIF() : PIB())[e] = a;
+        }
+        wv.sync();
+    }
+
+    // y = M v on the wavefront's 8x8 grid (M row-major in LDS): v at index i -> y at index j
+    // (l: the lane within the wavefront, formed once by the caller)
+    IMPC_WF double mv_i(const double *M, double v, int l) {
+        return wv.sum_stride8(prod_nc(M[8 * (l & 7) + (l >> 3)], v));
+    }
+    // v at index j -> y at index i
+    IMPC_WF double mv_j(const double *M, double v, int l) { return wv.sum_contig8(prod_nc(M[l], v)); }
+
+    // Phase A forward, chunk [K0, K1): a^_{K0} = t_{K0}; stores a^_k, K0 < k < K1, to rb and
+    // a^_{K1-1} to xo (XO).  Stage k's vector sits at index i (k even) / j (k odd).
+    template <int K0, int K1, bool XO>
+    IMPC_WF void fwd_chunk(const double *tb, double *rb, double *xo) {
+        const double *Fm = F();
+        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;
+        double *junk = lds + LD::JUNK_OFF + lo;
+        constexpr int NS = K1 - 1 - K0;
+        double a = tb[13 * K0 + ((K0 & 1) ? j : i)];
+        double cs = 0.0, cc = 0.0;  // step m kept by lane i == m (strided steps) / j == m (contiguous)
+        _Pragma("unroll") for (int k = K0; k < K1 - 1; k++) {
+            const double f = Fm[64 * k + l], t = tb[13 * (k + 1) + ((k & 1) ? i : j)];
+            if ((k & 1) == 0) {
+                a = rstep<true>(f, t, a);
+                cs = i == k - K0 ? a : cs;
+            } else {
+                a = rstep<false>(f, t, a);
+                cc = j == k - K0 ? a : cc;
+            }
+        }
+        const int ke = K0 + i, ko = K0 + j;
+        *((i < NS && !(ke & 1)) ? rb + 13 * (ke + 1) + j : junk) = cs;
+        *((j < NS && (ko & 1)) ? rb + 13 * (ko + 1) + i : junk) = cc;
+        if constexpr (XO) {
+            if constexpr (((K1 - 1) & 1) == 0)
+                *(j == 0 ? xo + i : junk) = a;
+            else
+                *(i == 0 ? xo + j : junk) = a;
+        }
+    }
+
+    // Phase B forward, chunk C >= 1: entry a_{S(C)-1} from the boundary values, then the stages
+    template <int C>
+    IMPC_WF void fwd_fix(const double *tb, double *rb) {
+        const double *X = lds + LD::XF_OFF;
+        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;
+        double *junk = lds + LD::JUNK_OFF + lo;
+        double v = X[8 * (C - 1) + j];
+        if constexpr (C >= 2) v = v + mv_i(PF(LD::S(C) - 1), X[8 * (C - 2) + i], l);
+        if constexpr (C == 3) v = v + mv_i(PIF(), X[i], l);
+        constexpr int K0 = LD::S(C), K1 = LD::S(C + 1);
+        double r[K1 - K0];
+        _Pragma("unroll") for (int k = K0; k < K1; k++) r[k - K0] = mv_j(PF(k), v, l);
+        _Pragma("unroll") for (int k = K0; k < K1; k++) {
+            const double ah = k == K0 ? tb[13 * k + i] : rb[13 * k + i];
+            *(j == 0 ? rb + 13 * k + i : junk) = ah + r[k - K0];
+        }
+    }
+
+    // Phase A backward, chunk [KB, KT]: x^_{KT} = e_{KT}; stores x^_k, KB <= k < KT, to xb and
+    // x^_{KB} to xo (XO)
+    template <int KB, int KT, bool XO>
+    IMPC_WF void bwd_chunk(const double *eb, double *xb, double *xo) {
+        const double *Fm = F();
+        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;
+        double *junk = lds + LD::JUNK_OFF + lo;
+        constexpr int NS = KT - KB;
+        double x = eb[13 * KT + ((KT & 1) ? j : i)];
+        double cs = 0.0, cc = 0.0;
+        _Pragma("unroll") for (int k = KT - 1; k >= KB; k--) {
+            const double f = Fm[64 * k + l], e = eb[13 * k + ((k & 1) ? j : i)];
+            if (k & 1) {
+                x = rstep<true>(f, e, x);
+                cs = i == KT - 1 - k ? x : cs;
+            } else {
+                x = rstep<false>(f, e, x);
+                cc = j == KT - 1 - k ? x : cc;
+            }
+        }
+        const int ks = KT - 1 - i, kc = KT - 1 - j;
+        *((i < NS && (ks & 1)) ? xb + 13 * ks + j : junk) = cs;
+        *((j < NS && !(kc & 1)) ? xb + 13 * kc + i : junk) = cc;
+        if constexpr (XO) {
+            if constexpr ((KB & 1) == 0)
+                *(j == 0 ? xo + i : junk) = x;
+            else
+                *(i == 0 ? xo + j : junk) = x;
+        }
+    }
+
+    // Phase B backward, chunk C <= 2: entry x_{S(C+1)}, then the stages
+    template <int C>
+    IMPC_WF void bwd_fix(const double *eb, double *xb) {
+        const double *X = lds + LD::XB_OFF;  // x^_{S(c)} at X + 8 (c - 1)
+        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;
+        double *junk = lds + LD::JUNK_OFF + lo;
+        double v = X[8 * C + j];
+        if constexpr (C <= 1) v = v + mv_i(PB(LD::S(C + 1)), X[8 * (C + 1) + i], l);
+        if constexpr (C == 0) v = v + mv_i(PIB(), X[16 + i], l);
+        constexpr int K0 = LD::S(C), K1 = LD::S(C + 1);
+        double r[K1 - K0];
+        _Pragma("unroll") for (int k = K0; k < K1; k++) r[k - K0] = mv_j(PB(k), v, l);
+        _Pragma("unroll") for (int k = K0; k < K1; k++) {
+            const double xh = k == K1 - 1 ? eb[13 * k + i] : xb[13 * k + i];
+            *(j == 0 ? xb + 13 * k + i : junk) = xh + r[k - K0];
+        }
+    }
+
+    IMPC_WF void fwd_chunked(const double *tb, double *rb) {
+        double *X = lds + LD::XF_OFF;
+        const int w = L >> 6;
+        if (w == 0) fwd_chunk<LD::S(0), LD::S(1), true>(tb, rb, X);
+        else if (w == 1) fwd_chunk<LD::S(1), LD::S(2), true>(tb, rb, X + 8);
+        else if (w == 2) fwd_chunk<LD::S(2), LD::S(3), true>(tb, rb, X + 16);
+        else fwd_chunk<LD::S(3), LD::S(4), false>(tb, rb, X);
+        wv.sync();
+        if (w == 1) fwd_fix<1>(tb, rb);
+        else if (w == 2) fwd_fix<2>(tb, rb);
+        else if (w == 3) fwd_fix<3>(tb, rb);
+    }
+
+    IMPC_WF void bwd_chunked(const double *eb, double *xb) {
+        double *X = lds + LD::XB_OFF;
+        const int w = L >> 6;
+        if (w == 0) bwd_chunk<LD::S(0), LD::S(1) - 1, false>(eb, xb, X);
+        else if (w == 1) bwd_chunk<LD::S(1), LD::S(2) - 1, true>(eb, xb, X);
+        else if (w == 2) bwd_chunk<LD::S(2), LD::S(3) - 1, true>(eb, xb, X + 8);
+        else bwd_chunk<LD::S(3), LD::S(4) - 1, true>(eb, xb, X + 16);
+        wv.sync();
+        if (w == 0) bwd_fix<0>(eb, xb);
+        else if (w == 1) bwd_fix<1>(eb, xb);
+        else if (w == 2) bwd_fix<2>(eb, xb);
     }
 
     // One step of a stage recursion on the 8x8 lane grid: returns c - R(F v), R the strided
@@ -685,7 +937,7 @@ struct WaveQP {
         double *pb = pbuf();
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
             if (gok[s]) {
-                double vv = rhog_[s] * z[s] - y[s];
+                double vv = rhog_(s) * z[s] - y[s];
                 _Pragma("unroll") for (int e = 0; e < 4; e++) pb[gdst(s, e)] = a[s][e] * vv;
             }
         }
@@ -694,7 +946,7 @@ struct WaveQP {
 
     // --------------------------------------------------------------- one ADMM iteration
     IMPC_WF void iterate(bool need_delta) {
-        const int n = T.n, W = T.W;
+        const int n = T.n, W = Wst();
         double *rb = rbuf(), *tb = tbuf(), *eb = ebuf(), *xb = xbuf();
         const double sigma = st.sigma, alpha = st.alpha, oma = (double)1.0 - st.alpha;
         IMPC_REP(kSecRhs) {
@@ -702,7 +954,7 @@ struct WaveQP {
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
                 if (!vok[s]) continue;
                 int v = NL * s + L;
-                double vb = rhob[s] * zb[s] - yb[s];
+                double vb = rhob(s) * zb[s] - yb[s];
                 double r = sigma * x[s] - q[s];
                 r += ab[s] * vb;
                 r += col_gather(v);
@@ -735,7 +987,9 @@ struct WaveQP {
             // One wavefront of the team (rw) runs it -- the others go straight to the barrier and
             // leave their SIMD's issue slots to the co-resident team.
             if (L < 8) rb[L] = tb[L];
-            if ((L >> 6) == rw) {
+            if (LD::CHUNK && W == LD::WSPEC) {
+                if constexpr (LD::CHUNK) fwd_chunked(tb, rb);
+            } else if ((L >> 6) == rw) {
                 if (W == LD::WSPEC)
                     fwd_sweep<LD::WSPEC>(tb, rb, W);
                 else
@@ -760,7 +1014,9 @@ struct WaveQP {
             // S4: backward 8-dim recursion x_k[:8] = e_k[:8] - F_k' x_{k+1}[:8] on the same grid and
             // stored layout: even steps reduce over j (contiguous), odd steps over i (strided).
             if (L < 8) xb[13 * W + L] = eb[13 * W + L];
-            if ((L >> 6) == rw) {
+            if (LD::CHUNK && W == LD::WSPEC) {
+                if constexpr (LD::CHUNK) bwd_chunked(eb, xb);
+            } else if ((L >> 6) == rw) {
                 if (W == LD::WSPEC)
                     bwd_sweep<((LD::WSPEC - 1) & 1) != 0, LD::WSPEC>(eb, xb, W);
                 else if ((W - 1) & 1)
@@ -788,14 +1044,14 @@ struct WaveQP {
             if (!vok[s]) continue;
             double xt = xb[NL * s + L];
             double xn = alpha * xt + oma * x[s];
-            if (need_delta) dxv[s] = xn - x[s];
+            if (need_delta) dxv(s) = xn - x[s];
             x[s] = xn;
             double zt = ab[s] * xt;
             double zr = alpha * zt + oma * zb[s];
-            double zn = dmin(dmax(zr + rhoib[s] * yb[s], lb[s]), ub[s]);
-            double dy = rhob[s] * (zr - zn);
+            double zn = dmin(dmax(zr + rhoib(s) * yb[s], lb[s]), ub[s]);
+            double dy = rhob(s) * (zr - zn);
             yb[s] += dy;
-            if (need_delta) dyb[s] = dy;
+            if (need_delta) dyb(s) = dy;
             zb[s] = zn;
         }
         // general rows
@@ -804,10 +1060,10 @@ struct WaveQP {
             double zt = 0.0;
             _Pragma("unroll") for (int e = 0; e < 4; e++) zt += a[s][e] * xb[gcol(s, e)];
             double zr = alpha * zt + oma * z[s];
-            double zn = dmin(dmax(zr + rhoig_[s] * y[s], lg[s]), ug[s]);
-            double dy = rhog_[s] * (zr - zn);
+            double zn = dmin(dmax(zr + rhoig_(s) * y[s], lg[s]), ug[s]);
+            double dy = rhog_(s) * (zr - zn);
             y[s] += dy;
-            if (need_delta) dyg[s] = dy;
+            if (need_delta) dyg(s) = dy;
             z[s] = zn;
         }
         wv.sync();
@@ -823,7 +1079,7 @@ struct WaveQP {
     };
 
     IMPC_WF void load_scal(int64_t b, double D[VS], double Eb[VS], double Eg[GS]) {
-        const double *sc = io.scal + b * (int64_t)(2 * T.n + T.mg);
+        const double *sc = scal(b);
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             D[s] = vok[s] ? sc[NL * s + L] : 1.0;
             Eb[s] = vok[s] ? sc[T.n + NL * s + L] : 1.0;
@@ -920,23 +1176,23 @@ struct WaveQP {
         double nrm = 0.0, lhs = 0.0;
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (!vok[s]) continue;
-            double d = dyb[s];
+            double d = dyb(s);
             if (ub[s] > kInf * kMinScaling)
                 d = (lb[s] < -kInf * kMinScaling) ? 0.0 : dmin(d, 0.0);
             else if (lb[s] < -kInf * kMinScaling)
                 d = dmax(d, 0.0);
-            dyb[s] = d;
+            dyb(s) = d;
             nrm = dmax(nrm, fabs(unsc ? Eb[s] * d : d));
             lhs += ub[s] * dmax(d, 0) + lb[s] * dmin(d, 0);
         }
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
             if (!gok[s]) continue;
-            double d = dyg[s];
+            double d = dyg(s);
             if (ug[s] > kInf * kMinScaling)
                 d = (lg[s] < -kInf * kMinScaling) ? 0.0 : dmin(d, 0.0);
             else if (lg[s] < -kInf * kMinScaling)
                 d = dmax(d, 0.0);
-            dyg[s] = d;
+            dyg(s) = d;
             nrm = dmax(nrm, fabs(unsc ? Eg[s] * d : d));
             lhs += ug[s] * dmax(d, 0) + lg[s] * dmin(d, 0);
         }
@@ -947,13 +1203,13 @@ struct WaveQP {
             double *pb = pbuf();
             _Pragma("unroll") for (int s = 0; s < GS; s++) {
                 if (gok[s])
-                    _Pragma("unroll") for (int e = 0; e < 4; e++) pb[gdst(s, e)] = a[s][e] * dyg[s];
+                    _Pragma("unroll") for (int e = 0; e < 4; e++) pb[gdst(s, e)] = a[s][e] * dyg(s);
             }
             wv.sync();
             double mx = 0.0;
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
                 if (!vok[s]) continue;
-                double t = ab[s] * dyb[s] + col_gather(NL * s + L);
+                double t = ab[s] * dyb(s) + col_gather(NL * s + L);
                 if (unsc) t = (1. / D[s]) * t;
                 mx = dmax(mx, fabs(t));
             }
@@ -970,8 +1226,8 @@ struct WaveQP {
         double nrm = 0.0, qdx = 0.0, cs = unsc ? c : 1.0;
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (!vok[s]) continue;
-            nrm = dmax(nrm, fabs(unsc ? D[s] * dxv[s] : dxv[s]));
-            qdx += q[s] * dxv[s];
+            nrm = dmax(nrm, fabs(unsc ? D[s] * dxv(s) : dxv(s)));
+            qdx += q[s] * dxv(s);
         }
         nrm = wv.max(nrm);
         qdx = wv.sum(qdx);
@@ -980,7 +1236,7 @@ struct WaveQP {
             double mx = 0.0;
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
                 if (!vok[s]) continue;
-                double pv = pd[s] * dxv[s];
+                double pv = pd[s] * dxv(s);
                 if (unsc) pv = (1. / D[s]) * pv;
                 mx = dmax(mx, fabs(pv));
             }
@@ -988,12 +1244,12 @@ struct WaveQP {
             if (mx < cs * eps * nrm) {
                 double *xb = xbuf();
                 _Pragma("unroll") for (int s = 0; s < VS; s++)
-                    if (vok[s]) xb[NL * s + L] = dxv[s];
+                    if (vok[s]) xb[NL * s + L] = dxv(s);
                 wv.sync();
                 double viol = 0.0;
                 _Pragma("unroll") for (int s = 0; s < VS; s++) {
                     if (!vok[s]) continue;
-                    double t = ab[s] * dxv[s];
+                    double t = ab[s] * dxv(s);
                     if (unsc) t = (1. / Eb[s]) * t;
                     if ((ub[s] < kInf * kMinScaling && t > eps * nrm) || (lb[s] > -kInf * kMinScaling && t < -eps * nrm))
                         viol = 1.0;

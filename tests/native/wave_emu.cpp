@@ -49,6 +49,7 @@ struct EmuWave {
         return b[(l & ~63) + src];
     }
     double shfl(double v, int src) { return bcast(v, src); }
+    static double uniform(double v) { return v; }  // every lane already holds the same value
     double sum_contig8(double v) {  // the GPU's DPP order: ((v0+v1)+(v2+v3)) + ((v4+v5)+(v6+v7))
         double *b = next_wbuf();
         b[l] = v;
@@ -90,8 +91,8 @@ struct EmuWave {
     }
 };
 
-template <int VS, int GS>
-void run(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSettings &st) {
+template <int VS, int GS, int WF>
+void run_w(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSettings &st) {
     using LD = impc::WaveLds<NL, VS, GS>;
     std::vector<double> lds((size_t)LD::size(T.CG, T.n), 0.0);
     EmuShared sh;
@@ -99,13 +100,23 @@ void run(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSetti
     for (int l = 0; l < NL; l++)
         th.emplace_back([&, l] {
             EmuWave wv{l, &sh};
-            impc::WaveQP<EmuWave, NL, VS, GS>::load_tables(wv, T, lds.data());
+            impc::WaveQP<EmuWave, NL, VS, GS, WF>::load_tables(wv, T, lds.data());
             for (int64_t b = 0; b < io.B; b++) {
-                impc::WaveQP<EmuWave, NL, VS, GS> qp(wv, T, io, st, lds.data());
+                impc::WaveQP<EmuWave, NL, VS, GS, WF> qp(wv, T, io, st, lds.data());
                 qp.solve(b);
             }
         });
     for (auto &t : th) t.join();
+}
+
+// the product's dispatch: the default-horizon specialisation when W matches (impc_qp.hip launch_wave)
+template <int VS, int GS>
+void run(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSettings &st) {
+    constexpr int WS = impc::WaveLds<NL, VS, GS>::WSPEC;
+    if (T.W == WS)
+        run_w<VS, GS, WS>(T, io, st);
+    else
+        run_w<VS, GS, 0>(T, io, st);
 }
 
 }  // namespace
