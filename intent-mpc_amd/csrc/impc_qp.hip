@@ -333,6 +333,28 @@ struct impc_ctx_s {
     std::vector<GroupEntry> h_group;
 };
 
+// Every host->device transfer and fill below goes through the context's stream and has finished
+// when the call returns: the solver's kernels run on that stream, which is non-blocking, so the
+// legacy null stream of a plain hipMemcpy / hipMemset would not be ordered before them (a pageable
+// hipMemcpy may also return before its DMA lands).
+static int h2d_sync(hipStream_t st, void *dst, const void *src, size_t bytes) {
+    if (!bytes) return IMPC_OK;
+    HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st));
+    HIP_OK(hipStreamSynchronize(st));
+    return IMPC_OK;
+}
+static int fill0_sync(hipStream_t st, void *dst, size_t bytes) {
+    if (!bytes) return IMPC_OK;
+    HIP_OK(hipMemsetAsync(dst, 0, bytes, st));
+    HIP_OK(hipStreamSynchronize(st));
+    return IMPC_OK;
+}
+#define IMPC_TRY(expr)          \
+    do {                        \
+        int rc_ = (expr);       \
+        if (rc_) return rc_;    \
+    } while (0)
+
 struct impc_batch_s {
     impc_ctx ctx = nullptr;
     int64_t n = 0, m = 0, nnzP = 0, nnzA = 0;
@@ -455,7 +477,7 @@ int ensure_generic(impc_batch b) {
     for (size_t k = 0; k < arrs.size(); k++)
         if (!arrs[k]->empty()) std::memcpy(hsym.data() + offs[k], arrs[k]->data(), arrs[k]->size() * 4);
     HIP_OK(hipMalloc(&b->d_sym, hsym.size() * 4));
-    HIP_OK(hipMemcpy(b->d_sym, hsym.data(), hsym.size() * 4, hipMemcpyHostToDevice));
+    IMPC_TRY(h2d_sync(b->ctx->stream, b->d_sym, hsym.data(), hsym.size() * 4));
     const int32_t *base = (const int32_t *)b->d_sym;
     impc::DevSym &d = b->dsym;
     d.n = s.n;
@@ -494,7 +516,7 @@ int ensure_generic(impc_batch b) {
         b->d_work = nullptr;
         return fail(IMPC_MEM_ALLOC_ERROR, "hipMalloc(generic workspace) failed: batch too large for device memory");
     }
-    HIP_OK(hipMemset(b->d_work, 0, work_bytes));
+    IMPC_TRY(fill0_sync(b->ctx->stream, b->d_work, work_bytes));
     int64_t off = 0;
     for (auto &sl : slots) {
         *sl.dst = b->d_work + off * b->S;
@@ -687,7 +709,7 @@ int prepare_structured(impc_batch b) {
     for (size_t k = 0; k < arrs.size(); k++)
         if (!arrs[k]->empty()) std::memcpy(h.data() + offs[k], arrs[k]->data(), arrs[k]->size() * 4);
     HIP_OK(hipMalloc(&b->d_tables, h.size() * 4));
-    HIP_OK(hipMemcpy(b->d_tables, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    IMPC_TRY(h2d_sync(b->ctx->stream, b->d_tables, h.data(), h.size() * 4));
     const int32_t *base = (const int32_t *)b->d_tables;
     impc::WaveTables &t = b->wt;
     t.n = s.n;
@@ -831,12 +853,12 @@ int impc_batch_create(impc_ctx ctx, int64_t n, int64_t m, const int64_t *Pp, con
     b->in_xws = p;
     p += b->n * B;
     b->in_yws = p;
-    HIP_OK(hipMemset(b->d_in, 0, in_bytes));
+    IMPC_TRY(fill0_sync(ctx->stream, b->d_in, in_bytes));
     if (hipMalloc((void **)&b->d_xout, sizeof(double) * (size_t)(std::max<int64_t>(n, 1) * B)) != hipSuccess ||
         hipMalloc((void **)&b->d_yout, sizeof(double) * (size_t)(std::max<int64_t>(m, 1) * B)) != hipSuccess ||
         hipMalloc((void **)&b->d_info, sizeof(impc_info) * (size_t)B) != hipSuccess)
         return fail(IMPC_MEM_ALLOC_ERROR, "hipMalloc(results) failed");
-    HIP_OK(hipMemset(b->d_info, 0, sizeof(impc_info) * (size_t)B));
+    IMPC_TRY(fill0_sync(ctx->stream, b->d_info, sizeof(impc_info) * (size_t)B));
     b->device_bytes = (int64_t)(in_bytes + sizeof(double) * (n + m) * B + sizeof(impc_info) * B);
     int rc = prepare_structured(b.get());
     if (rc) return rc;
@@ -896,12 +918,12 @@ int impc_batch_set_values(impc_batch b, const double *Px, const double *q, const
         }
     HIP_OK(hipSetDevice(b->ctx->device));
     const size_t B = (size_t)b->B;
-    if (b->nnzP) HIP_OK(hipMemcpy(b->in_Px, Px, sizeof(double) * b->nnzP * B, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(b->in_q, q, sizeof(double) * b->n * B, hipMemcpyHostToDevice));
-    if (b->nnzA) HIP_OK(hipMemcpy(b->in_Ax, Ax, sizeof(double) * b->nnzA * B, hipMemcpyHostToDevice));
+    IMPC_TRY(h2d_sync(b->ctx->stream, b->in_Px, Px, sizeof(double) * b->nnzP * B));
+    IMPC_TRY(h2d_sync(b->ctx->stream, b->in_q, q, sizeof(double) * b->n * B));
+    IMPC_TRY(h2d_sync(b->ctx->stream, b->in_Ax, Ax, sizeof(double) * b->nnzA * B));
     if (b->m) {
-        HIP_OK(hipMemcpy(b->in_l, l, sizeof(double) * b->m * B, hipMemcpyHostToDevice));
-        HIP_OK(hipMemcpy(b->in_u, u, sizeof(double) * b->m * B, hipMemcpyHostToDevice));
+        IMPC_TRY(h2d_sync(b->ctx->stream, b->in_l, l, sizeof(double) * b->m * B));
+        IMPC_TRY(h2d_sync(b->ctx->stream, b->in_u, u, sizeof(double) * b->m * B));
     }
     b->values_set = true;
     b->generic_dirty = true;
@@ -937,12 +959,12 @@ int impc_batch_warm_start(impc_batch b, const double *x, const double *y) {
         return IMPC_OK;
     }
     const size_t B = (size_t)b->B;
-    HIP_OK(hipMemcpy(b->in_xws, x, sizeof(double) * b->n * B, hipMemcpyHostToDevice));
+    IMPC_TRY(h2d_sync(b->ctx->stream, b->in_xws, x, sizeof(double) * b->n * B));
     if (b->m) {
         if (y)
-            HIP_OK(hipMemcpy(b->in_yws, y, sizeof(double) * b->m * B, hipMemcpyHostToDevice));
+            IMPC_TRY(h2d_sync(b->ctx->stream, b->in_yws, y, sizeof(double) * b->m * B));
         else
-            HIP_OK(hipMemset(b->in_yws, 0, sizeof(double) * b->m * B));
+            IMPC_TRY(fill0_sync(b->ctx->stream, b->in_yws, sizeof(double) * b->m * B));
     }
     b->has_ws = true;
     b->generic_dirty = true;
@@ -1015,7 +1037,7 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
             HIP_OK(hipMalloc((void **)&ctx->d_group, sizeof(GroupEntry) * (size_t)count));
             ctx->group_cap = count;
         }
-        HIP_OK(hipMemcpy(ctx->d_group, entries.data(), sizeof(GroupEntry) * (size_t)count, hipMemcpyHostToDevice));
+        IMPC_TRY(h2d_sync(st, ctx->d_group, entries.data(), sizeof(GroupEntry) * (size_t)count));
         ctx->h_group = entries;
     }
     HIP_OK(hipMemsetAsync(b0->d_counter, 0, 256, st));
@@ -1059,7 +1081,7 @@ int impc_batch_device_results(impc_batch b, double **x, double **y, impc_info **
 }
 
 static int upload_interleaved(impc_batch b, const double *host, double *qp_major, double *dst, int64_t len) {
-    HIP_OK(hipMemcpy(qp_major, host, sizeof(double) * len * b->B, hipMemcpyHostToDevice));
+    IMPC_TRY(h2d_sync(b->ctx->stream, qp_major, host, sizeof(double) * len * b->B));
     int rc = interleave(b, qp_major, dst, len, b->ctx->stream);
     if (rc) return rc;
     HIP_OK(hipStreamSynchronize(b->ctx->stream));
@@ -1166,7 +1188,7 @@ extern "C" int impc_debug_sections(impc_batch b, unsigned long long *out) {
     if (!b->d_sec) return IMPC_OK;
     HIP_OK(hipStreamSynchronize(b->ctx->stream));
     HIP_OK(hipMemcpy(out, b->d_sec, sizeof(unsigned long long) * impc::kSecCount, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemset(b->d_sec, 0, sizeof(unsigned long long) * impc::kSecCount));
+    IMPC_TRY(fill0_sync(b->ctx->stream, b->d_sec, sizeof(unsigned long long) * impc::kSecCount));
     return IMPC_OK;
 }
 #endif
@@ -1200,7 +1222,7 @@ int impc_copy_to_device(impc_ctx ctx, void *dst, const void *src, int64_t bytes)
     if (!ctx || (bytes > 0 && (!dst || !src)) || bytes < 0) return fail(IMPC_INVALID_ARGUMENT, "invalid argument");
     HIP_OK(hipSetDevice(ctx->device));
     HIP_OK(hipStreamSynchronize(ctx->stream));
-    if (bytes) HIP_OK(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyHostToDevice));
+    IMPC_TRY(h2d_sync(ctx->stream, dst, src, (size_t)bytes));
     return IMPC_OK;
 }
 int impc_copy_to_host(impc_ctx ctx, void *dst, const void *src, int64_t bytes) {

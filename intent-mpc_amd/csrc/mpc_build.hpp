@@ -136,11 +136,11 @@ extern "C" int impc_mpc_builder_create(impc_ctx ctx, const impc_mpc_params *p, i
     HIP_OK(hipMalloc((void **)&b->d_tl, sizeof(double) * b->m));
     HIP_OK(hipMalloc((void **)&b->d_tu, sizeof(double) * b->m));
     HIP_OK(hipMalloc((void **)&b->d_slot, sizeof(int32_t) * std::max<size_t>(1, sl32.size())));
-    HIP_OK(hipMemcpy(b->d_tPx, Px.data(), sizeof(double) * b->nnzP, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(b->d_tAx, Ax.data(), sizeof(double) * b->nnzA, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(b->d_tl, l.data(), sizeof(double) * b->m, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(b->d_tu, u.data(), sizeof(double) * b->m, hipMemcpyHostToDevice));
-    if (!sl32.empty()) HIP_OK(hipMemcpy(b->d_slot, sl32.data(), sizeof(int32_t) * sl32.size(), hipMemcpyHostToDevice));
+    IMPC_TRY(h2d_sync(ctx->stream, b->d_tPx, Px.data(), sizeof(double) * b->nnzP));
+    IMPC_TRY(h2d_sync(ctx->stream, b->d_tAx, Ax.data(), sizeof(double) * b->nnzA));
+    IMPC_TRY(h2d_sync(ctx->stream, b->d_tl, l.data(), sizeof(double) * b->m));
+    IMPC_TRY(h2d_sync(ctx->stream, b->d_tu, u.data(), sizeof(double) * b->m));
+    IMPC_TRY(h2d_sync(ctx->stream, b->d_slot, sl32.data(), sizeof(int32_t) * sl32.size()));
     *out = b.release();
     return IMPC_OK;
 }
