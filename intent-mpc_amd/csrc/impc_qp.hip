@@ -252,6 +252,39 @@ struct GpuTeam {
         __syncthreads();
         return r;
     }
+    // K team maxima at once: DPP / permlane exchanges inside each wavefront (max is
+    // order-independent, so any pairing that covers the wave will do), one LDS round across
+    // wavefronts instead of K (a termination check reduces 14 norms)
+    template <int K>
+    __device__ void max_n(double (&v)[K]) {
+        static_assert(K * (NL / 64) <= 64, "team reduction scratch (WaveLds RED_OFF) holds 64 doubles");
+        auto mx = [](double a, double b) { return b > a ? b : a; };
+        _Pragma("unroll") for (int k = 0; k < K; k++) {
+            double t = v[k];
+            t = mx(t, dpp<0xB1>(t));   // quad_perm [1,0,3,2]
+            t = mx(t, dpp<0x4E>(t));   // quad_perm [2,3,0,1]
+            t = mx(t, dpp<0x141>(t));  // row_half_mirror
+            t = mx(t, dpp<0x128>(t));  // row_ror:8
+            const int lo = __double2loint(t), hi = __double2hiint(t);
+            auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+            auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+            t = mx(__hiloint2double(rh[0], rl[0]), __hiloint2double(rh[1], rl[1]));
+            const int lo2 = __double2loint(t), hi2 = __double2hiint(t);
+            auto ql = __builtin_amdgcn_permlane32_swap(lo2, lo2, false, false);
+            auto qh = __builtin_amdgcn_permlane32_swap(hi2, hi2, false, false);
+            v[k] = mx(__hiloint2double(qh[0], ql[0]), __hiloint2double(qh[1], ql[1]));
+        }
+        if (NL == 64) return;
+        if ((threadIdx.x & 63) == 0)
+            _Pragma("unroll") for (int k = 0; k < K; k++) red[(threadIdx.x >> 6) * K + k] = v[k];
+        __syncthreads();
+        _Pragma("unroll") for (int k = 0; k < K; k++) {
+            double r = red[k];
+            for (int w = 1; w < NL / 64; w++) r = red[w * K + k] > r ? red[w * K + k] : r;
+            v[k] = r;
+        }
+        __syncthreads();
+    }
     __device__ double sum(double v) {
         for (int mask = 32; mask >= 1; mask >>= 1) v = v + __shfl_xor(v, mask);
         v = bcast(v, 0);

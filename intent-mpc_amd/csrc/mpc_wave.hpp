@@ -1066,7 +1066,8 @@ struct WaveQP {
             if (need_delta) dyg(s) = dy;
             z[s] = zn;
         }
-        wv.sync();
+        // no barrier: the products go to their own LDS region, which nothing above reads, and
+        // write_v_products ends with the barrier the next rhs gather needs
         IMPC_SEC(kSecUpdate);
         IMPC_REP(kSecProducts) write_v_products();
         IMPC_SEC(kSecProducts);
@@ -1138,20 +1139,12 @@ struct WaveQP {
             aty_u = dmax(aty_u, fabs(di * aty));
             px_u = dmax(px_u, fabs(di * px));
         }
-        pr_u = wv.max(pr_u);
-        z_u = wv.max(z_u);
-        ax_u = wv.max(ax_u);
-        pr_p = wv.max(pr_p);
-        z_p = wv.max(z_p);
-        ax_p = wv.max(ax_p);
-        dr_u = wv.max(dr_u);
-        q_u = wv.max(q_u);
-        aty_u = wv.max(aty_u);
-        px_u = wv.max(px_u);
-        dr_p = wv.max(dr_p);
-        q_p = wv.max(q_p);
-        aty_p = wv.max(aty_p);
-        px_p = wv.max(px_p);
+        {
+            double r[14] = {pr_u, z_u, ax_u, pr_p, z_p, ax_p, dr_u, q_u, aty_u, px_u, dr_p, q_p, aty_p, px_p};
+            wv.max_n(r);  // one team reduction for all 14 norms
+            pr_u = r[0], z_u = r[1], ax_u = r[2], pr_p = r[3], z_p = r[4], ax_p = r[5], dr_u = r[6];
+            q_u = r[7], aty_u = r[8], px_u = r[9], dr_p = r[10], q_p = r[11], aty_p = r[12], px_p = r[13];
+        }
         inf.pri_plain = pr_p;
         inf.dua_plain = dr_p;
         inf.pri_norm_s = dmax(z_p, ax_p);

@@ -72,6 +72,10 @@ struct EmuWave {
         for (int i = 1; i < NL; i++) r = b[i] > r ? b[i] : r;
         return r;
     }
+    template <int K>
+    void max_n(double (&v)[K]) {
+        for (int k = 0; k < K; k++) v[k] = max(v[k]);
+    }
     double sum(double v) {  // per-wavefront xor butterfly (lane 0's value), waves added in order
         double *b = next_buf();
         b[l] = v;
