@@ -22,6 +22,7 @@
 #include "../../include/impc_qp.h"
 #include "../../include/impc_select.h"
 #include "../../include/impc_mpc.h"
+#include "../../include/impc_fanout.h"
 #include "mpc_qp_internal.hpp"
 #include "admm_core.hpp"
 #include "mpc_structure.hpp"
@@ -1268,6 +1269,9 @@ int impc_copy_to_host(impc_ctx ctx, void *dst, const void *src, int64_t bytes) {
 
 // ---------------------------------------------------------------- candidate scoring / selection
 #include "select.hpp"
+
+// ---------------------------------------------------------------- intent-hypothesis fan-out
+#include "fanout.hpp"
 
 // ---------------------------------------------------------------- on-device MPC -> QP assembly
 #include "mpc_build.hpp"

@@ -139,6 +139,8 @@ _sig("impc_mpc_builder_create", C.c_int, _P, C.POINTER(MpcParams), C.c_int32, C.
 _sig("impc_mpc_builder_destroy", C.c_int, _P)
 _sig("impc_mpc_build_values_device", C.c_int, _P, C.c_int64, *([_P] * 14), _P)
 _sig("impc_mpc_warm_start", C.c_int, C.POINTER(MpcParams), C.c_int64, _dp, _dp, _dp)
+_sig("impc_intent_fanout", C.c_int, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int32, *([_P] * 16))
+_sig("impc_intent_fanout_device", C.c_int, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int32, *([_P] * 16), _P)
 
 # every symbol declared in include/*.h (checked by tests/test_abi.py)
 KERNEL_AUTO, KERNEL_GENERIC, KERNEL_STRUCTURED = 0, 1, 2
@@ -152,7 +154,7 @@ EXPORTED = [
     "impc_batch_get_timings", "impc_batch_set_kernel", "impc_batch_solve_group", "impc_device_alloc", "impc_device_free",
     "impc_copy_to_device", "impc_copy_to_host", "impc_select_best", "impc_select_best_device", "impc_mpc_dims",
     "impc_mpc_build_pattern", "impc_mpc_build_values", "impc_mpc_warm_start", "impc_mpc_builder_create",
-    "impc_mpc_builder_destroy", "impc_mpc_build_values_device",
+    "impc_mpc_builder_destroy", "impc_mpc_build_values_device", "impc_intent_fanout", "impc_intent_fanout_device",
 ]
 
 
@@ -386,6 +388,29 @@ def select_best(ctx, params, x_ptrs, valid, first_time, prev_states, prev_count,
                                 _d(keep["dp"]), _d(keep["ds"]), _d(keep["prob"]), v(best), v(pos), _d(scores),
                                 _d(weighted)), "impc_select_best")
     return dict(best_cand=best, best_pos=pos, scores=scores, weighted=weighted)
+
+
+def intent_fanout(ctx, curr_pos, first_time, prev_states, prev_count, dyn_cur, pred_pos, pred_size, prob):
+    """impc_intent_fanout: findClosestObstacle + getIntentComb for I instances on the device.
+
+    Shapes: curr_pos [I][3], first_time [I], prev_states [I][P][8], prev_count [I], dyn_cur
+    [I][K][3], pred_pos / pred_size [I][K][4][L][3], prob [I][K][4].  Returns dict(ob_idx,
+    cand_type [I][6], cand_slot [I][6], closest_prob [I][4], single_pos / single_size
+    [I][4][K][L][3], pair_pos / pair_size [I][2][K+1][L][3])."""
+    arr = lambda a, t: np.ascontiguousarray(a, dtype=t)  # noqa: E731
+    pp = arr(pred_pos, np.float64)
+    I, K, _, L, _ = pp.shape
+    prev = arr(prev_states, np.float64).reshape(I, -1, 8)
+    keep = [arr(curr_pos, np.float64), arr(first_time, np.int8), prev, arr(prev_count, np.int32),
+            arr(dyn_cur, np.float64), pp, arr(pred_size, np.float64), arr(prob, np.float64)]
+    out = dict(ob_idx=np.empty(I, np.int32), cand_type=np.empty((I, 6), np.int32), cand_slot=np.empty((I, 6), np.int32),
+               closest_prob=np.empty((I, 4)), single_pos=np.empty((I, 4, K, L, 3)),
+               single_size=np.empty((I, 4, K, L, 3)), pair_pos=np.empty((I, 2, K + 1, L, 3)),
+               pair_size=np.empty((I, 2, K + 1, L, 3)))
+    v = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    _check(lib.impc_intent_fanout(ctx.h, I, K, L, prev.shape[1], *[v(a) for a in keep], *[v(a) for a in out.values()]),
+           "impc_intent_fanout")
+    return out
 
 
 class MpcBuilder:
