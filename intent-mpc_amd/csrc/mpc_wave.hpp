@@ -75,7 +75,7 @@ struct WaveIO {
 // team accumulates s_memtime deltas per section; IMPC_SEC(X) closes section X.
 enum {
     kSecSetup, kSecFactor, kSecWarm, kSecRhs, kSecS1, kSecFwd, kSecS3, kSecBwd, kSecS5, kSecUpdate, kSecProducts,
-    kSecChecks, kSecOutput, kSecIters = 15, kSecCount = 16
+    kSecChecks, kSecOutput, kSecFAsm, kSecFDense, kSecIters = 15, kSecCount = 16
 };
 // The clock is the 100 MHz s_memrealtime counter (the one the time-limit path reads; a
 // SHADER_CYCLES s_getreg reads 0 on gfx950, and s_memtime perturbed the LDS wait counts of this
@@ -513,6 +513,7 @@ struct WaveQP {
                     A[dd] = val;
             }
             wv.sync();
+            IMPC_SEC(kSecFAsm);
             if (k > 0) {
                 if (L < 64) {
                     int i = L >> 3, j = L & 7;
@@ -591,6 +592,7 @@ struct WaveQP {
                 }
                 wv.sync();
             }
+            IMPC_SEC(kSecFDense);
         }
         _Pragma("unroll") for (int s = 0; s < VS; s++)
             if (vok[s] && vs_[s] == 0 && vr_[s] < 8)
@@ -1328,7 +1330,8 @@ struct WaveQP {
         }
         set_rho(dmin(dmax(st.rho, kRhoMin), kRhoMax));
         IMPC_SEC(kSecSetup);
-        int bad = factorize();
+        int bad = 0;
+        IMPC_REP(kSecFactor) bad = factorize();  // (phase-cost experiments only)
         IMPC_SEC(kSecFactor);
         impc_info *out = io.info + b;
         if (bad) {

@@ -18,7 +18,8 @@ os.environ.setdefault("IMPC_SECTION_PROF", "1")
 import impc  # noqa: E402
 from impc import scenarios  # noqa: E402
 
-NAMES = ["setup", "factor", "warm", "rhs", "S1", "fwd", "S3", "bwd", "S5", "update", "products", "checks", "output"]
+NAMES = ["setup", "factor", "warm", "rhs", "S1", "fwd", "S3", "bwd", "S5", "update", "products", "checks", "output",
+         "f-assembly", "f-dense"]
 
 
 def main():
@@ -42,7 +43,7 @@ def main():
         impc.lib.impc_debug_sections(b.h, sec)
         sec = np.array(sec[:], dtype=np.float64)
         iters = sec[15]
-        tot = sec[:13].sum()
+        tot = sec[:15].sum()
         tot_ns, per_ns = 10.0 * tot, 10.0 * sec
         print(f"K={K} B={B} kernel {b.timings()[1]:.1f} ms, mean iter {iters / B:.1f}, "
               f"us/QP {tot_ns / B / 1e3:.1f}, ns/iter {tot_ns / iters:.0f}")
