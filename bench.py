@@ -57,6 +57,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1024, help="QPs solved by the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-allgather", action="store_true")
+    ap.add_argument("--full-values", action="store_true",
+                    help="ship every QP's full CSC values (default: shared P / dynamics / box values, "
+                         "per-QP obstacle rows, impc_batch_set_values_shared)")
     args = ap.parse_args()
 
     import impc
@@ -73,13 +76,19 @@ def main():
     settings = impc.default_settings(verbose=0)
 
     ctx = impc.Context(local_rank if world > 1 else 0)
-    batches = []
+    batches, nvar = [], {}
     for K, bk in sorted(buckets.items()):
         pat, vals = bk["pattern"], bk["values"]
         B = vals["q"].shape[0]
         b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], B)
         b.set_settings(settings)
-        b.set_values(vals["Px"], vals["q"], vals["Ax"], vals["l"], vals["u"])
+        split = None if args.full_values else impc.shared_split(vals["Px"], vals["Ax"])
+        if split is None:
+            b.set_values(vals["Px"], vals["q"], vals["Ax"], vals["l"], vals["u"])
+        else:
+            Px0, Ax0, var, Axv = split
+            b.set_values_shared(Px0, Ax0, var, Axv, vals["q"], vals["l"], vals["u"])
+            nvar[K] = int(var.size)
         b.warm_start(bk["x_ws"], np.zeros((B, pat["m"])))
         b.set_profiling(True)
         batches.append((K, bk, b))
@@ -152,12 +161,14 @@ def main():
         pat = bk["pattern"]
         alg_flops += b.B * algorithmic_flops(pat["n"], pat["m"], int(pat["Ap"][-1]), 20, mean_iter)
     achieved = alg_bytes / (solve_ms * 1e-3) / 1e9 if solve_ms > 0 else None
+    values_mode = "shared" if nvar and len(nvar) == len(batches) else "full"
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_k_solve.json")
     if os.path.exists(pmc_path):
         try:
             pm = json.load(open(pmc_path))
-            if pm.get("qps_per_launch") == total_qps and pm.get("kernel") == kernel_name:
+            if pm.get("qps_per_launch") == total_qps and pm.get("kernel") == kernel_name and \
+                    pm.get("values", "full") == values_mode:
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -188,6 +199,8 @@ def main():
             "horizon": 20,
             "settings": "OSQP 0.6.2 defaults, adaptive_rho_interval auto->25, warm-started from previous plan",
             "parallelism": f"independent QPs, {world} rank(s)",
+            "values": values_mode + (f" (P and dynamics/box A entries once per bucket, per-QP A entries {nvar})"
+                                     if values_mode == "shared" else " (every QP's full CSC values)"),
         },
         "iters": {"mean": mean_iter, "p50": float(np.median(iters_all)), "max": int(iters_all.max())},
         "status_counts": {str(int(k)): int(v) for k, v in zip(*np.unique(status_all, return_counts=True))},

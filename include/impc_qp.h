@@ -135,6 +135,16 @@ int impc_batch_set_values(impc_batch b, const double *Px, const double *q, const
 int impc_batch_set_values_device(impc_batch b, const double *Px, const double *q, const double *Ax, const double *l,
                                  const double *u);
 
+/* Shared-structure values (host arrays): the batch's QPs share P and every A entry except the
+ * nvar positions var_pos (ascending indices into the CSC values of A) -- e.g. the replan QPs of
+ * one shape, whose dynamics / box entries are the same and whose obstacle-row entries differ.
+ * Px [nnzP] and Ax [nnzA] once, Ax_var [B][nvar], q [B][n], l [B][m], u [B][m] per QP.  The
+ * solve then reads the shared values from L2 instead of B copies from HBM; results are those of
+ * impc_batch_set_values on the expanded arrays. */
+int impc_batch_set_values_shared(impc_batch b, const double *Px, const double *Ax, int64_t nvar,
+                                 const int64_t *var_pos, const double *Ax_var, const double *q, const double *l,
+                                 const double *u);
+
 /* osqp_warm_start(x, y) for every QP (host, QP-major; y may be NULL = zero duals).
  * Pass x = NULL to clear a previous warm start (cold start). */
 int impc_batch_warm_start(impc_batch b, const double *x, const double *y);

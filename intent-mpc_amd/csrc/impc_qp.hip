@@ -405,6 +405,11 @@ struct impc_batch_s {
     impc_info *d_info = nullptr;
     int64_t device_bytes = 0;
     bool values_set = false, has_ws = false;
+    // shared-structure values (impc_batch_set_values_shared)
+    bool shared = false, shared_expanded = false;
+    int64_t nvar = 0, nvar_cap = -1;
+    double *d_shPx = nullptr, *d_shAx = nullptr, *d_Axv = nullptr;
+    int32_t *d_vmap = nullptr;
     // ---- structured path
     std::unique_ptr<impc::MpcStructure> ms;
     bool structured_ok = false;
@@ -489,6 +494,35 @@ int deinterleave(impc_batch b, const double *src, double *dst_dev, int64_t len, 
     return IMPC_OK;
 }
 
+// The structured kernel's view of a batch's inputs / outputs.
+impc::WaveIO wave_io(impc_batch b) {
+    impc::WaveIO io{b->B,        b->shared ? b->d_shPx : b->in_Px, b->in_q, b->shared ? b->d_shAx : b->in_Ax,
+                    b->in_l,     b->in_u,   b->in_xws, b->in_yws, b->has_ws ? 1 : 0, b->d_xout, b->d_yout,
+                    b->d_scal,   b->d_info};
+    if (b->shared) {
+        io.shared = 1;
+        io.nvar = b->nvar;
+        io.vmap = b->d_vmap;
+        io.Ax_var = b->d_Axv;
+    }
+    return io;
+}
+
+// Shared-structure values expanded into the QP-major input arrays (the generic kernel's input)
+__global__ void k_expand_shared(const double *Px, const double *Ax, const int32_t *vmap, const double *Axv,
+                                int64_t nvar, int64_t nnzP, int64_t nnzA, int64_t B, double *oPx, double *oAx) {
+    const int64_t tot = B * (nnzP + nnzA);
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+        if (e < B * nnzP) {
+            oPx[e] = Px[e % nnzP];
+        } else {
+            const int64_t f = e - B * nnzP, b = f / nnzA, p = f % nnzA;
+            const int32_t v = vmap[p];
+            oAx[f] = v >= 0 ? Axv[b * nvar + v] : Ax[p];
+        }
+    }
+}
+
 // ---- generic path: symbolic analysis + interleaved workspace, allocated on first use
 int ensure_generic(impc_batch b) {
     if (b->d_work) return IMPC_OK;
@@ -571,6 +605,14 @@ int ensure_generic(impc_batch b) {
 int generic_setup(impc_batch b, hipStream_t st) {
     int rc = ensure_generic(b);
     if (rc) return rc;
+    if (b->shared && !b->shared_expanded) {
+        const int64_t tot = b->B * (b->nnzP + b->nnzA);
+        const int64_t blocks = std::min<int64_t>((tot + 255) / 256, (int64_t)b->ctx->num_cu * 16);
+        hipLaunchKernelGGL(k_expand_shared, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, st, b->d_shPx,
+                           b->d_shAx, b->d_vmap, b->d_Axv, b->nvar, b->nnzP, b->nnzA, b->B, b->in_Px, b->in_Ax);
+        HIP_OK(hipGetLastError());
+        b->shared_expanded = true;
+    }
     impc::DevWork &w = b->dwk;
     if ((rc = interleave(b, b->in_Px, const_cast<double *>(w.Px), b->nnzP, st))) return rc;
     if ((rc = interleave(b, b->in_q, const_cast<double *>(w.q), b->n, st))) return rc;
@@ -653,8 +695,7 @@ int launch_wave(impc_batch b, hipStream_t st, const impc::WaveIO &io) {
 }
 
 int structured_solve(impc_batch b, hipStream_t st) {
-    impc::WaveIO io{b->B,        b->in_Px,  b->in_q,  b->in_Ax,  b->in_l,  b->in_u, b->in_xws, b->in_yws,
-                    b->has_ws ? 1 : 0, b->d_xout, b->d_yout, b->d_scal, b->d_info};
+    impc::WaveIO io = wave_io(b);
     HIP_OK(hipMemsetAsync(b->d_counter, 0, 256, st));
 #ifdef IMPC_SECTION_PROF
     if (!b->d_sec) {
@@ -908,8 +949,8 @@ int impc_batch_destroy(impc_batch b) {
     }
     for (hipEvent_t e : b->ev)
         if (e) (void)hipEventDestroy(e);
-    void *ptrs[] = {b->d_in, b->d_xout, b->d_yout, b->d_info, b->d_tables, b->d_scal, b->d_counter, b->d_sym,
-                    b->d_work, b->d_sec};
+    void *ptrs[] = {b->d_in,     b->d_xout,  b->d_yout,  b->d_info,  b->d_tables, b->d_scal, b->d_counter,
+                    b->d_sym,    b->d_work,  b->d_sec,   b->d_shPx,  b->d_shAx,   b->d_Axv,  b->d_vmap};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete b;
@@ -959,6 +1000,59 @@ int impc_batch_set_values(impc_batch b, const double *Px, const double *q, const
         IMPC_TRY(h2d_sync(b->ctx->stream, b->in_l, l, sizeof(double) * b->m * B));
         IMPC_TRY(h2d_sync(b->ctx->stream, b->in_u, u, sizeof(double) * b->m * B));
     }
+    b->shared = false;
+    b->values_set = true;
+    b->generic_dirty = true;
+    return IMPC_OK;
+}
+
+int impc_batch_set_values_shared(impc_batch b, const double *Px, const double *Ax, int64_t nvar,
+                                 const int64_t *var_pos, const double *Ax_var, const double *q, const double *l,
+                                 const double *u) {
+    if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
+    if ((b->nnzP && !Px) || !q || (b->nnzA && !Ax) || (b->m && (!l || !u)) || nvar < 0 || nvar > b->nnzA ||
+        (nvar && (!var_pos || !Ax_var)))
+        return fail(IMPC_INVALID_ARGUMENT, "null value array or bad nvar");
+    std::vector<int32_t> vmap((size_t)std::max<int64_t>(b->nnzA, 1), -1);
+    for (int64_t k = 0; k < nvar; k++) {
+        if (var_pos[k] < 0 || var_pos[k] >= b->nnzA || (k && var_pos[k] <= var_pos[k - 1]))
+            return fail(IMPC_DATA_VALIDATION_ERROR, "var_pos must be ascending positions in [0, nnzA)");
+        vmap[(size_t)var_pos[k]] = (int32_t)k;
+    }
+    for (int64_t k = 0; k < b->m * b->B; k++)
+        if (l[k] > u[k]) {
+            char msg[160];
+            std::snprintf(msg, sizeof msg, "lower bound greater than upper bound (QP %lld, row %lld)",
+                          (long long)(k / b->m), (long long)(k % b->m));
+            return fail(IMPC_DATA_VALIDATION_ERROR, msg);
+        }
+    HIP_OK(hipSetDevice(b->ctx->device));
+    hipStream_t st = b->ctx->stream;
+    HIP_OK(hipStreamSynchronize(st));  // no solve in flight reads the arrays replaced below
+    if (!b->d_shPx) {
+        HIP_OK(hipMalloc((void **)&b->d_shPx, sizeof(double) * std::max<int64_t>(b->nnzP, 1)));
+        HIP_OK(hipMalloc((void **)&b->d_shAx, sizeof(double) * std::max<int64_t>(b->nnzA, 1)));
+        HIP_OK(hipMalloc((void **)&b->d_vmap, sizeof(int32_t) * vmap.size()));
+    }
+    if (nvar > b->nvar_cap) {
+        if (b->d_Axv) HIP_OK(hipFree(b->d_Axv));
+        b->d_Axv = nullptr;
+        HIP_OK(hipMalloc((void **)&b->d_Axv, sizeof(double) * (size_t)std::max<int64_t>(nvar, 1) * (size_t)b->B));
+        b->nvar_cap = nvar;
+    }
+    const size_t B = (size_t)b->B;
+    IMPC_TRY(h2d_sync(st, b->d_shPx, Px, sizeof(double) * b->nnzP));
+    IMPC_TRY(h2d_sync(st, b->d_shAx, Ax, sizeof(double) * b->nnzA));
+    IMPC_TRY(h2d_sync(st, b->d_vmap, vmap.data(), sizeof(int32_t) * vmap.size()));
+    IMPC_TRY(h2d_sync(st, b->d_Axv, Ax_var, sizeof(double) * (size_t)nvar * B));
+    IMPC_TRY(h2d_sync(st, b->in_q, q, sizeof(double) * b->n * B));
+    if (b->m) {
+        IMPC_TRY(h2d_sync(st, b->in_l, l, sizeof(double) * b->m * B));
+        IMPC_TRY(h2d_sync(st, b->in_u, u, sizeof(double) * b->m * B));
+    }
+    b->nvar = nvar;
+    b->shared = true;
+    b->shared_expanded = false;
     b->values_set = true;
     b->generic_dirty = true;
     return IMPC_OK;
@@ -979,6 +1073,7 @@ int impc_batch_set_values_device(impc_batch b, const double *Px, const double *q
         HIP_OK(hipMemcpyAsync(b->in_l, l, sizeof(double) * b->m * B, hipMemcpyDeviceToDevice, st));
         HIP_OK(hipMemcpyAsync(b->in_u, u, sizeof(double) * b->m * B, hipMemcpyDeviceToDevice, st));
     }
+    b->shared = false;
     b->values_set = true;
     b->generic_dirty = true;
     return IMPC_OK;
@@ -1050,8 +1145,7 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
         impc_batch b = bs[k];
         GroupEntry &e = entries[(size_t)k];
         e.T = b->wt;
-        e.io = impc::WaveIO{b->B,        b->in_Px,  b->in_q,  b->in_Ax,  b->in_l,  b->in_u, b->in_xws, b->in_yws,
-                            b->has_ws ? 1 : 0, b->d_xout, b->d_yout, b->d_scal, b->d_info};
+        e.io = wave_io(b);
         e.st = b->dst;
         e.first = total;
         total += b->B;

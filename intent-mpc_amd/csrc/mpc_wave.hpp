@@ -69,6 +69,12 @@ struct WaveIO {
     double *scal;      // per-QP scratch [B][n + n + mg]: D, E(box), E(general)
     impc_info *info;
     unsigned long long *sec = nullptr;  // section-profiling build only: cycle sums [kSecCount]
+    // shared-structure values (impc_batch_set_values_shared): Px / Ax above are one copy each,
+    // A entry p is Ax_var[b][vmap[p]] when vmap[p] >= 0
+    int32_t shared = 0;
+    int64_t nvar = 0;
+    const int32_t *vmap = nullptr;
+    const double *Ax_var = nullptr;
 };
 
 // Section profiling (profiling build of the library only, -DIMPC_SECTION_PROF): lane 0 of each
@@ -273,7 +279,15 @@ struct WaveQP {
     // ------------------------------------------------------------------ load + scaling
     IMPC_WF void load(int64_t b) {
         const int n = T.n, m = T.m;
-        const int64_t bn = b * n, bm = b * m, bP = b * T.nnzP, bA = b * T.nnzA;
+        const int64_t bn = b * n, bm = b * m, bP = io.shared ? 0 : b * T.nnzP, bA = io.shared ? 0 : b * T.nnzA;
+        // A value at CSC position p of this QP (shared-structure batches: the per-QP override)
+        auto Aval = [&](int p) -> double {
+            if (io.shared) {
+                const int32_t v = io.vmap[p];
+                return v >= 0 ? io.Ax_var[b * io.nvar + v] : io.Ax[p];
+            }
+            return io.Ax[bA + p];
+        };
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             int v = NL * s + L;
             vok[s] = v < n;
@@ -286,7 +300,7 @@ struct WaveQP {
                 q[s] = io.q[bn + ov];
                 int pp = T.var_pdiag[v];
                 pd[s] = pp >= 0 ? io.Px[bP + pp] : 0.0;
-                ab[s] = io.Ax[bA + T.var_boxpos[v]];
+                ab[s] = Aval(T.var_boxpos[v]);
                 int br = T.var_boxrow[v];
                 lb[s] = dmin(dmax(io.l[bm + br], -kInf), kInf);
                 ub[s] = dmin(dmax(io.u[bm + br], -kInf), kInf);
@@ -308,7 +322,7 @@ struct WaveQP {
                     int col = T.gen_col[4 * g + e], pos = T.gen_pos[4 * g + e];
                     if (col >= 0) {
                         gc[s][e] = ((int)gs[4 * g + e] << 16) | col;
-                        a[s][e] = io.Ax[bA + pos];
+                        a[s][e] = Aval(pos);
                     }
                 }
                 int row = T.gen_row[g];

@@ -101,6 +101,7 @@ _sig("impc_batch_destroy", C.c_int, _P)
 _sig("impc_batch_set_settings", C.c_int, _P, C.POINTER(Settings))
 _sig("impc_batch_set_values", C.c_int, _P, _dp, _dp, _dp, _dp, _dp)
 _sig("impc_batch_set_values_device", C.c_int, _P, _P, _P, _P, _P, _P)
+_sig("impc_batch_set_values_shared", C.c_int, _P, _dp, _dp, C.c_int64, _i64p, _dp, _dp, _dp, _dp)
 _sig("impc_batch_warm_start", C.c_int, _P, _dp, _dp)
 _sig("impc_batch_setup", C.c_int, _P, _P)
 _sig("impc_batch_solve", C.c_int, _P, _P)
@@ -148,7 +149,7 @@ KERNEL_AUTO, KERNEL_GENERIC, KERNEL_STRUCTURED = 0, 1, 2
 EXPORTED = [
     "impc_default_settings", "impc_last_error", "impc_version", "impc_ctx_create", "impc_ctx_destroy",
     "impc_ctx_stream", "impc_ctx_synchronize", "impc_batch_create", "impc_batch_destroy", "impc_batch_set_settings",
-    "impc_batch_set_values", "impc_batch_set_values_device", "impc_batch_warm_start", "impc_batch_setup",
+    "impc_batch_set_values", "impc_batch_set_values_device", "impc_batch_set_values_shared", "impc_batch_warm_start", "impc_batch_setup",
     "impc_batch_solve", "impc_batch_get", "impc_batch_device_results", "impc_batch_update_lin_cost",
     "impc_batch_update_bounds", "impc_batch_get_stats", "impc_batch_get_perm", "impc_batch_set_profiling",
     "impc_batch_get_timings", "impc_batch_set_kernel", "impc_batch_solve_group", "impc_device_alloc", "impc_device_free",
@@ -232,6 +233,17 @@ class Batch:
         assert arrs[0].size == self.B * self.nnzP and arrs[1].size == self.B * self.n
         assert arrs[2].size == self.B * self.nnzA and arrs[3].size == self.B * self.m == arrs[4].size
         _check(lib.impc_batch_set_values(self.h, *[_d(a) for a in arrs]), "impc_batch_set_values")
+
+    def set_values_shared(self, Px, Ax, var_pos, Ax_var, q, l, u):
+        """Shared P / A values (one copy) with per-QP overrides Ax_var [B][len(var_pos)] at the A
+        positions var_pos, per-QP q, l, u (impc_batch_set_values_shared)."""
+        Px, Ax, Axv, q, l, u = [np.ascontiguousarray(a, dtype=np.float64) for a in (Px, Ax, Ax_var, q, l, u)]
+        vp = np.ascontiguousarray(var_pos, dtype=np.int64)
+        assert Px.size == self.nnzP and Ax.size == self.nnzA and Axv.size == self.B * vp.size
+        assert q.size == self.B * self.n and l.size == self.B * self.m == u.size
+        _check(lib.impc_batch_set_values_shared(self.h, _d(Px), _d(Ax), vp.size,
+                                                vp.ctypes.data_as(_i64p), _d(Axv), _d(q), _d(l), _d(u)),
+               "impc_batch_set_values_shared")
 
     def set_values_device(self, Px, q, Ax, l, u):
         """Device pointers (ints) of QP-major float64 arrays, e.g. torch tensors' data_ptr()."""
@@ -477,3 +489,14 @@ def solve_group(batches, stream=None):
     """impc_batch_solve_group: one persistent launch over several structured batches."""
     arr = (_P * len(batches))(*[b.h for b in batches])
     _check(lib.impc_batch_solve_group(arr, len(batches), _P(stream) if stream else None), "impc_batch_solve_group")
+
+
+def shared_split(Px, Ax):
+    """For a batch's QP-major Px [B][nnzP], Ax [B][nnzA]: (Px0, Ax0, var_pos, Ax_var) when P is the
+    same for every QP (None otherwise); var_pos are the A positions whose value differs between
+    QPs, Ax_var their per-QP values -- the inputs of Batch.set_values_shared."""
+    Px, Ax = np.asarray(Px), np.asarray(Ax)
+    if not (Px == Px[0]).all():
+        return None
+    var = np.flatnonzero((Ax != Ax[0]).any(axis=0))
+    return Px[0], Ax[0], var, np.ascontiguousarray(Ax[:, var])

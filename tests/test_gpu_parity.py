@@ -131,3 +131,37 @@ def test_grouped_launch_equals_separate_solves(ctx):
         assert np.array_equal(x0, x1) and np.array_equal(y0, y1) and np.array_equal(i0["iter"], i1["iter"])
     for b in sep + grp:
         b.close()
+
+
+def solve_shared(ctx, cfg, settings, kernel):
+    pat, v = cfg["pattern"], cfg["values"]
+    B = v["q"].shape[0]
+    split = impc.shared_split(v["Px"], v["Ax"])
+    assert split is not None
+    Px0, Ax0, var, Axv = split
+    b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], B)
+    try:
+        b.set_kernel(kernel)
+        b.set_settings(settings)
+        b.set_values_shared(Px0, Ax0, var, Axv, v["q"], v["l"], v["u"])
+        if cfg.get("x_ws") is not None:
+            b.warm_start(cfg["x_ws"], None)
+        b.solve()
+        return b.get(), var.size
+    finally:
+        b.close()
+
+
+@KERNELS
+def test_shared_structure_values_match_full_values(ctx, kernel):
+    """impc_batch_set_values_shared (P and the dynamics / box entries of A once, obstacle-row
+    entries per QP) gives bitwise the results of impc_batch_set_values on the same QPs."""
+    buckets = scenarios.intent_config(instances=16, seed=606)
+    s = impc.default_settings(**S25)
+    for K, bk in buckets.items():
+        (xs, ys, infs), nvar = solve_shared(ctx, bk, s, kernel)
+        assert 0 < nvar < bk["values"]["Ax"].shape[1]
+        xf, yf, inff = gpu(ctx, bk, s, kernel)
+        np.testing.assert_array_equal(xs, xf)
+        np.testing.assert_array_equal(ys, yf)
+        np.testing.assert_array_equal(infs["iter"], inff["iter"])

@@ -26,7 +26,7 @@ if [ -n "${PMC:-}" ]; then
   cd /tmp || exit 1
   timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/gpurun_out/pmc_fetch" -o pmc -- python3 "$R/bench.py" --steps 1 --warmup 0 --cpu-sample 0 > "$R/gpurun_out/pmc_fetch.log" 2>&1 || { tail -30 "$R/gpurun_out/pmc_fetch.log"; exit 1; }
   timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/gpurun_out/pmc_write" -o pmc -- python3 "$R/bench.py" --steps 1 --warmup 0 --cpu-sample 0 > "$R/gpurun_out/pmc_write.log" 2>&1 || { tail -30 "$R/gpurun_out/pmc_write.log"; exit 1; }
-  python3 "$R/tools/pmc_summary.py" "$R/gpurun_out/pmc_fetch" "$R/gpurun_out/pmc_write" k_mpc_wave_group 65536 > "$R/gpurun_out/pmc_k_solve.json" && cat "$R/gpurun_out/pmc_k_solve.json"
+  python3 "$R/tools/pmc_summary.py" "$R/gpurun_out/pmc_fetch" "$R/gpurun_out/pmc_write" k_mpc_wave_group 65536 shared > "$R/gpurun_out/pmc_k_solve.json" && cat "$R/gpurun_out/pmc_k_solve.json"
 fi
 if [ -n "${CONFIGS:-}" ]; then
   step configs
