@@ -274,6 +274,9 @@ struct GpuTeam {
             auto ql = __builtin_amdgcn_permlane32_swap(lo2, lo2, false, false);
             auto qh = __builtin_amdgcn_permlane32_swap(hi2, hi2, false, false);
             v[k] = mx(__hiloint2double(qh[0], ql[0]), __hiloint2double(qh[1], ql[1]));
+            // one value at a time: interleaving all K exchange chains would need ~2K extra VGPRs
+            // at a point where the whole per-QP state is live (measured: spills)
+            asm volatile("" : "+v"(v[k]));
         }
         if (NL == 64) return;
         if ((threadIdx.x & 63) == 0)
