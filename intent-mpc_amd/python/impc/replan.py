@@ -1,0 +1,117 @@
+"""makePlanWithPred (trajectory_planner mpcPlanner.cpp:571-661) for a batch of planning instances,
+with every stage on the device: the intent fan-out (impc_intent_fanout_device, :663-769), the
+MPC -> QP assembly of the two candidate shapes (impc_mpc_build_values_device, :891-1197), one
+grouped solve of all candidate QPs (impc_batch_solve_group, the OSQP call of solveTraj) and the
+candidate scoring / selection (impc_select_best, :771-887).
+
+Host work is limited to the per-candidate repetition of the instance inputs (every candidate of
+a replan is linearised at the same previous plan) and the small candidate-pointer table.
+"""
+import ctypes as C
+import time
+
+import numpy as np
+
+from . import (Batch, DeviceArray, MpcBuilder, _P, _check, lib, mpc_dims, mpc_pattern, select_best, solve_group)
+
+
+class DeviceReplan:
+    """Device buffers and solver batches for I instances with K dynamic obstacles each
+    (L prediction steps, horizon N = params.horizon)."""
+
+    def __init__(self, ctx, params, pd, I, K, L, settings):
+        self.ctx, self.params, self.pd, self.I, self.K, self.L = ctx, params, pd, I, K, L
+        self.N = params.horizon
+        N = self.N
+        self.fan = dict(ob_idx=DeviceArray(ctx, (I,), np.int32), cand_type=DeviceArray(ctx, (I, 6), np.int32),
+                        cand_slot=DeviceArray(ctx, (I, 6), np.int32), closest_prob=DeviceArray(ctx, (I, 4)),
+                        single_pos=DeviceArray(ctx, (I, 4, K, L, 3)), single_size=DeviceArray(ctx, (I, 4, K, L, 3)),
+                        pair_pos=DeviceArray(ctx, (I, 2, K + 1, L, 3)),
+                        pair_size=DeviceArray(ctx, (I, 2, K + 1, L, 3)))
+        self.shapes = []
+        for kk, nb in ((K, 4 * I), (K + 1, 2 * I)):
+            n, m, nnzP, nnzA = mpc_dims(params, 0, kk)
+            pat = mpc_pattern(params, 0, kk)
+            b = Batch(ctx, n, m, pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], nb)
+            b.set_settings(settings)
+            outs = [DeviceArray(ctx, (nb, k)) for k in (nnzP, n, nnzA, m, m)]
+            self.shapes.append(dict(K=kk, nb=nb, n=n, m=m, batch=b, builder=MpcBuilder(ctx, params, 0, kk, L),
+                                    vals=outs))
+
+    def run(self, pos, vel, xref, prev, first_time, prev_count, dyn_cur, pred_pos, pred_size, prob, timings=None):
+        """Returns dict(best_cand, cand_type, cand_slot, ob_idx, x_single, x_pair, info_single, info_pair)."""
+        I, K, L, N = self.I, self.K, self.L, self.N
+        t = {}
+        t0 = time.perf_counter()
+        din = [DeviceArray(self.ctx, np.ascontiguousarray(a, dt)) for a, dt in
+               ((pos, np.float64), (first_time, np.int8), (prev, np.float64), (prev_count, np.int32),
+                (dyn_cur, np.float64), (pred_pos, np.float64), (pred_size, np.float64), (prob, np.float64))]
+        # per-candidate copies of the instance inputs: 4 single-intent, 2 two-intent candidates
+        rep = {}
+        for cnt in (4, 2):
+            rep[cnt] = [DeviceArray(self.ctx, np.ascontiguousarray(np.repeat(a, cnt, axis=0)))
+                        for a in (pos, vel, xref, prev)]
+        x_ws = {cnt: np.repeat(np.concatenate([prev.reshape(I, -1), np.zeros((I, 5 * (N - 1)))], axis=1), cnt, axis=0)
+                for cnt in (4, 2)}
+        for sh, cnt in zip(self.shapes, (4, 2)):
+            sh["batch"].warm_start(x_ws[cnt], None)
+        self.ctx.synchronize()
+        t["upload_s"] = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        f = self.fan
+        _check(lib.impc_intent_fanout_device(
+            self.ctx.h, I, K, L, prev.shape[1], *[_P(d.ptr) for d in din],
+            *[_P(f[k].ptr) for k in ("ob_idx", "cand_type", "cand_slot", "closest_prob", "single_pos",
+                                     "single_size", "pair_pos", "pair_size")], None), "impc_intent_fanout_device")
+        for sh, cnt, dp, ds in zip(self.shapes, (4, 2), ("single_pos", "pair_pos"), ("single_size", "pair_size")):
+            r = rep[cnt]
+            sh["builder"].build(sh["nb"], r[0].ptr, r[1].ptr, r[2].ptr, r[3].ptr, None, None, None, f[dp].ptr,
+                                f[ds].ptr, *[v.ptr for v in sh["vals"]])
+            sh["batch"].set_values_device(*[sh["vals"][k].ptr for k in (0, 1, 2, 3, 4)])
+        solve_group([sh["batch"] for sh in self.shapes])
+        self.ctx.synchronize()
+        t["fanout_build_solve_s"] = time.perf_counter() - t0
+        # selection: candidate c of instance i is row slot (single) or slot - 4 (pair) of its shape
+        t0 = time.perf_counter()
+        slot = f["cand_slot"].get()
+        xs = [sh["batch"].device_results()[0] for sh in self.shapes]
+        ptr = np.empty((I, 6), np.uint64)
+        ii = np.arange(I)[:, None]
+        single = slot < 4
+        ptr[single] = (xs[0] + 8 * self.shapes[0]["n"] * (4 * ii + slot))[single]
+        ptr[~single] = (xs[1] + 8 * self.shapes[1]["n"] * (2 * ii + slot - 4))[~single]
+        # obstacle sets of each candidate in select's padded [I][C][K+1][L][3] layout
+        spos, ssz = f["single_pos"].get(), f["single_size"].get()
+        ppos, psz = f["pair_pos"].get(), f["pair_size"].get()
+        dyn_count = np.where(single, K, K + 1).astype(np.int32)
+        m5 = single[:, :, None, None, None]
+        gs_p, gs_s = spos[ii, np.where(single, slot, 0)], ssz[ii, np.where(single, slot, 0)]      # [I][6][K]
+        gp_p, gp_s = ppos[ii, np.where(single, 0, slot - 4)], psz[ii, np.where(single, 0, slot - 4)]  # [I][6][K+1]
+        dyn_pos = np.where(m5, np.concatenate([gs_p, np.zeros_like(gp_p[:, :, :1])], axis=2), gp_p)
+        dyn_size = np.where(m5, np.concatenate([gs_s, np.zeros_like(gp_s[:, :, :1])], axis=2), gp_s)
+        sp = dict(horizon=N, num_candidates=6, max_dynamic=K + 1, pred_len=L, num_static=0, prev_len=N,
+                  dynamic_safety_dist=self.pd["dynamic_safety_dist"], static_safety_dist=self.pd["static_safety_dist"])
+        sel = select_best(self.ctx, sp, ptr.reshape(-1), np.ones((I, 6), np.int8), np.asarray(first_time, np.int8),
+                          prev, np.full(I, N, np.int32), xref, np.zeros((I, 0, 3)), np.zeros((I, 0, 3)), dyn_count,
+                          dyn_pos, dyn_size, f["closest_prob"].get())
+        t["select_s"] = time.perf_counter() - t0
+        for d in din + rep[4] + rep[2]:
+            d.free()
+        if timings is not None:
+            timings.update(t)
+        out = dict(best_cand=sel["best_cand"], cand_type=f["cand_type"].get(), cand_slot=slot,
+                   ob_idx=f["ob_idx"].get())
+        for sh, nm in zip(self.shapes, ("single", "pair")):
+            x, y, info = sh["batch"].get()
+            out["x_" + nm], out["info_" + nm] = x, info
+            out["vals_" + nm] = [v.get() for v in sh["vals"]]
+        return out
+
+    def close(self):
+        for d in self.fan.values():
+            d.free()
+        for sh in self.shapes:
+            sh["batch"].close()
+            sh["builder"].close()
+            for v in sh["vals"]:
+                v.free()

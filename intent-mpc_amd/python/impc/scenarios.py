@@ -158,7 +158,8 @@ def intent_config(N=20, K=8, instances=8192, hyps=8, seed=3000, params=None):
             buckets[kk]["inst"].append(i)
             buckets[kk]["hyp"].append(h)
     # per-instance inputs of the candidate selection (makePlanWithPred / evaluateTraj)
-    inst_data = dict(prev=prev, xref=xref, prob=prob[np.arange(I), ob], closest=ob)
+    inst_data = dict(prev=prev, xref=xref, prob=prob[np.arange(I), ob], closest=ob,
+                     pos=pos, vel=vel, obp=obp, pred=pred, prob_all=prob, size=size)
     out = {}
     for kk, bk in buckets.items():
         if not bk["inst"]:
