@@ -125,6 +125,14 @@ def main():
     # per-kernel durations of the last step (HIP events on the solver stream)
     for K, _, b in batches:
         kt[K] = list(b.timings())
+    # per-QP device solve latency of the last step (structured kernel; work-queue pick-up to results)
+    try:
+        lat = np.concatenate([b.qp_latency() for _, _, b in batches])
+        qp_lat = {"p50": float(np.percentile(lat, 50)), "p90": float(np.percentile(lat, 90)),
+                  "p99": float(np.percentile(lat, 99)), "max": float(lat.max()), "unit": "ms",
+                  "what": "per-QP device solve latency (dequeue to results written), last timed step"}
+    except impc.ImpcError:
+        qp_lat = None
     elapsed = D.max_over_ranks(dist, elapsed)
     ms_per_step = 1000.0 * elapsed / args.steps
 
@@ -202,6 +210,7 @@ def main():
             "values": values_mode + (f" (P and dynamics/box A entries once per bucket, per-QP A entries {nvar})"
                                      if values_mode == "shared" else " (every QP's full CSC values)"),
         },
+        "qp_latency_ms": qp_lat,
         "iters": {"mean": mean_iter, "p50": float(np.median(iters_all)), "max": int(iters_all.max())},
         "status_counts": {str(int(k)): int(v) for k, v in zip(*np.unique(status_all, return_counts=True))},
         "kernel_ms": {"setup": setup_ms, "solve": solve_ms,

@@ -212,6 +212,11 @@ int impc_batch_set_profiling(impc_batch b, int on);
 /* Durations (ms) of the last profiled setup / solve-kernel / output-transpose launches. */
 int impc_batch_get_timings(impc_batch b, double *setup_ms, double *solve_ms, double *output_ms);
 
+/* Per-QP solve latency (ms) of the last profiled structured-kernel solve: from the moment a
+ * workgroup takes the QP off the work queue to its results being written (device wall clock,
+ * 100 MHz), for each of the B QPs.  Profiling must be on before the solve. */
+int impc_batch_get_qp_latency(impc_batch b, double *ms);
+
 /* Factor-order permutation chosen by the symbolic analysis (perm[k] = variable at position k). */
 int impc_batch_get_perm(impc_batch b, int64_t *perm);
 

@@ -408,6 +408,8 @@ struct impc_batch_s {
     impc_info *d_info = nullptr;
     int64_t device_bytes = 0;
     bool values_set = false, has_ws = false;
+    unsigned long long *d_qpt = nullptr;  // profiling: per-QP (start, end) device clock
+    bool qpt_valid = false;
     // shared-structure values (impc_batch_set_values_shared)
     bool shared = false, shared_expanded = false;
     int64_t nvar = 0, nvar_cap = -1;
@@ -502,6 +504,8 @@ impc::WaveIO wave_io(impc_batch b) {
     impc::WaveIO io{b->B,        b->shared ? b->d_shPx : b->in_Px, b->in_q, b->shared ? b->d_shAx : b->in_Ax,
                     b->in_l,     b->in_u,   b->in_xws, b->in_yws, b->has_ws ? 1 : 0, b->d_xout, b->d_yout,
                     b->d_scal,   b->d_info};
+    if (b->profile && b->d_qpt) io.qpt = b->d_qpt;
+    b->qpt_valid = io.qpt != nullptr;
     if (b->shared) {
         io.shared = 1;
         io.nvar = b->nvar;
@@ -640,6 +644,7 @@ int generic_setup(impc_batch b, hipStream_t st) {
 }
 
 int generic_solve(impc_batch b, hipStream_t st) {
+    b->qpt_valid = false;  // per-QP latency is recorded by the structured kernel only
     if (b->generic_dirty) {
         int rc = generic_setup(b, st);
         if (rc) return rc;
@@ -953,7 +958,8 @@ int impc_batch_destroy(impc_batch b) {
     for (hipEvent_t e : b->ev)
         if (e) (void)hipEventDestroy(e);
     void *ptrs[] = {b->d_in,     b->d_xout,  b->d_yout,  b->d_info,  b->d_tables, b->d_scal, b->d_counter,
-                    b->d_sym,    b->d_work,  b->d_sec,   b->d_shPx,  b->d_shAx,   b->d_Axv,  b->d_vmap};
+                    b->d_sym,    b->d_work,  b->d_sec,   b->d_shPx,  b->d_shAx,   b->d_Axv,  b->d_vmap,
+                    b->d_qpt};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete b;
@@ -1276,7 +1282,19 @@ int impc_batch_set_profiling(impc_batch b, int on) {
     HIP_OK(hipSetDevice(b->ctx->device));
     if (on && !b->ev[0])
         for (hipEvent_t &e : b->ev) HIP_OK(hipEventCreate(&e));
+    if (on && !b->d_qpt) HIP_OK(hipMalloc((void **)&b->d_qpt, sizeof(unsigned long long) * 2 * (size_t)b->B));
     b->profile = on != 0;
+    return IMPC_OK;
+}
+
+int impc_batch_get_qp_latency(impc_batch b, double *ms) {
+    if (!b || !ms) return fail(IMPC_INVALID_ARGUMENT, "null batch or output");
+    if (!b->qpt_valid) return fail(IMPC_INVALID_ARGUMENT, "no profiled structured-kernel solve");
+    HIP_OK(hipSetDevice(b->ctx->device));
+    HIP_OK(hipStreamSynchronize(b->ctx->stream));
+    std::vector<unsigned long long> t((size_t)b->B * 2);
+    HIP_OK(hipMemcpy(t.data(), b->d_qpt, sizeof(unsigned long long) * t.size(), hipMemcpyDeviceToHost));
+    for (int64_t k = 0; k < b->B; k++) ms[k] = (double)(t[2 * k + 1] - t[2 * k]) * 1e-5;  // 100 MHz ticks
     return IMPC_OK;
 }
 

@@ -69,6 +69,7 @@ struct WaveIO {
     double *scal;      // per-QP scratch [B][n + n + mg]: D, E(box), E(general)
     impc_info *info;
     unsigned long long *sec = nullptr;  // section-profiling build only: cycle sums [kSecCount]
+    unsigned long long *qpt = nullptr;  // profiling: per-QP (start, end) device clock [B][2]
     // shared-structure values (impc_batch_set_values_shared): Px / Ax above are one copy each,
     // A entry p is Ax_var[b][vmap[p]] when vmap[p] >= 0
     int32_t shared = 0;
@@ -1334,6 +1335,7 @@ struct WaveQP {
     // not occupy registers across the ADMM loop.
     IMPC_WF void solve(int64_t b) {
         const int n = T.n, m = T.m;
+        const uint64_t t_begin = io.qpt ? device_clock_100mhz() : 0;
         rw = (int)(b % (NL / 64));  // spread the serial recursions of co-resident QPs over SIMDs
         IMPC_SEC_START();
         clear_exchange();
@@ -1500,6 +1502,10 @@ struct WaveQP {
             if (!gok[s]) continue;
             double yv = has_sol2 ? (scaled ? (Eg[s] * y[s]) * cinv : y[s]) : kNan;
             io.yo[b * m + T.gen_row[NL * s + L]] = yv;
+        }
+        if (L == 0 && io.qpt) {
+            io.qpt[2 * b] = t_begin;
+            io.qpt[2 * b + 1] = device_clock_100mhz();
         }
         if (L == 0) {
             out->iter = info_iter;

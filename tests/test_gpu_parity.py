@@ -165,3 +165,23 @@ def test_shared_structure_values_match_full_values(ctx, kernel):
         np.testing.assert_array_equal(xs, xf)
         np.testing.assert_array_equal(ys, yf)
         np.testing.assert_array_equal(infs["iter"], inff["iter"])
+
+
+def test_per_qp_latency_recorded_by_structured_kernel(ctx):
+    cfg = scenarios.static_config(batch=64, identical=False, seed=808)
+    pat, v = cfg["pattern"], cfg["values"]
+    b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], 64)
+    try:
+        b.set_settings(impc.default_settings(verbose=0))
+        b.set_values(v["Px"], v["q"], v["Ax"], v["l"], v["u"])
+        b.set_profiling(True)
+        b.set_kernel(impc.KERNEL_STRUCTURED)
+        b.solve()
+        lat = b.qp_latency()
+        assert np.all(lat > 0) and np.all(lat < 1000)
+        b.set_kernel(impc.KERNEL_GENERIC)
+        b.solve()
+        with pytest.raises(impc.ImpcError):
+            b.qp_latency()
+    finally:
+        b.close()
