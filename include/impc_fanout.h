@@ -53,6 +53,17 @@ int impc_intent_fanout_device(impc_ctx ctx, int64_t instances, int32_t num_obsta
                               int32_t *cand_type, int32_t *cand_slot, double *closest_prob, double *single_pos,
                               double *single_size, double *pair_pos, double *pair_size, void *stream);
 
+/* The selection inputs of the replan's candidates, on the device: for candidate c of instance i
+ * (slot s = cand_slot[i][c]) the pointer to its QP solution -- x_single + (4 i + s) n_single or
+ * x_pair + (2 i + s - 4) n_pair doubles -- its obstacle count (K or K + 1) and its obstacle sets
+ * in impc_select_best_device's padded [I][6][K+1][L][3] layout (zero-filled slot K for the
+ * single-intent candidates).  Everything stays on the device; asynchronous on `stream`. */
+int impc_fanout_candidates_device(impc_ctx ctx, int64_t instances, int32_t num_obstacles, int32_t pred_len,
+                                  const int32_t *cand_slot, const double *single_pos, const double *single_size,
+                                  const double *pair_pos, const double *pair_size, const double *x_single,
+                                  int64_t n_single, const double *x_pair, int64_t n_pair, const double **x_cand,
+                                  int32_t *dyn_count, double *dyn_pos, double *dyn_size, void *stream);
+
 /* Same with host arrays (copied to / from the device; synchronous). */
 int impc_intent_fanout(impc_ctx ctx, int64_t instances, int32_t num_obstacles, int32_t pred_len, int32_t prev_len,
                        const double *curr_pos, const int8_t *first_time, const double *prev_states,

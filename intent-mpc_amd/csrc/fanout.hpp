@@ -138,7 +138,66 @@ __global__ __launch_bounds__(256) void k_fanout_copy(Args a) {
     }
 }
 
+// candidate -> (solution pointer, obstacle count, padded obstacle sets) for impc_select_best
+__global__ __launch_bounds__(256) void k_fanout_candidates(int64_t I, int K, int L, const int32_t *cand_slot,
+                                                           const double *spos, const double *ssz, const double *ppos,
+                                                           const double *psz, const double *xs, int64_t ns,
+                                                           const double *xp, int64_t np, const double **x_cand,
+                                                           int32_t *dyn_count, double *dpos, double *dsz) {
+    const int64_t rows = (int64_t)(K + 1) * L, total = I * 6 * rows;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t ic = e / rows, i = ic / 6;
+        const int r = (int)(e - ic * rows), o = r / L, st = r % L;
+        const int s = cand_slot[ic];
+        const bool pair = s >= 4;
+        if (r == 0) {
+            x_cand[ic] = pair ? xp + (2 * i + s - 4) * np : xs + (4 * i + s) * ns;
+            dyn_count[ic] = pair ? K + 1 : K;
+        }
+        const double *sp, *sz;
+        if (pair) {
+            const int64_t src = (((i * 2 + s - 4) * (int64_t)(K + 1) + o) * L + st) * 3;
+            sp = ppos + src;
+            sz = psz + src;
+        } else {
+            const int64_t src = (((i * 4 + s) * (int64_t)K + (o < K ? o : 0)) * L + st) * 3;
+            sp = spos + src;
+            sz = ssz + src;
+        }
+        const bool pad = !pair && o == K;
+        for (int d = 0; d < 3; d++) {
+            dpos[e * 3 + d] = pad ? 0.0 : sp[d];
+            dsz[e * 3 + d] = pad ? 0.0 : sz[d];
+        }
+    }
+}
+
 }  // namespace impc_fanout
+
+extern "C" int impc_fanout_candidates_device(impc_ctx ctx, int64_t instances, int32_t num_obstacles,
+                                             int32_t pred_len, const int32_t *cand_slot, const double *single_pos,
+                                             const double *single_size, const double *pair_pos,
+                                             const double *pair_size, const double *x_single, int64_t n_single,
+                                             const double *x_pair, int64_t n_pair, const double **x_cand,
+                                             int32_t *dyn_count, double *dyn_pos, double *dyn_size, void *stream) {
+    if (!ctx) return fail(IMPC_INVALID_ARGUMENT, "null context");
+    if (instances < 0 || num_obstacles < 1 || pred_len < 1 || n_single < 1 || n_pair < 1)
+        return fail(IMPC_INVALID_ARGUMENT, "fanout candidates: bad sizes");
+    if (instances == 0) return IMPC_OK;
+    if (!cand_slot || !single_pos || !single_size || !pair_pos || !pair_size || !x_single || !x_pair || !x_cand ||
+        !dyn_count || !dyn_pos || !dyn_size)
+        return fail(IMPC_INVALID_ARGUMENT, "fanout candidates: null argument");
+    HIP_OK(hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    const int64_t total = instances * 6 * (int64_t)(num_obstacles + 1) * pred_len;
+    const int64_t blocks = std::min<int64_t>((total + 255) / 256, (int64_t)ctx->num_cu * 16);
+    hipLaunchKernelGGL(impc_fanout::k_fanout_candidates, dim3((unsigned)blocks), dim3(256), 0, st, instances,
+                       num_obstacles, pred_len, cand_slot, single_pos, single_size, pair_pos, pair_size, x_single,
+                       n_single, x_pair, n_pair, x_cand, dyn_count, dyn_pos, dyn_size);
+    HIP_OK(hipGetLastError());
+    return IMPC_OK;
+}
 
 extern "C" int impc_intent_fanout_device(impc_ctx ctx, int64_t instances, int32_t num_obstacles, int32_t pred_len,
                                          int32_t prev_len, const double *curr_pos, const int8_t *first_time,

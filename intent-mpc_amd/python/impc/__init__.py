@@ -143,6 +143,8 @@ _sig("impc_mpc_build_values_device", C.c_int, _P, C.c_int64, *([_P] * 14), _P)
 _sig("impc_mpc_warm_start", C.c_int, C.POINTER(MpcParams), C.c_int64, _dp, _dp, _dp)
 _sig("impc_intent_fanout", C.c_int, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int32, *([_P] * 16))
 _sig("impc_intent_fanout_device", C.c_int, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int32, *([_P] * 16), _P)
+_sig("impc_fanout_candidates_device", C.c_int, _P, C.c_int64, C.c_int32, C.c_int32, _P, _P, _P, _P, _P, _P,
+     C.c_int64, _P, C.c_int64, _P, _P, _P, _P, _P)
 
 # every symbol declared in include/*.h (checked by tests/test_abi.py)
 KERNEL_AUTO, KERNEL_GENERIC, KERNEL_STRUCTURED = 0, 1, 2
@@ -157,6 +159,7 @@ EXPORTED = [
     "impc_copy_to_device", "impc_copy_to_host", "impc_select_best", "impc_select_best_device", "impc_mpc_dims",
     "impc_mpc_build_pattern", "impc_mpc_build_values", "impc_mpc_warm_start", "impc_mpc_builder_create",
     "impc_mpc_builder_destroy", "impc_mpc_build_values_device", "impc_intent_fanout", "impc_intent_fanout_device",
+    "impc_fanout_candidates_device",
 ]
 
 

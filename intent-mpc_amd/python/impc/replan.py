@@ -5,14 +5,15 @@ grouped solve of all candidate QPs (impc_batch_solve_group, the OSQP call of sol
 candidate scoring / selection (impc_select_best, :771-887).
 
 Host work is limited to the per-candidate repetition of the instance inputs (every candidate of
-a replan is linearised at the same previous plan) and the small candidate-pointer table.
+a replan is linearised at the same previous plan); the candidate table of the selection is built
+on the device (impc_fanout_candidates_device).
 """
 import ctypes as C
 import time
 
 import numpy as np
 
-from . import (Batch, DeviceArray, MpcBuilder, _P, _check, lib, mpc_dims, mpc_pattern, select_best, solve_group)
+from . import (Batch, DeviceArray, MpcBuilder, SelectParams, _P, _check, lib, mpc_dims, mpc_pattern, solve_group)
 
 
 class DeviceReplan:
@@ -28,6 +29,11 @@ class DeviceReplan:
                         single_pos=DeviceArray(ctx, (I, 4, K, L, 3)), single_size=DeviceArray(ctx, (I, 4, K, L, 3)),
                         pair_pos=DeviceArray(ctx, (I, 2, K + 1, L, 3)),
                         pair_size=DeviceArray(ctx, (I, 2, K + 1, L, 3)))
+        self.sel = dict(x_cand=DeviceArray(ctx, (I, 6), np.uint64), dyn_count=DeviceArray(ctx, (I, 6), np.int32),
+                        dyn_pos=DeviceArray(ctx, (I, 6, K + 1, L, 3)), dyn_size=DeviceArray(ctx, (I, 6, K + 1, L, 3)),
+                        valid=DeviceArray(ctx, np.ones((I, 6), np.int8)), best_cand=DeviceArray(ctx, (I,), np.int32),
+                        best_pos=DeviceArray(ctx, (I,), np.int32), scores=DeviceArray(ctx, (I, 6, 3)),
+                        weighted=DeviceArray(ctx, (I, 6)))
         self.shapes = []
         for kk, nb in ((K, 4 * I), (K + 1, 2 * I)):
             n, m, nnzP, nnzA = mpc_dims(params, 0, kk)
@@ -46,6 +52,7 @@ class DeviceReplan:
         din = [DeviceArray(self.ctx, np.ascontiguousarray(a, dt)) for a, dt in
                ((pos, np.float64), (first_time, np.int8), (prev, np.float64), (prev_count, np.int32),
                 (dyn_cur, np.float64), (pred_pos, np.float64), (pred_size, np.float64), (prob, np.float64))]
+        xref_d = DeviceArray(self.ctx, np.ascontiguousarray(xref, np.float64))
         # per-candidate copies of the instance inputs: 4 single-intent, 2 two-intent candidates
         rep = {}
         for cnt in (4, 2):
@@ -71,35 +78,34 @@ class DeviceReplan:
         solve_group([sh["batch"] for sh in self.shapes])
         self.ctx.synchronize()
         t["fanout_build_solve_s"] = time.perf_counter() - t0
-        # selection: candidate c of instance i is row slot (single) or slot - 4 (pair) of its shape
+        # selection, on the device: the candidate table (solution pointers, obstacle sets in the
+        # selection's padded layout) from the fan-out outputs, then scoring + evaluateTraj
         t0 = time.perf_counter()
-        slot = f["cand_slot"].get()
+        sel = self.sel
         xs = [sh["batch"].device_results()[0] for sh in self.shapes]
-        ptr = np.empty((I, 6), np.uint64)
-        ii = np.arange(I)[:, None]
-        single = slot < 4
-        ptr[single] = (xs[0] + 8 * self.shapes[0]["n"] * (4 * ii + slot))[single]
-        ptr[~single] = (xs[1] + 8 * self.shapes[1]["n"] * (2 * ii + slot - 4))[~single]
-        # obstacle sets of each candidate in select's padded [I][C][K+1][L][3] layout
-        spos, ssz = f["single_pos"].get(), f["single_size"].get()
-        ppos, psz = f["pair_pos"].get(), f["pair_size"].get()
-        dyn_count = np.where(single, K, K + 1).astype(np.int32)
-        m5 = single[:, :, None, None, None]
-        gs_p, gs_s = spos[ii, np.where(single, slot, 0)], ssz[ii, np.where(single, slot, 0)]      # [I][6][K]
-        gp_p, gp_s = ppos[ii, np.where(single, 0, slot - 4)], psz[ii, np.where(single, 0, slot - 4)]  # [I][6][K+1]
-        dyn_pos = np.where(m5, np.concatenate([gs_p, np.zeros_like(gp_p[:, :, :1])], axis=2), gp_p)
-        dyn_size = np.where(m5, np.concatenate([gs_s, np.zeros_like(gp_s[:, :, :1])], axis=2), gp_s)
-        sp = dict(horizon=N, num_candidates=6, max_dynamic=K + 1, pred_len=L, num_static=0, prev_len=N,
-                  dynamic_safety_dist=self.pd["dynamic_safety_dist"], static_safety_dist=self.pd["static_safety_dist"])
-        sel = select_best(self.ctx, sp, ptr.reshape(-1), np.ones((I, 6), np.int8), np.asarray(first_time, np.int8),
-                          prev, np.full(I, N, np.int32), xref, np.zeros((I, 0, 3)), np.zeros((I, 0, 3)), dyn_count,
-                          dyn_pos, dyn_size, f["closest_prob"].get())
+        _check(lib.impc_fanout_candidates_device(
+            self.ctx.h, I, K, L, _P(f["cand_slot"].ptr), _P(f["single_pos"].ptr), _P(f["single_size"].ptr),
+            _P(f["pair_pos"].ptr), _P(f["pair_size"].ptr), _P(xs[0]), self.shapes[0]["n"], _P(xs[1]),
+            self.shapes[1]["n"], _P(sel["x_cand"].ptr), _P(sel["dyn_count"].ptr), _P(sel["dyn_pos"].ptr),
+            _P(sel["dyn_size"].ptr), None), "impc_fanout_candidates_device")
+        sp = SelectParams(horizon=N, num_candidates=6, max_dynamic=K + 1, pred_len=L, num_static=0,
+                          prev_len=prev.shape[1], dynamic_safety_dist=self.pd["dynamic_safety_dist"],
+                          static_safety_dist=self.pd["static_safety_dist"])
+        _check(lib.impc_select_best_device(
+            self.ctx.h, C.byref(sp), I, _P(sel["x_cand"].ptr), _P(sel["valid"].ptr), _P(din[1].ptr),
+            _P(din[2].ptr), _P(din[3].ptr), _P(xref_d.ptr), None, None, _P(sel["dyn_count"].ptr),
+            _P(sel["dyn_pos"].ptr), _P(sel["dyn_size"].ptr), _P(f["closest_prob"].ptr), _P(sel["best_cand"].ptr),
+            _P(sel["best_pos"].ptr), _P(sel["scores"].ptr), _P(sel["weighted"].ptr), None),
+            "impc_select_best_device")
+        self.ctx.synchronize()
+        din.append(xref_d)
+        slot = f["cand_slot"].get()
         t["select_s"] = time.perf_counter() - t0
         for d in din + rep[4] + rep[2]:
             d.free()
         if timings is not None:
             timings.update(t)
-        out = dict(best_cand=sel["best_cand"], cand_type=f["cand_type"].get(), cand_slot=slot,
+        out = dict(best_cand=sel["best_cand"].get(), cand_type=f["cand_type"].get(), cand_slot=slot,
                    ob_idx=f["ob_idx"].get())
         for sh, nm in zip(self.shapes, ("single", "pair")):
             x, y, info = sh["batch"].get()
@@ -108,7 +114,7 @@ class DeviceReplan:
         return out
 
     def close(self):
-        for d in self.fan.values():
+        for d in list(self.fan.values()) + list(self.sel.values()):
             d.free()
         for sh in self.shapes:
             sh["batch"].close()

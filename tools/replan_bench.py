@@ -42,7 +42,7 @@ def main():
     print(json.dumps({"instances": I, "candidate_qps": qps, "device_stages_s": t["fanout_build_solve_s"],
                       "replans_per_s_device": I / t["fanout_build_solve_s"],
                       "qp_solves_per_s_incl_fanout_build": qps / t["fanout_build_solve_s"],
-                      "upload_s": t["upload_s"], "select_incl_host_gather_s": t["select_s"], "total_s": t["total_s"],
+                      "upload_s": t["upload_s"], "select_device_s": t["select_s"], "total_s": t["total_s"],
                       "mean_iter": float(np.concatenate([out["info_single"]["iter"], out["info_pair"]["iter"]]).mean()),
                       "picked_histogram": np.bincount(out["best_cand"][out["best_cand"] >= 0], minlength=6).tolist()}))
     rp.close()
