@@ -23,6 +23,7 @@
 #include "../../include/impc_select.h"
 #include "../../include/impc_mpc.h"
 #include "../../include/impc_fanout.h"
+#include "../../include/impc_predict.h"
 #include "mpc_qp_internal.hpp"
 #include "admm_core.hpp"
 #include "mpc_structure.hpp"
@@ -1387,6 +1388,9 @@ int impc_copy_to_host(impc_ctx ctx, void *dst, const void *src, int64_t bytes) {
 
 // ---------------------------------------------------------------- intent-hypothesis fan-out
 #include "fanout.hpp"
+
+// ---------------------------------------------------------------- obstacle intent probabilities
+#include "predict.hpp"
 
 // ---------------------------------------------------------------- on-device MPC -> QP assembly
 #include "mpc_build.hpp"

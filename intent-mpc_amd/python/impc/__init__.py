@@ -143,6 +143,16 @@ _sig("impc_mpc_build_values_device", C.c_int, _P, C.c_int64, *([_P] * 14), _P)
 _sig("impc_mpc_warm_start", C.c_int, C.POINTER(MpcParams), C.c_int64, _dp, _dp, _dp)
 _sig("impc_intent_fanout", C.c_int, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int32, *([_P] * 16))
 _sig("impc_intent_fanout_device", C.c_int, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int32, *([_P] * 16), _P)
+class IntentParams(C.Structure):
+    """impc_intent_params (include/impc_predict.h)."""
+    _fields_ = [("paramf", C.c_double), ("paraml", C.c_double), ("paramr", C.c_double), ("params", C.c_double),
+                ("pscale", C.c_double)]
+
+
+_sig("impc_intent_params_from_config", C.c_int, C.c_double, C.c_double, C.c_double, C.c_double,
+     C.POINTER(IntentParams))
+_sig("impc_intent_prob", C.c_int, _P, C.POINTER(IntentParams), C.c_int64, C.c_int32, _P, _P, _P, _P)
+_sig("impc_intent_prob_device", C.c_int, _P, C.POINTER(IntentParams), C.c_int64, C.c_int32, _P, _P, _P, _P, _P)
 _sig("impc_fanout_candidates_device", C.c_int, _P, C.c_int64, C.c_int32, C.c_int32, _P, _P, _P, _P, _P, _P,
      C.c_int64, _P, C.c_int64, _P, _P, _P, _P, _P)
 
@@ -159,7 +169,7 @@ EXPORTED = [
     "impc_copy_to_device", "impc_copy_to_host", "impc_select_best", "impc_select_best_device", "impc_mpc_dims",
     "impc_mpc_build_pattern", "impc_mpc_build_values", "impc_mpc_warm_start", "impc_mpc_builder_create",
     "impc_mpc_builder_destroy", "impc_mpc_build_values_device", "impc_intent_fanout", "impc_intent_fanout_device",
-    "impc_fanout_candidates_device",
+    "impc_fanout_candidates_device", "impc_intent_params_from_config", "impc_intent_prob", "impc_intent_prob_device",
 ]
 
 
@@ -510,3 +520,23 @@ def shared_split(Px, Ax):
         return None
     var = np.flatnonzero((Ax != Ax[0]).any(axis=0))
     return Px[0], Ax[0], var, np.ascontiguousarray(Ax[:, var])
+
+
+def intent_params(max_front_prob=0.5, front_angle_deg=10.0, stop_velocity=0.1, prob_scale=5.0):
+    """impc_intent_params_from_config (defaults: the reference's predictor_param.yaml)."""
+    ip = IntentParams()
+    _check(lib.impc_intent_params_from_config(max_front_prob, front_angle_deg, stop_velocity, prob_scale,
+                                              C.byref(ip)), "impc_intent_params_from_config")
+    return ip
+
+
+def intent_prob(ctx, ip, pos_hist, vel_hist, hist_len):
+    """impc_intent_prob: pos_hist / vel_hist [count][H][3] (entry 0 newest), hist_len [count]."""
+    ph = np.ascontiguousarray(pos_hist, np.float64)
+    vh = np.ascontiguousarray(vel_hist, np.float64)
+    hl = np.ascontiguousarray(hist_len, np.int32)
+    count, H = ph.shape[0], ph.shape[1]
+    out = np.empty((count, 4))
+    v = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    _check(lib.impc_intent_prob(ctx.h, C.byref(ip), count, H, v(hl), v(ph), v(vh), v(out)), "impc_intent_prob")
+    return out
