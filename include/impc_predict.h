@@ -18,8 +18,6 @@
  *                                      pscale)
  *   genTransitionVector      :257-281  FORWARD / LEFT / RIGHT / STOP probabilities
  * Intent indices follow dynamicPredictor's enum: FORWARD, LEFT, RIGHT, STOP = 0..3.
- * (The trajectory half, predTraj, samples motion models against the occupancy map and is not
- * part of this library.)
  */
 #ifndef IMPC_PREDICT_H
 #define IMPC_PREDICT_H
@@ -51,6 +49,44 @@ int impc_intent_prob_device(impc_ctx ctx, const impc_intent_params *p, int64_t c
 /* Same with host arrays (copied to / from the device; synchronous). */
 int impc_intent_prob(impc_ctx ctx, const impc_intent_params *p, int64_t count, int32_t H, const int32_t *hist_len,
                      const double *pos_hist, const double *vel_hist, double *prob);
+
+/* ---- Trajectory half: predTraj (dynamicPredictor.cpp:283-566) -- per obstacle and intent the
+ * motion-model samples (FORWARD :351-396: heading x speed grid, speeds ascend until the first
+ * sample that hits the map; LEFT / RIGHT :398-472: speed x turn rate x end heading grid, hitting
+ * samples dropped; STOP / slow obstacles :474-488: stationary with growing size), their mean and
+ * variance (genTraj :501-538: size += 2 sqrt(var) z_score) and positionCorrection (:540-566: a
+ * mean that hits the map is replaced by the closest sample).  The map is map_manager's inflated
+ * occupancy grid (occupancyMap.h:218-269): voxel (floor((p - origin) / res)), outside the grid
+ * counts as occupied, address x * dims[1] * dims[2] + y * dims[2] + z. */
+typedef struct {
+    double origin[3];    /* mapSizeMin_ */
+    double resolution;   /* mapRes_ */
+    int32_t dims[3];     /* mapVoxelMax_ (mapVoxelMin_ = 0) */
+    int32_t reserved;
+} impc_occ_map;
+
+typedef struct {
+    int32_t num_pred;          /* prediction_size: num_pred + 1 points per trajectory */
+    int32_t reserved;
+    double dt;                 /* prediction_time_step */
+    double stop_velocity;      /* stop_velocity_thereshold */
+    double front_angle_deg;    /* front_angle (degrees, as the ROS parameter) */
+    double min_turning_time, max_turning_time;
+    double z_score;            /* prediction_z_score */
+} impc_traj_params;
+
+/* DEVICE pointers; asynchronous.  occ_inflated [dims[0] * dims[1] * dims[2]] (nonzero =
+ * occupied); per obstacle the newest history entry pos, vel, size [count][3]; outputs
+ * pred_pos / pred_size [count][4][num_pred + 1][3] (obPredPos_ / obPredSize_, the fan-out's
+ * pred_pos / pred_size). */
+int impc_predict_traj_device(impc_ctx ctx, const impc_traj_params *tp, const impc_occ_map *map,
+                             const uint8_t *occ_inflated, int64_t count, const double *pos, const double *vel,
+                             const double *size, double *pred_pos, double *pred_size, void *stream);
+
+/* Same with host arrays (synchronous). */
+int impc_predict_traj(impc_ctx ctx, const impc_traj_params *tp, const impc_occ_map *map, const uint8_t *occ_inflated,
+                      int64_t count, const double *pos, const double *vel, const double *size, double *pred_pos,
+                      double *pred_size);
 
 #ifdef __cplusplus
 }

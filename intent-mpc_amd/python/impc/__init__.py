@@ -153,6 +153,22 @@ _sig("impc_intent_params_from_config", C.c_int, C.c_double, C.c_double, C.c_doub
      C.POINTER(IntentParams))
 _sig("impc_intent_prob", C.c_int, _P, C.POINTER(IntentParams), C.c_int64, C.c_int32, _P, _P, _P, _P)
 _sig("impc_intent_prob_device", C.c_int, _P, C.POINTER(IntentParams), C.c_int64, C.c_int32, _P, _P, _P, _P, _P)
+class OccMap(C.Structure):
+    """impc_occ_map (include/impc_predict.h)."""
+    _fields_ = [("origin", C.c_double * 3), ("resolution", C.c_double), ("dims", C.c_int32 * 3),
+                ("reserved", C.c_int32)]
+
+
+class TrajParams(C.Structure):
+    """impc_traj_params (include/impc_predict.h)."""
+    _fields_ = [("num_pred", C.c_int32), ("reserved", C.c_int32), ("dt", C.c_double), ("stop_velocity", C.c_double),
+                ("front_angle_deg", C.c_double), ("min_turning_time", C.c_double), ("max_turning_time", C.c_double),
+                ("z_score", C.c_double)]
+
+
+_sig("impc_predict_traj", C.c_int, _P, C.POINTER(TrajParams), C.POINTER(OccMap), _P, C.c_int64, _P, _P, _P, _P, _P)
+_sig("impc_predict_traj_device", C.c_int, _P, C.POINTER(TrajParams), C.POINTER(OccMap), _P, C.c_int64, _P, _P, _P,
+     _P, _P, _P)
 _sig("impc_fanout_candidates_device", C.c_int, _P, C.c_int64, C.c_int32, C.c_int32, _P, _P, _P, _P, _P, _P,
      C.c_int64, _P, C.c_int64, _P, _P, _P, _P, _P)
 
@@ -170,6 +186,7 @@ EXPORTED = [
     "impc_mpc_build_pattern", "impc_mpc_build_values", "impc_mpc_warm_start", "impc_mpc_builder_create",
     "impc_mpc_builder_destroy", "impc_mpc_build_values_device", "impc_intent_fanout", "impc_intent_fanout_device",
     "impc_fanout_candidates_device", "impc_intent_params_from_config", "impc_intent_prob", "impc_intent_prob_device",
+    "impc_predict_traj", "impc_predict_traj_device",
 ]
 
 
@@ -540,3 +557,16 @@ def intent_prob(ctx, ip, pos_hist, vel_hist, hist_len):
     v = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
     _check(lib.impc_intent_prob(ctx.h, C.byref(ip), count, H, v(hl), v(ph), v(vh), v(out)), "impc_intent_prob")
     return out
+
+
+def predict_traj(ctx, tp, omap, occ, pos, vel, size):
+    """impc_predict_traj: per obstacle [count][3] inputs -> pred_pos, pred_size [count][4][P+1][3]."""
+    v = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    occ = np.ascontiguousarray(occ, np.uint8)
+    pos, vel, size = [np.ascontiguousarray(a, np.float64) for a in (pos, vel, size)]
+    count = pos.shape[0]
+    pp = np.empty((count, 4, tp.num_pred + 1, 3))
+    ps = np.empty_like(pp)
+    _check(lib.impc_predict_traj(ctx.h, C.byref(tp), C.byref(omap), v(occ), count, v(pos), v(vel), v(size), v(pp),
+                                 v(ps)), "impc_predict_traj")
+    return pp, ps

@@ -69,3 +69,154 @@ def intent_prob(p, pos_hist, vel_hist):
             nP.append(acc)
         P = nP
     return P
+
+
+# ---------------------------------------------------------------- trajectory prediction (predTraj)
+# dynamicPredictor.cpp:283-566 with the occupancy map of map_manager (occupancyMap.h:218-269:
+# posToIndex = floor((p - mapSizeMin) / res), outside [0, mapVoxelMax) counts as occupied,
+# address = x * max_y * max_z + y * max_z + z).  Eigen's 4x4 state update is x + dt vx (the
+# multiplications by the model's 0 / 1 entries are exact).
+
+def occupied(m, occ, p):
+    idx = [math.floor((p[a] - m["origin"][a]) / m["res"]) for a in range(3)]
+    d = m["dims"]
+    if not all(0 <= idx[a] < d[a] for a in range(3)):
+        return True
+    return occ[(idx[0] * d[1] + idx[1]) * d[2] + idx[2]] != 0
+
+
+def _stop_sizes(tp, vel, size):
+    v = math.sqrt(vel[0] * vel[0] + vel[1] * vel[1])
+    s = list(size)
+    out = []
+    for _ in range(tp["num_pred"] + 1):
+        out.append(list(s))
+        g = 2 * min(v, tp["stop_vel"]) * tp["dt"]
+        s[0] += g
+        s[1] += g
+    return out
+
+
+def model_forward(tp, m, occ, pos, vel):
+    """:351-396 -- for each angle, velocities ascend until the first colliding sample."""
+    dt, P = tp["dt"], tp["num_pred"]
+    v = math.sqrt(vel[0] * vel[0] + vel[1] * vel[1])
+    a0 = math.atan2(vel[1], vel[0])
+    fa = tp["front_angle_deg"] * math.pi / 180
+    min_v, max_v = v - v, v + v
+    samples = []
+    i = a0 - fa
+    while i < a0 + fa:
+        j = min_v
+        while j < max_v:
+            st = [pos[0], pos[1], j * math.cos(i), j * math.sin(i)]
+            pts, valid = [list(pos)], True
+            for _ in range(P):
+                nxt = [st[0] + dt * st[2], st[1] + dt * st[3], st[2], st[3]]
+                p = [nxt[0], nxt[1], pos[2]]
+                if occupied(m, occ, p):
+                    valid = False
+                    break
+                pts.append(p)
+                st = nxt
+            if not valid:
+                break
+            samples.append(pts)
+            j += 0.1
+        i += 0.1
+    return samples
+
+
+def model_turning(tp, m, occ, intent, pos, vel):
+    """:398-472 -- (speed, angular rate, end angle) grid; colliding samples are dropped."""
+    dt, P = tp["dt"], tp["num_pred"]
+    v = math.sqrt(vel[0] * vel[0] + vel[1] * vel[1])
+    a0 = math.atan2(vel[1], vel[0])
+    fa = tp["front_angle_deg"] * math.pi / 180
+    if intent == LEFT:
+        e_min, e_max = fa + a0, (math.pi - fa) + a0
+        w_min, w_max = (math.pi / 2) / tp["max_turning_time"], (math.pi / 2) / tp["min_turning_time"]
+    else:
+        e_min, e_max = -(math.pi - fa) + a0, -fa + a0
+        w_min, w_max = (-math.pi / 2) / tp["min_turning_time"], (-math.pi / 2) / tp["max_turning_time"]
+    samples = []
+    i = v - v
+    while i < v + v:
+        j = w_min
+        while j < w_max:
+            e = e_min
+            while e < e_max:
+                ang = a0
+                st = [pos[0], pos[1], i * math.cos(ang), i * math.sin(ang)]
+                pts, valid = [list(pos)], True
+                for _ in range(P):
+                    nxt = [st[0] + dt * st[2], st[1] + dt * st[3], st[2], st[3]]
+                    p = [nxt[0], nxt[1], pos[2]]
+                    if occupied(m, occ, p):
+                        valid = False
+                        break
+                    pts.append(p)
+                    st = nxt
+                    ang += j * dt
+                    ang = (e if e < ang else ang) if intent == LEFT else (e if ang < e else ang)
+                    vv = math.sqrt(st[2] * st[2] + st[3] * st[3])
+                    st[2], st[3] = vv * math.cos(ang), vv * math.sin(ang)
+                if valid:
+                    samples.append(pts)
+                e += 0.2
+            j += 0.2
+        i += 0.2
+    return samples
+
+
+def gen_traj(tp, m, occ, samples, sizes):
+    """:501-566 genTraj + positionCorrection (all samples have num_pred + 1 points)."""
+    n = len(samples)
+    mean = []
+    for t in range(tp["num_pred"] + 1):
+        sx = sy = 0.0
+        for s in samples:
+            sx += s[t][0]
+            sy += s[t][1]
+        mx, my = sx / n, sy / n
+        vx = vy = 0.0
+        for s in samples:
+            vx += (s[t][0] - mx) * (s[t][0] - mx)
+            vy += (s[t][1] - my) * (s[t][1] - my)
+        mean.append([mx, my, samples[0][0][2]])
+        sizes[t][0] += 2 * math.sqrt(vx / n) * tp["z_score"]
+        sizes[t][1] += 2 * math.sqrt(vy / n) * tp["z_score"]
+    if any(occupied(m, occ, p) for p in mean):
+        min_sum, min_idx = math.inf, -1
+        for k, s in enumerate(samples):
+            sm = 0.0
+            for t in range(len(mean)):
+                dx, dy = s[t][0] - mean[t][0], s[t][1] - mean[t][1]
+                sm += math.sqrt(dx * dx + dy * dy)
+                if sm > min_sum:
+                    break
+            if sm < min_sum:
+                min_sum, min_idx = sm, k
+        mean = [list(p) for p in samples[min_idx]]
+    return mean, sizes
+
+
+def predict_traj(tp, m, occ, pos, vel, size):
+    """predTraj for one obstacle (:283-330): per intent (FORWARD, LEFT, RIGHT, STOP) the predicted
+    positions and sizes, num_pred + 1 each."""
+    v = math.sqrt(vel[0] * vel[0] + vel[1] * vel[1])
+    out_p, out_s = [], []
+    for intent in (FORWARD, LEFT, RIGHT, STOP):
+        if v <= tp["stop_vel"] or intent == STOP:
+            samples, sizes = [[list(pos)] * (tp["num_pred"] + 1)], _stop_sizes(tp, vel, size)
+        elif intent == FORWARD:
+            samples, sizes = model_forward(tp, m, occ, pos, vel), [list(size) for _ in range(tp["num_pred"] + 1)]
+        else:
+            samples, sizes = model_turning(tp, m, occ, intent, pos, vel), [list(size) for _ in range(tp["num_pred"] + 1)]
+        if samples:
+            mean, sizes = gen_traj(tp, m, occ, samples, sizes)
+        else:  # every sample collided (:312-326)
+            mean, sizes = [list(pos)] * (tp["num_pred"] + 1), _stop_sizes(tp, vel, size)
+        out_p.append(mean)
+        out_s.append(sizes)
+    return out_p, out_s

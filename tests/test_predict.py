@@ -83,3 +83,69 @@ def test_device_intent_prob_matches_restatement(ctx):
         n = hl[o]
         ref = pr.intent_prob(P, ph[o, :n].tolist(), vh[o, :n].tolist())
         np.testing.assert_allclose(out[o], ref, rtol=1e-13, atol=1e-15)
+
+
+# ---------------------------------------------------------------- predTraj
+TP = dict(num_pred=33, dt=0.1, stop_vel=0.1, front_angle_deg=10.0, min_turning_time=2.0, max_turning_time=3.0,
+          z_score=0.674)  # predictor_param.yaml
+
+
+def world(rng=None):
+    """A 20 x 20 x 5 m map at 0.1 m with a few inflated walls / pillars."""
+    m = dict(origin=[-10.0, -10.0, 0.0], res=0.1, dims=[200, 200, 50])
+    occ = np.zeros((200, 200, 50), np.uint8)
+    occ[120:124, 40:160, :] = 1      # wall at x = 2.0 .. 2.4
+    occ[60:160, 150:154, :] = 1      # wall at y = 5.0 .. 5.4
+    occ[80:86, 80:86, :] = 1         # pillar around (-2, -2)
+    return m, occ
+
+
+def test_traj_stop_and_slow_obstacles_are_stationary():
+    m, occ = world()
+    pp, ps = pr.predict_traj(TP, m, occ.reshape(-1), [0.0, 0.0, 1.0], [0.05, 0.0, 0.0], [0.5, 0.5, 1.0])
+    for it in range(4):
+        assert all(p == [0.0, 0.0, 1.0] for p in pp[it])
+        assert ps[it][1][0] == 0.5 + 2 * 0.05 * 0.1 and ps[it][-1][2] == 1.0
+
+
+def test_traj_forward_is_straight_and_wall_stops_faster_samples():
+    m, occ = world()
+    pp, ps = pr.predict_traj(TP, m, occ.reshape(-1), [-5.0, -5.0, 1.0], [1.0, 0.0, 0.0], [0.5, 0.5, 1.0])
+    fwd = pp[pr.FORWARD]
+    assert fwd[-1][0] > -5.0 and abs(fwd[-1][1] - (-5.0)) < 0.5       # heads +x, spread +-10 deg
+    assert ps[pr.FORWARD][-1][1] > 0.5                                  # lateral spread -> wider
+    # toward the wall at x = 2: samples that would cross it are cut, the mean stays in front of it
+    pp2, _ = pr.predict_traj(TP, m, occ.reshape(-1), [0.5, 0.0, 1.0], [2.0, 0.0, 0.0], [0.5, 0.5, 1.0])
+    assert max(p[0] for p in pp2[pr.FORWARD]) < 2.0
+
+
+def test_traj_left_turns_left():
+    m, occ = world()
+    pp, _ = pr.predict_traj(TP, m, occ.reshape(-1), [-5.0, -5.0, 1.0], [1.0, 0.0, 0.0], [0.5, 0.5, 1.0])
+    assert pp[pr.LEFT][-1][1] > pp[pr.RIGHT][-1][1]
+
+
+@pytest.mark.gpu
+def test_device_predict_traj_matches_restatement(ctx):
+    import impc
+    m, occ = world()
+    tp = impc.TrajParams(num_pred=TP["num_pred"], dt=TP["dt"], stop_velocity=TP["stop_vel"],
+                         front_angle_deg=TP["front_angle_deg"], min_turning_time=TP["min_turning_time"],
+                         max_turning_time=TP["max_turning_time"], z_score=TP["z_score"])
+    om = impc.OccMap()
+    om.origin[:] = m["origin"]
+    om.resolution = m["res"]
+    om.dims[:] = m["dims"]
+    rng = np.random.default_rng(12)
+    count = 24
+    pos = np.stack([rng.uniform(-6, 4, count), rng.uniform(-6, 6, count), np.full(count, 1.0)], axis=1)
+    hd = rng.uniform(-math.pi, math.pi, count)
+    sp = rng.choice([0.05, 0.5, 1.0, 1.8], count)
+    vel = np.stack([sp * np.cos(hd), sp * np.sin(hd), np.zeros(count)], axis=1)
+    size = np.tile([0.5, 0.5, 1.0], (count, 1))
+    pp, ps = impc.predict_traj(ctx, tp, om, occ.reshape(-1), pos, vel, size)
+    flat = occ.reshape(-1)
+    for o in range(count):
+        rp, rs = pr.predict_traj(TP, m, flat, pos[o].tolist(), vel[o].tolist(), size[o].tolist())
+        np.testing.assert_allclose(pp[o], np.asarray(rp), rtol=1e-12, atol=1e-12, err_msg=f"obstacle {o}")
+        np.testing.assert_allclose(ps[o], np.asarray(rs), rtol=1e-12, atol=1e-12, err_msg=f"obstacle {o}")
