@@ -185,3 +185,13 @@ def test_per_qp_latency_recorded_by_structured_kernel(ctx):
             b.qp_latency()
     finally:
         b.close()
+
+
+@KERNELS
+@pytest.mark.parametrize("K", [19, 20])
+def test_many_obstacles_three_general_row_slots(ctx, kernel, K):
+    """Config 4's largest buckets: K = 19, 20 obstacles push the general rows past 512 (the
+    structured kernel's three-slot shape, and its larger products region)."""
+    cfg = scenarios.static_config(N=20, K=K, batch=16, identical=False, seed=950 + K)
+    s = impc.default_settings(**S25)
+    compare(gpu(ctx, cfg, s, kernel), oracle(cfg, s))
