@@ -137,11 +137,12 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
 
     # results + parity-relevant statistics (outside the timed region)
-    iters_all, status_all, recs = [], [], []
+    iters_all, status_all, rho_all, recs = [], [], [], []
     for K, bk, b in batches:
         x, y, info = b.get()
         iters_all.append(info["iter"])
         status_all.append(info["status_val"])
+        rho_all.append(info["rho_updates"])
         recs.append(D.make_records(rank, bk["inst"], bk["hyp"], info))
     iters_all = np.concatenate(iters_all)
     status_all = np.concatenate(status_all)
@@ -211,7 +212,8 @@ def main():
                                      if values_mode == "shared" else " (every QP's full CSC values)"),
         },
         "qp_latency_ms": qp_lat,
-        "iters": {"mean": mean_iter, "p50": float(np.median(iters_all)), "max": int(iters_all.max())},
+        "iters": {"mean": mean_iter, "p50": float(np.median(iters_all)), "max": int(iters_all.max()),
+                  "rho_updates_mean": float(np.concatenate(rho_all).mean())},
         "status_counts": {str(int(k)): int(v) for k, v in zip(*np.unique(status_all, return_counts=True))},
         "kernel_ms": {"setup": setup_ms, "solve": solve_ms,
                       "outputs": sum(kt[K][2] for K in kt)},
