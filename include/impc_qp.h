@@ -180,7 +180,8 @@ int impc_batch_update_bounds(impc_batch b, const double *l, const double *u);
 
 /* Kernel selection.  AUTO picks the one-QP-per-wavefront structured kernel when the pattern is
  * the stage-structured mpcPlanner QP and fits its register layout, else the
- * generic one-QP-per-lane kernel.  The persistent update calls need the GENERIC kernel. */
+ * generic one-QP-per-lane kernel.  The persistent update calls work on both (structured: after
+ * impc_batch_set_persistent). */
 #define IMPC_KERNEL_AUTO 0
 #define IMPC_KERNEL_GENERIC 1
 #define IMPC_KERNEL_STRUCTURED 2
@@ -211,6 +212,16 @@ int impc_batch_get_stats(impc_batch b, impc_batch_stats *out);
 int impc_batch_set_profiling(impc_batch b, int on);
 /* Durations (ms) of the last profiled setup / solve-kernel / output-transpose launches. */
 int impc_batch_get_timings(impc_batch b, double *setup_ms, double *solve_ms, double *output_ms);
+
+/* Persistent workspace (structured kernel; OSQP's workspace kept between osqp_solve calls, as a
+ * persistent OsqpEigen::Solver does -- polyTrajSolver.cpp:183-237).  With it on, each solve keeps
+ * the QPs' scaling, rho and scaled iterates on the device; impc_batch_update_lin_cost /
+ * impc_batch_update_bounds (osqp_update_lin_cost / osqp_update_bounds semantics) then apply to
+ * the next solve, which continues from the stored iterates (an explicit impc_batch_warm_start is
+ * applied once instead).  New values (impc_batch_set_values*) start over with a full setup.
+ * Costs 8 (24 + 3 n + 2 m_general) bytes per QP of device memory and that much HBM traffic per
+ * solve.  Off by default. */
+int impc_batch_set_persistent(impc_batch b, int on);
 
 /* Per-QP solve latency (ms) of the last profiled structured-kernel solve: from the moment a
  * workgroup takes the QP off the work queue to its results being written (device wall clock,

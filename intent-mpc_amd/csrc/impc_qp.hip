@@ -410,6 +410,9 @@ struct impc_batch_s {
     int64_t device_bytes = 0;
     bool values_set = false, has_ws = false;
     unsigned long long *d_qpt = nullptr;  // profiling: per-QP (start, end) device clock
+    // persistent workspace of the structured kernel (impc_batch_set_persistent)
+    double *d_persist = nullptr;
+    bool persist_on = false, persist_valid = false, q_by_update = false;
     bool qpt_valid = false;
     // shared-structure values (impc_batch_set_values_shared)
     bool shared = false, shared_expanded = false;
@@ -506,6 +509,11 @@ impc::WaveIO wave_io(impc_batch b) {
                     b->in_l,     b->in_u,   b->in_xws, b->in_yws, b->has_ws ? 1 : 0, b->d_xout, b->d_yout,
                     b->d_scal,   b->d_info};
     if (b->profile && b->d_qpt) io.qpt = b->d_qpt;
+    if (b->persist_on && b->d_persist) {
+        io.persist = b->d_persist;
+        io.resume = b->persist_valid ? 1 : 0;
+        io.q_updated = b->q_by_update ? 1 : 0;
+    }
     b->qpt_valid = io.qpt != nullptr;
     if (b->shared) {
         io.shared = 1;
@@ -703,6 +711,14 @@ int launch_wave(impc_batch b, hipStream_t st, const impc::WaveIO &io) {
     return b->ms->W == WS ? launch_wave_w<VS, GS, WS>(b, st, io) : launch_wave_w<VS, GS, 0>(b, st, io);
 }
 
+// After a structured solve of a persistent batch: its workspace holds the scaled iterates, and an
+// explicit warm start has been consumed (OSQP applies osqp_warm_start once).
+void structured_solved(impc_batch b) {
+    if (!b->persist_on) return;
+    b->persist_valid = true;
+    b->has_ws = false;
+}
+
 int structured_solve(impc_batch b, hipStream_t st) {
     impc::WaveIO io = wave_io(b);
     HIP_OK(hipMemsetAsync(b->d_counter, 0, 256, st));
@@ -725,6 +741,7 @@ int structured_solve(impc_batch b, hipStream_t st) {
         default: return fail(IMPC_UNSUPPORTED, "no structured kernel for this size");
     }
     if (rc) return rc;
+    structured_solved(b);
     if (b->profile) {
         HIP_OK(hipEventRecord(b->ev[3], st));
         HIP_OK(hipEventRecord(b->ev[4], st));
@@ -960,7 +977,7 @@ int impc_batch_destroy(impc_batch b) {
         if (e) (void)hipEventDestroy(e);
     void *ptrs[] = {b->d_in,     b->d_xout,  b->d_yout,  b->d_info,  b->d_tables, b->d_scal, b->d_counter,
                     b->d_sym,    b->d_work,  b->d_sec,   b->d_shPx,  b->d_shAx,   b->d_Axv,  b->d_vmap,
-                    b->d_qpt};
+                    b->d_qpt,    b->d_persist};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete b;
@@ -1011,6 +1028,7 @@ int impc_batch_set_values(impc_batch b, const double *Px, const double *q, const
         IMPC_TRY(h2d_sync(b->ctx->stream, b->in_u, u, sizeof(double) * b->m * B));
     }
     b->shared = false;
+    b->persist_valid = b->q_by_update = false;  // new data: the next solve sets up from scratch
     b->values_set = true;
     b->generic_dirty = true;
     return IMPC_OK;
@@ -1063,6 +1081,7 @@ int impc_batch_set_values_shared(impc_batch b, const double *Px, const double *A
     b->nvar = nvar;
     b->shared = true;
     b->shared_expanded = false;
+    b->persist_valid = b->q_by_update = false;
     b->values_set = true;
     b->generic_dirty = true;
     return IMPC_OK;
@@ -1084,6 +1103,7 @@ int impc_batch_set_values_device(impc_batch b, const double *Px, const double *q
         HIP_OK(hipMemcpyAsync(b->in_u, u, sizeof(double) * b->m * B, hipMemcpyDeviceToDevice, st));
     }
     b->shared = false;
+    b->persist_valid = b->q_by_update = false;  // new data: the next solve sets up from scratch
     b->values_set = true;
     b->generic_dirty = true;
     return IMPC_OK;
@@ -1191,6 +1211,7 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
         default: return fail(IMPC_UNSUPPORTED, "no structured kernel for this size");
     }
     if (rc) return rc;
+    for (int k = 0; k < count; k++) structured_solved(bs[k]);
     if (b0->profile) {
         HIP_OK(hipEventRecord(b0->ev[3], st));
         HIP_OK(hipEventRecord(b0->ev[4], st));
@@ -1228,8 +1249,16 @@ static int upload_interleaved(impc_batch b, const double *host, double *qp_major
 
 int impc_batch_update_lin_cost(impc_batch b, const double *q) {
     if (!b || !q) return fail(IMPC_INVALID_ARGUMENT, "null batch or q");
-    if (use_structured(b))
-        return fail(IMPC_UNSUPPORTED, "persistent updates need impc_batch_set_kernel(b, IMPC_KERNEL_GENERIC)");
+    if (use_structured(b)) {  // the next structured solve resumes the workspace with this q
+        if (!b->persist_on || !b->persist_valid)
+            return fail(IMPC_WORKSPACE_NOT_INIT_ERROR,
+                        "structured kernel: impc_batch_set_persistent(b, 1) and one solve before updates");
+        HIP_OK(hipSetDevice(b->ctx->device));
+        IMPC_TRY(h2d_sync(b->ctx->stream, b->in_q, q, sizeof(double) * b->n * b->B));
+        b->q_by_update = true;
+        b->generic_dirty = true;
+        return IMPC_OK;
+    }
     if (!b->generic_setup_done || b->generic_dirty)
         return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "setup has not run on current data");
     int rc = upload_interleaved(b, q, b->in_q, const_cast<double *>(b->dwk.q), b->n);
@@ -1242,8 +1271,20 @@ int impc_batch_update_lin_cost(impc_batch b, const double *q) {
 
 int impc_batch_update_bounds(impc_batch b, const double *l, const double *u) {
     if (!b || (b->m && (!l || !u))) return fail(IMPC_INVALID_ARGUMENT, "null batch or bounds");
-    if (use_structured(b))
-        return fail(IMPC_UNSUPPORTED, "persistent updates need impc_batch_set_kernel(b, IMPC_KERNEL_GENERIC)");
+    if (use_structured(b)) {  // the next structured solve resumes the workspace with these bounds
+        if (!b->persist_on || !b->persist_valid)
+            return fail(IMPC_WORKSPACE_NOT_INIT_ERROR,
+                        "structured kernel: impc_batch_set_persistent(b, 1) and one solve before updates");
+        for (int64_t k = 0; k < b->m * b->B; k++)
+            if (l[k] > u[k]) return fail(IMPC_DATA_VALIDATION_ERROR, "lower bound greater than upper bound");
+        HIP_OK(hipSetDevice(b->ctx->device));
+        if (b->m) {
+            IMPC_TRY(h2d_sync(b->ctx->stream, b->in_l, l, sizeof(double) * b->m * b->B));
+            IMPC_TRY(h2d_sync(b->ctx->stream, b->in_u, u, sizeof(double) * b->m * b->B));
+        }
+        b->generic_dirty = true;
+        return IMPC_OK;
+    }
     if (!b->generic_setup_done || b->generic_dirty)
         return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "setup has not run on current data");
     for (int64_t k = 0; k < b->m * b->B; k++)
@@ -1285,6 +1326,25 @@ int impc_batch_set_profiling(impc_batch b, int on) {
         for (hipEvent_t &e : b->ev) HIP_OK(hipEventCreate(&e));
     if (on && !b->d_qpt) HIP_OK(hipMalloc((void **)&b->d_qpt, sizeof(unsigned long long) * 2 * (size_t)b->B));
     b->profile = on != 0;
+    return IMPC_OK;
+}
+
+int impc_batch_set_persistent(impc_batch b, int on) {
+    if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
+    if (on && !b->structured_ok) return fail(IMPC_UNSUPPORTED, "persistent workspaces are a structured-kernel mode");
+    if (on && b->settings.scaling > impc::kPersistMaxScaling)
+        return fail(IMPC_UNSUPPORTED, "persistent workspaces support scaling <= 20 Ruiz passes");
+    HIP_OK(hipSetDevice(b->ctx->device));
+    if (on && !b->d_persist) {
+        const size_t bytes = sizeof(double) * (size_t)b->B * (size_t)impc::persist_stride((int)b->n, b->ms->mg);
+        if (hipMalloc((void **)&b->d_persist, bytes) != hipSuccess) {
+            b->d_persist = nullptr;
+            return fail(IMPC_MEM_ALLOC_ERROR, "hipMalloc(persistent workspace) failed");
+        }
+        b->device_bytes += (int64_t)bytes;
+    }
+    b->persist_on = on != 0;
+    b->persist_valid = b->q_by_update = false;  // the next solve sets up from scratch
     return IMPC_OK;
 }
 

@@ -76,7 +76,18 @@ struct WaveIO {
     int64_t nvar = 0;
     const int32_t *vmap = nullptr;
     const double *Ax_var = nullptr;
+    // persistent workspace (impc_batch_set_persistent, OSQP's workspace between solves): per QP
+    // [kPersistHdr + 3 n + 2 mg]: cost-scaling factors of the Ruiz passes, rho, then the scaled
+    // iterates x, z (box), y (box), z (general), y (general).  resume = 1: scale with the stored
+    // factors (the same D, E, c and scaled P, A as the first setup), start from the stored rho and
+    // iterates, and -- when q_updated -- scale q as osqp_update_lin_cost does ((D q) c).
+    double *persist = nullptr;
+    int32_t resume = 0, q_updated = 0;
 };
+
+constexpr int kPersistHdr = 24;      // ct[0 .. kPersistMaxScaling), rho at kPersistHdr - 1
+constexpr int kPersistMaxScaling = 20;
+IMPC_HD int64_t persist_stride(int n, int mg) { return kPersistHdr + 3 * (int64_t)n + 2 * (int64_t)mg; }
 
 // Section profiling (profiling build of the library only, -DIMPC_SECTION_PROF): lane 0 of each
 // team accumulates s_memtime deltas per section; IMPC_SEC(X) closes section X.
@@ -386,7 +397,9 @@ struct WaveQP {
 
     // scale_data (scaling.h:21): Ruiz equilibration + cost scaling; D, E kept in registers here,
     // written to the per-QP scratch at the end.
-    IMPC_WF void scale(int64_t b, double D[VS], double Eb[VS], double Eg[GS]) {
+    // ps: the QP's persistent record (or null): the Ruiz passes' cost factors are stored there,
+    // or replayed from it when resuming
+    IMPC_WF void scale(int64_t b, double D[VS], double Eb[VS], double Eg[GS], double *ps) {
         const int n = T.n;
         _Pragma("unroll") for (int s = 0; s < VS; s++) D[s] = Eb[s] = 1.0;
         _Pragma("unroll") for (int s = 0; s < GS; s++) Eg[s] = 1.0;
@@ -452,6 +465,12 @@ struct WaveQP {
             ct = ct < kMinScaling ? 1.0 : ct;
             ct = ct > kMaxScaling ? kMaxScaling : ct;
             ct = 1. / ct;
+            if (ps) {
+                if (io.resume)
+                    ct = ps[it];
+                else if (L == 0)
+                    ps[it] = ct;
+            }
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
                 pd[s] *= ct;
                 q[s] *= ct;
@@ -1340,11 +1359,15 @@ struct WaveQP {
         IMPC_SEC_START();
         clear_exchange();
         load(b);
+        double *ps = io.persist ? io.persist + b * persist_stride(T.n, T.mg) : nullptr;
         {
             double D[VS], Eb[VS], Eg[GS];
-            scale(b, D, Eb, Eg);
+            scale(b, D, Eb, Eg, ps);
+            if (ps && io.resume && io.q_updated)  // osqp_update_lin_cost: q = c (D q)
+                _Pragma("unroll") for (int s = 0; s < VS; s++)
+                    if (vok[s]) q[s] = (D[s] * io.q[b * n + T.var_orig[NL * s + L]]) * c;
         }
-        set_rho(dmin(dmax(st.rho, kRhoMin), kRhoMax));
+        set_rho(ps && io.resume ? ps[kPersistHdr - 1] : dmin(dmax(st.rho, kRhoMin), kRhoMax));
         IMPC_SEC(kSecSetup);
         int bad = 0;
         IMPC_REP(kSecFactor) bad = factorize();  // (phase-cost experiments only)
@@ -1370,7 +1393,22 @@ struct WaveQP {
             return;
         }
         // iterates: zero, then osqp_warm_start (x <- Dinv x, y <- c Einv y, z <- A x)
-        if (io.has_ws) {
+        if (ps && io.resume && !io.has_ws) {  // OSQP keeps its iterates between solves
+            const double *it = ps + kPersistHdr;
+            _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                if (!vok[s]) continue;
+                const int v = NL * s + L;
+                x[s] = it[v];
+                zb[s] = it[n + v];
+                yb[s] = it[2 * n + v];
+            }
+            _Pragma("unroll") for (int s = 0; s < GS; s++) {
+                if (!gok[s]) continue;
+                const int g = NL * s + L;
+                z[s] = it[3 * n + g];
+                y[s] = it[3 * n + T.mg + g];
+            }
+        } else if (io.has_ws) {
             double D[VS], Eb[VS], Eg[GS];
             load_scal(b, D, Eb, Eg);
             double *xb = xbuf();
@@ -1490,6 +1528,23 @@ struct WaveQP {
         const bool has_sol2 = status != IMPC_PRIMAL_INFEASIBLE && status != IMPC_PRIMAL_INFEASIBLE_INACCURATE &&
                               status != IMPC_DUAL_INFEASIBLE && status != IMPC_DUAL_INFEASIBLE_INACCURATE &&
                               status != IMPC_NON_CVX;
+        if (ps) {  // the workspace after osqp_solve: rho and the scaled iterates
+            double *it = ps + kPersistHdr;
+            if (L == 0) ps[kPersistHdr - 1] = R.rho;
+            _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                if (!vok[s]) continue;
+                const int v = NL * s + L;
+                it[v] = x[s];
+                it[n + v] = zb[s];
+                it[2 * n + v] = yb[s];
+            }
+            _Pragma("unroll") for (int s = 0; s < GS; s++) {
+                if (!gok[s]) continue;
+                const int g = NL * s + L;
+                it[3 * n + g] = z[s];
+                it[3 * n + T.mg + g] = y[s];
+            }
+        }
         const bool scaled = st.scaling > 0;
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (!vok[s]) continue;

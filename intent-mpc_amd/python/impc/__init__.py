@@ -114,6 +114,7 @@ _sig("impc_batch_get_perm", C.c_int, _P, _i64p)
 _sig("impc_batch_set_profiling", C.c_int, _P, C.c_int)
 _sig("impc_batch_get_timings", C.c_int, _P, _dp, _dp, _dp)
 _sig("impc_batch_get_qp_latency", C.c_int, _P, _dp)
+_sig("impc_batch_set_persistent", C.c_int, _P, C.c_int)
 _sig("impc_batch_set_kernel", C.c_int, _P, C.c_int)
 _sig("impc_batch_solve_group", C.c_int, C.POINTER(_P), C.c_int, _P)
 _sig("impc_device_alloc", C.c_int, _P, C.c_int64, C.POINTER(_P))
@@ -181,7 +182,7 @@ EXPORTED = [
     "impc_batch_set_values", "impc_batch_set_values_device", "impc_batch_set_values_shared", "impc_batch_warm_start", "impc_batch_setup",
     "impc_batch_solve", "impc_batch_get", "impc_batch_device_results", "impc_batch_update_lin_cost",
     "impc_batch_update_bounds", "impc_batch_get_stats", "impc_batch_get_perm", "impc_batch_set_profiling",
-    "impc_batch_get_timings", "impc_batch_get_qp_latency", "impc_batch_set_kernel", "impc_batch_solve_group", "impc_device_alloc", "impc_device_free",
+    "impc_batch_get_timings", "impc_batch_get_qp_latency", "impc_batch_set_persistent", "impc_batch_set_kernel", "impc_batch_solve_group", "impc_device_alloc", "impc_device_free",
     "impc_copy_to_device", "impc_copy_to_host", "impc_select_best", "impc_select_best_device", "impc_mpc_dims",
     "impc_mpc_build_pattern", "impc_mpc_build_values", "impc_mpc_warm_start", "impc_mpc_builder_create",
     "impc_mpc_builder_destroy", "impc_mpc_build_values_device", "impc_intent_fanout", "impc_intent_fanout_device",
@@ -298,6 +299,9 @@ class Batch:
         info = np.empty(self.B, dtype=INFO_DTYPE)
         _check(lib.impc_batch_get(self.h, _d(x), _d(y), info.ctypes.data_as(C.c_void_p)), "impc_batch_get")
         return x.reshape(self.B, self.n), y[: self.B * self.m].reshape(self.B, self.m), info
+
+    def set_persistent(self, on=True):
+        _check(lib.impc_batch_set_persistent(self.h, int(on)), "impc_batch_set_persistent")
 
     def qp_latency(self):
         """Per-QP device solve latency (ms) of the last profiled structured solve."""

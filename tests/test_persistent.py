@@ -1,0 +1,78 @@
+"""Persistent workspaces (osqp_update_lin_cost / osqp_update_bounds between solves, as a persistent
+OsqpEigen::Solver does, polyTrajSolver.cpp:183-237): both kernels against the oracle's persistent
+workspace (oracle/osqp_oracle.c ora_update_*, osqp.h:114,125) over a sequence setup+solve ->
+update q -> solve -> update bounds -> solve.  Identical statuses and iteration counts, primal
+within 1e-5 relative at every step."""
+import numpy as np
+import pytest
+
+import impc
+from impc import scenarios
+from oracle import osqp_oracle as ora
+
+pytestmark = pytest.mark.gpu
+
+KERNELS = pytest.mark.parametrize("kernel", [impc.KERNEL_GENERIC, impc.KERNEL_STRUCTURED],
+                                  ids=["generic", "structured"])
+
+
+def check(x, info, ref, rtol=1e-5):
+    xr, _, ir = ref
+    assert info["status_val"] == ir["status_val"] and info["iter"] == ir["iter"], (info, ir)
+    if ir["status_val"] in (1, 2):
+        assert np.abs(x - xr).max() <= rtol * max(np.abs(xr).max(), 1e-12)
+
+
+@KERNELS
+def test_update_sequence_matches_persistent_oracle(ctx, kernel):
+    cfg = scenarios.static_config(N=20, K=4, batch=12, identical=False, seed=515)
+    pat, v = cfg["pattern"], cfg["values"]
+    B = v["q"].shape[0]
+    s = impc.default_settings(verbose=0, adaptive_rho_interval=25)
+    rng = np.random.default_rng(9)
+    q2 = v["q"] * (1 + 0.05 * rng.standard_normal(v["q"].shape))
+    # bounds update: shift the finite box bounds of the states a little
+    l3, u3 = v["l"].copy(), v["u"].copy()
+    fin = np.isfinite(l3) & np.isfinite(u3) & (u3 - l3 > 1e-3)
+    l3[fin] -= 0.05
+    u3[fin] += 0.05
+    b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], B)
+    try:
+        b.set_kernel(kernel)
+        b.set_settings(s)
+        b.set_values(v["Px"], v["q"], v["Ax"], v["l"], v["u"])
+        if kernel == impc.KERNEL_STRUCTURED:
+            b.set_persistent(True)
+        b.solve()
+        r1 = b.get()
+        b.update_lin_cost(q2)
+        b.solve()
+        r2 = b.get()
+        b.update_bounds(l3, u3)
+        b.solve()
+        r3 = b.get()
+    finally:
+        b.close()
+    os_ = ora.settings_from(s)
+    for i in range(B):
+        w = ora.Workspace(pat, v["Px"][i], v["q"][i], v["Ax"][i], v["l"][i], v["u"][i], os_)
+        check(r1[0][i], r1[2][i], w.solve())
+        w.update_lin_cost(q2[i])
+        check(r2[0][i], r2[2][i], w.solve())
+        w.update_bounds(l3[i], u3[i])
+        check(r3[0][i], r3[2][i], w.solve())
+        w.close()
+
+
+def test_structured_updates_need_persistence(ctx):
+    cfg = scenarios.static_config(N=20, K=2, batch=4, identical=False, seed=516)
+    pat, v = cfg["pattern"], cfg["values"]
+    b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], 4)
+    try:
+        b.set_kernel(impc.KERNEL_STRUCTURED)
+        b.set_values(v["Px"], v["q"], v["Ax"], v["l"], v["u"])
+        b.solve()
+        with pytest.raises(impc.ImpcError):
+            b.update_lin_cost(v["q"])
+    finally:
+        b.close()
