@@ -22,8 +22,11 @@
  * reference's call pattern: Data copies vectors when they are set (OsqpEigen keeps the caller's
  * pointer until initSolver); osqp_setup's numeric work runs on the device at the first solve, so
  * a non-convex P surfaces as ErrorExitFlag::NonCvxError from solveProblem instead of a failed
- * initSolver; the update* calls on a stage-structured pattern re-run setup on the device and
- * warm-start from the last solution (the generic kernel keeps OSQP's factor reuse).
+ * initSolver; the update* calls keep OSQP's workspace semantics on both kernels (scaling, rho,
+ * factor and iterates carried over: the structured kernel through a persistent workspace,
+ * impc_batch_set_persistent, the generic kernel in place).  An update before the first solve,
+ * or on a structured batch whose settings exceed the persistent workspace's 20 Ruiz passes,
+ * re-runs setup from the new data instead, warm-started from the last solution.
  *
  * Requires Eigen's <Eigen/Dense> and <Eigen/Sparse> (the reference's own dependency) and
  * linking against intent-mpc_amd/lib/libimpc_qp.so.
@@ -221,6 +224,8 @@ class Solver {
     impc_info m_info{};
     Eigen::Matrix<double, Eigen::Dynamic, 1> m_x, m_y;
 
+    bool m_persistent = false;  // structured batch with a persistent workspace
+
     bool structured() const {
         impc_batch_stats st{};
         return m_batch && impc_batch_get_stats(m_batch, &st) == IMPC_OK && st.kernel == IMPC_KERNEL_STRUCTURED;
@@ -268,6 +273,9 @@ public:
             m_batch = nullptr;
             return false;
         }
+        // updateGradient / updateBounds between solves keep the solver state, as osqp_update_*
+        // does; scaling > 20 passes is refused (IMPC_UNSUPPORTED) and falls back to re-setup
+        m_persistent = structured() && impc_batch_set_persistent(m_batch, 1) == IMPC_OK;
         m_x.setZero(d.numberOfVariables());
         m_y.setZero(d.numberOfConstraints());
         m_solved = false;
@@ -278,10 +286,16 @@ public:
         if (m_batch) impc_batch_destroy(m_batch);
         m_batch = nullptr;
         m_solved = false;
+        m_persistent = false;
     }
 
     bool clearSolverVariables() {
         if (!m_batch) return false;
+        // osqp cold start: zero iterates (a persistent workspace would otherwise resume from its own)
+        if (m_persistent) {
+            std::vector<double> x((size_t)m_data->numberOfVariables(), 0.0), y((size_t)m_data->numberOfConstraints(), 0.0);
+            return impc_batch_warm_start(m_batch, x.data(), y.data()) == IMPC_OK;
+        }
         return impc_batch_warm_start(m_batch, nullptr, nullptr) == IMPC_OK;
     }
 
@@ -338,7 +352,7 @@ public:
     bool updateGradient(const V &gradient) {
         if (!m_batch) return false;
         if (!detail::copy_vec(gradient, m_data->numberOfVariables(), m_data->q)) return false;
-        if (structured()) return resetup_from_data();
+        if (structured() && !(m_persistent && m_solved)) return resetup_from_data();
         return impc_batch_update_lin_cost(m_batch, m_data->q.data()) == IMPC_OK;
     }
     template <typename L, typename U>
@@ -346,7 +360,7 @@ public:
         if (!m_batch) return false;
         const int64_t m = m_data->numberOfConstraints();
         if (!detail::copy_vec(lowerBound, m, m_data->l) || !detail::copy_vec(upperBound, m, m_data->u)) return false;
-        if (structured()) return resetup_from_data();
+        if (structured() && !(m_persistent && m_solved)) return resetup_from_data();
         return impc_batch_update_bounds(m_batch, m_data->l.data(), m_data->u.data()) == IMPC_OK;
     }
     template <typename L>

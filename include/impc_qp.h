@@ -145,8 +145,10 @@ int impc_batch_set_values_shared(impc_batch b, const double *Px, const double *A
                                  const int64_t *var_pos, const double *Ax_var, const double *q, const double *l,
                                  const double *u);
 
-/* osqp_warm_start(x, y) for every QP (host, QP-major; y may be NULL = zero duals).
- * Pass x = NULL to clear a previous warm start (cold start). */
+/* osqp_warm_start(x, y) for every QP (host, QP-major; y may be NULL = zero duals).  As in OSQP
+ * it turns the warm_start setting on.  On a set-up workspace (generic kernel after a solve,
+ * structured kernel with a persistent workspace) it replaces the iterates and keeps scaling, rho
+ * and factor.  Pass x = NULL to clear a pending warm start (the next setup cold-starts). */
 int impc_batch_warm_start(impc_batch b, const double *x, const double *y);
 
 /* osqp_setup's numeric part on the device: Ruiz scaling, rho vector, KKT assembly and

@@ -155,6 +155,29 @@ IMPC_HD void refresh_v(const DevSym &sy, const DevWork &wk, int lane) {
         IMPC_AT(wk.v, i) = IMPC_AT(wk.rho, i) * IMPC_AT(wk.z, i) - IMPC_AT(wk.y, i);
 }
 
+// osqp_warm_start (osqp.h:157) into a set-up workspace: x <- Dinv x_ws, y <- c Einv y_ws,
+// z <- A x (scaled data); the caller refreshes v.
+IMPC_HD void apply_warm_start(const DevSym &sy, const DevWork &wk, const DevSettings &st, double c, int lane) {
+    const int64_t S = wk.S;
+    const int32_t n = sy.n, m = sy.m;
+    const bool scaled = st.scaling > 0;
+    for (int32_t j = 0; j < n; j++)
+        IMPC_AT(wk.x, j) = scaled ? IMPC_AT(wk.Dinv, j) * IMPC_AT(wk.xws, j) : IMPC_AT(wk.xws, j);
+    for (int32_t i = 0; i < m; i++) {
+        double yi = IMPC_AT(wk.yws, i);
+        if (scaled) {
+            yi = IMPC_AT(wk.Einv, i) * yi;
+            yi *= c;
+        }
+        IMPC_AT(wk.y, i) = yi;
+    }
+    for (int32_t i = 0; i < m; i++) {  // z = A x
+        double s = 0.0;
+        for (int32_t k = sy.Arp[i]; k < sy.Arp[i + 1]; k++) s += IMPC_AT(wk.As, sy.Arpos[k]) * IMPC_AT(wk.x, sy.Arcol[k]);
+        IMPC_AT(wk.z, i) = s;
+    }
+}
+
 // --------------------------------------------------------------------------- osqp_setup
 // validate (bounds), copy + clamp, scale_data (Ruiz, scaling.h:21), set_rho_vec, factor, and
 // the optional osqp_warm_start (osqp.h:157).  Returns the per-QP setup exitflag.
@@ -259,25 +282,7 @@ IMPC_HD int qp_setup(const DevSym &sy, const DevWork &wk, const DevSettings &st,
         IMPC_AT(wk.z, i) = 0.0;
         IMPC_AT(wk.y, i) = 0.0;
     }
-    if (has_ws) {
-        const bool scaled = st.scaling > 0;
-        for (int32_t j = 0; j < n; j++)
-            IMPC_AT(wk.x, j) = scaled ? IMPC_AT(wk.Dinv, j) * IMPC_AT(wk.xws, j) : IMPC_AT(wk.xws, j);
-        for (int32_t i = 0; i < m; i++) {
-            double yi = IMPC_AT(wk.yws, i);
-            if (scaled) {
-                yi = IMPC_AT(wk.Einv, i) * yi;
-                yi *= c;
-            }
-            IMPC_AT(wk.y, i) = yi;
-        }
-        for (int32_t i = 0; i < m; i++) {  // z = A x
-            double s = 0.0;
-            for (int32_t k = sy.Arp[i]; k < sy.Arp[i + 1]; k++)
-                s += IMPC_AT(wk.As, sy.Arpos[k]) * IMPC_AT(wk.x, sy.Arcol[k]);
-            IMPC_AT(wk.z, i) = s;
-        }
-    }
+    if (has_ws) apply_warm_start(sy, wk, st, c, lane);
     refresh_v(sy, wk, lane);
     return err;
 }

@@ -116,6 +116,16 @@ __global__ __launch_bounds__(kBlock) void k_solve(impc::DevSym sy, impc::DevWork
     impc::qp_solve(sy, wk, st, lane, lane, 0);
 }
 
+// osqp_warm_start (osqp.h:157) on a set-up workspace: scaling, rho and factor stay
+__global__ __launch_bounds__(kBlock) void k_warm_start(impc::DevSym sy, impc::DevWork wk, impc::DevSettings st,
+                                                        int64_t B) {
+    const int lane = blockIdx.x * kBlock + threadIdx.x;
+    if (lane >= B) return;
+    const int64_t S = wk.S;
+    impc::apply_warm_start(sy, wk, st, IMPC_AT(wk.scal, impc::SC_C), lane);
+    impc::refresh_v(sy, wk, lane);
+}
+
 // osqp_update_lin_cost (osqp.h:114): q <- c * D q
 __global__ __launch_bounds__(kBlock) void k_update_q(impc::DevSym sy, impc::DevWork wk, impc::DevSettings st,
                                                      int64_t B) {
@@ -999,8 +1009,12 @@ int impc_batch_set_settings(impc_batch b, const impc_settings *s) {
     impc::DevSettings d;
     int rc = to_dev_settings(s, &d);
     if (rc) return rc;
-    if (s->rho != b->settings.rho || s->sigma != b->settings.sigma || s->scaling != b->settings.scaling)
+    if (b->persist_on && s->scaling > impc::kPersistMaxScaling)
+        return fail(IMPC_UNSUPPORTED, "persistent workspaces support scaling <= 20 Ruiz passes");
+    if (s->rho != b->settings.rho || s->sigma != b->settings.sigma || s->scaling != b->settings.scaling) {
         b->generic_dirty = true;
+        b->persist_valid = b->q_by_update = false;  // a different setup: the next solve starts over
+    }
     b->settings = *s;
     b->dst = d;
     return IMPC_OK;
@@ -1124,6 +1138,20 @@ int impc_batch_warm_start(impc_batch b, const double *x, const double *y) {
             IMPC_TRY(h2d_sync(b->ctx->stream, b->in_yws, y, sizeof(double) * b->m * B));
         else
             IMPC_TRY(fill0_sync(b->ctx->stream, b->in_yws, sizeof(double) * b->m * B));
+    }
+    // osqp_warm_start turns the warm_start setting on (osqp.c, oracle ora_warm_start)
+    b->settings.warm_start = 1;
+    b->dst.warm_start = 1;
+    if (!use_structured(b) && b->generic_setup_done && !b->generic_dirty) {
+        // a set-up generic workspace takes the warm start in place, keeping scaling, rho and factor
+        hipStream_t st = b->ctx->stream;
+        int rc = interleave(b, b->in_xws, const_cast<double *>(b->dwk.xws), b->n, st);
+        if (!rc) rc = interleave(b, b->in_yws, const_cast<double *>(b->dwk.yws), b->m, st);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_warm_start, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk,
+                           b->dst, b->B);
+        HIP_OK(hipGetLastError());
+        return IMPC_OK;
     }
     b->has_ws = true;
     b->generic_dirty = true;

@@ -1393,7 +1393,7 @@ struct WaveQP {
             return;
         }
         // iterates: zero, then osqp_warm_start (x <- Dinv x, y <- c Einv y, z <- A x)
-        if (ps && io.resume && !io.has_ws) {  // OSQP keeps its iterates between solves
+        if (ps && io.resume && !io.has_ws && st.warm_start) {  // OSQP keeps its iterates between solves
             const double *it = ps + kPersistHdr;
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
                 if (!vok[s]) continue;

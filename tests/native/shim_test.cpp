@@ -1,12 +1,17 @@
 // TEST INFRASTRUCTURE ONLY -- drives include/OsqpEigen/OsqpEigen.h with the call sequence of
 // mpcPlanner::solveTraj (reference mpcPlanner.cpp:436-527), against the Eigen stand-in.
 //   shim_test cpu : conversion checks + graceful failure without a device (exit 0 = pass)
-//   shim_test gpu : OSQP demo QP through the shim on the GPU (x*, y*, status) (exit 0 = pass)
+//   shim_test gpu : OSQP demo QP through the shim on the GPU (x*, y*, status), then a
+//                   stage-structured mpcPlanner QP (impc_mpc_build_*) through the shim's
+//                   solve -> updateGradient -> solve -> updateBounds -> solve sequence against
+//                   a direct persistent batch of the C-ABI (exit 0 = pass)
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 
 #include <OsqpEigen/OsqpEigen.h>
+#include <impc_mpc.h>
+#include <vector>
 
 static int fails = 0;
 #define CHECK(c)                                                   \
@@ -16,6 +21,109 @@ static int fails = 0;
             fails++;                                               \
         }                                                          \
     } while (0)
+
+// One live-config mpcPlanner QP (N = 20, 2 dynamic obstacles ahead of the drone), through the
+// shim and through a direct persistent structured batch: the shim's update* calls must carry the
+// workspace over exactly as impc_batch_update_* on a persistent batch do (same iteration counts,
+// primal to 1e-9).
+static void structured_case() {
+    impc_mpc_params p{};
+    p.horizon = 20, p.num_half_space = 0, p.ts = 0.1, p.max_vel = 5.0, p.max_acc = 20.0;
+    p.y_range_min = -5.0, p.y_range_max = 5.0, p.z_range_min = 0.5, p.z_range_max = 4.5;
+    p.static_safety_dist = 0.8, p.dynamic_safety_dist = 1.5, p.static_slack = 0.01, p.dynamic_slack = 0.2;
+    p.position_weight = 1000.0, p.velocity_weight = 0.0, p.acceleration_weight = 10.0;
+    const int N = 20, K = 2, L = 20;
+    impc_qp_dims dm{};
+    CHECK(impc_mpc_dims(&p, 0, K, &dm) == IMPC_OK);
+    const int64_t n = dm.n, m = dm.m;
+    std::vector<int64_t> Pp(n + 1), Pi(dm.nnzP), Ap(n + 1), Ai(dm.nnzA);
+    CHECK(impc_mpc_build_pattern(&p, 0, K, Pp.data(), Pi.data(), Ap.data(), Ai.data()) == IMPC_OK);
+    double pos[3] = {0.0, 0.0, 1.2}, vel[3] = {1.0, 0.1, 0.0};
+    std::vector<double> xref((size_t)N * 8, 0.0), dpos((size_t)K * L * 3), dsize((size_t)K * L * 3, 0.6);
+    for (int j = 0; j < N; j++) {
+        xref[(size_t)j * 8 + 0] = 0.15 * j;
+        xref[(size_t)j * 8 + 2] = 1.2;
+        xref[(size_t)j * 8 + 3] = 1.5;
+    }
+    for (int k = 0; k < K; k++)
+        for (int j = 0; j < L; j++) {
+            double *d = &dpos[((size_t)k * L + j) * 3];
+            d[0] = 2.0 + 0.8 * k - 0.05 * j;
+            d[1] = (k ? -0.4 : 0.5) + 0.02 * j;
+            d[2] = 1.2;
+        }
+    std::vector<double> Px(dm.nnzP), q(n), Ax(dm.nnzA), l(m), u(m);
+    CHECK(impc_mpc_build_values(&p, 1, pos, vel, xref.data(), nullptr, 0, nullptr, nullptr, nullptr, K, L, dpos.data(),
+                                dsize.data(), Px.data(), q.data(), Ax.data(), l.data(), u.data()) == IMPC_OK);
+    Eigen::SparseMatrix<double> P((Eigen::Index)n, (Eigen::Index)n), A((Eigen::Index)m, (Eigen::Index)n);
+    for (int64_t j = 0; j < n; j++) {
+        for (int64_t k = Pp[j]; k < Pp[j + 1]; k++) P.insert(Pi[k], j) = Px[k];
+        for (int64_t k = Ap[j]; k < Ap[j + 1]; k++) A.insert(Ai[k], j) = Ax[k];
+    }
+    auto vec = [](const std::vector<double> &v) {
+        Eigen::VectorXd e((Eigen::Index)v.size());
+        for (size_t k = 0; k < v.size(); k++) e((Eigen::Index)k) = v[k];
+        return e;
+    };
+    // the update sequence: a shifted reference (q), then the y band narrowed (l / u)
+    std::vector<double> q2(q), l3(l), u3(u);
+    for (int64_t j = 0; j < n; j++) q2[j] = q[j] * 1.05 + (j % 8 == 1 ? 0.3 : 0.0);
+    for (int64_t i = 0; i < m; i++)
+        if (std::isfinite(l3[i]) && std::isfinite(u3[i]) && u3[i] - l3[i] > 0.1) l3[i] += 0.01, u3[i] -= 0.01;
+
+    OsqpEigen::Solver solver;
+    solver.settings()->setVerbosity(false);
+    solver.settings()->setWarmStart(true);
+    solver.data()->setNumberOfVariables((int)n);
+    solver.data()->setNumberOfConstraints((int)m);
+    CHECK(solver.data()->setHessianMatrix(P));
+    CHECK(solver.data()->setGradient(vec(q)));
+    CHECK(solver.data()->setLinearConstraintsMatrix(A));
+    CHECK(solver.data()->setLowerBound(vec(l)));
+    CHECK(solver.data()->setUpperBound(vec(u)));
+    CHECK(solver.initSolver());
+
+    impc_ctx ctx = nullptr;
+    impc_batch b = nullptr;
+    CHECK(impc_ctx_create(0, &ctx) == IMPC_OK);
+    CHECK(impc_batch_create(ctx, n, m, Pp.data(), Pi.data(), Ap.data(), Ai.data(), 1, &b) == IMPC_OK);
+    impc_settings st;
+    impc_default_settings(&st);
+    st.verbose = 0;
+    st.warm_start = 1;
+    impc_batch_stats bs{};
+    CHECK(impc_batch_get_stats(b, &bs) == IMPC_OK && bs.kernel == IMPC_KERNEL_STRUCTURED);
+    CHECK(impc_batch_set_settings(b, &st) == IMPC_OK);
+    CHECK(impc_batch_set_values(b, Px.data(), q.data(), Ax.data(), l.data(), u.data()) == IMPC_OK);
+    CHECK(impc_batch_set_persistent(b, 1) == IMPC_OK);
+    std::vector<double> xd(n), yd(m);
+    impc_info info{};
+    for (int step = 0; step < 3; step++) {
+        if (step == 1) {
+            CHECK(solver.updateGradient(vec(q2)));
+            CHECK(impc_batch_update_lin_cost(b, q2.data()) == IMPC_OK);
+        } else if (step == 2) {
+            CHECK(solver.updateBounds(vec(l3), vec(u3)));
+            CHECK(impc_batch_update_bounds(b, l3.data(), u3.data()) == IMPC_OK);
+        }
+        CHECK(solver.solveProblem() == OsqpEigen::ErrorExitFlag::NoError);
+        CHECK(impc_batch_solve(b, nullptr) == IMPC_OK);
+        CHECK(impc_batch_get(b, xd.data(), yd.data(), &info) == IMPC_OK);
+        const Eigen::VectorXd &xs = solver.getSolution();
+        double dx = 0.0, xm = 1e-12;
+        for (int64_t j = 0; j < n; j++) {
+            dx = std::fmax(dx, std::fabs(xs((Eigen::Index)j) - xd[j]));
+            xm = std::fmax(xm, std::fabs(xd[j]));
+        }
+        std::printf("structured step %d: status %d iters %lld (direct %lld) max|dx| %.3e\n", step,
+                    (int)solver.getStatus(), (long long)solver.getIterations(), (long long)info.iter, dx);
+        CHECK((int64_t)solver.getStatus() == info.status_val);
+        CHECK(solver.getIterations() == info.iter);
+        CHECK(dx <= 1e-9 * xm);
+    }
+    impc_batch_destroy(b);
+    impc_ctx_destroy(ctx);
+}
 
 int main(int argc, char **argv) {
     const bool gpu = argc > 1 && std::strcmp(argv[1], "gpu") == 0;
@@ -85,6 +193,7 @@ int main(int argc, char **argv) {
         CHECK(std::fabs(solver.getSolution()(1) - 0.6) < 2e-3);
         solver.clearSolver();
         CHECK(!solver.isInitialized());
+        structured_case();
     }
     std::printf("%s: %d failure(s)\n", gpu ? "gpu" : "cpu", fails);
     return fails ? 1 : 0;

@@ -24,11 +24,14 @@ def check(x, info, ref, rtol=1e-5):
 
 
 @KERNELS
-def test_update_sequence_matches_persistent_oracle(ctx, kernel):
+@pytest.mark.parametrize("warm", [1, 0], ids=["warm", "cold"])
+def test_update_sequence_matches_persistent_oracle(ctx, kernel, warm):
+    """warm = 0: every osqp_solve cold-starts its iterates (osqp.c osqp_solve, oracle
+    ora_solve :1140) but keeps the scaling, rho and factor of the workspace."""
     cfg = scenarios.static_config(N=20, K=4, batch=12, identical=False, seed=515)
     pat, v = cfg["pattern"], cfg["values"]
     B = v["q"].shape[0]
-    s = impc.default_settings(verbose=0, adaptive_rho_interval=25)
+    s = impc.default_settings(verbose=0, adaptive_rho_interval=25, warm_start=warm)
     rng = np.random.default_rng(9)
     q2 = v["q"] * (1 + 0.05 * rng.standard_normal(v["q"].shape))
     # bounds update: shift the finite box bounds of the states a little
@@ -76,3 +79,45 @@ def test_structured_updates_need_persistence(ctx):
             b.update_lin_cost(v["q"])
     finally:
         b.close()
+
+
+@KERNELS
+def test_explicit_warm_start_between_updates(ctx, kernel):
+    """osqp_warm_start on a persistent workspace replaces its iterates and turns the warm_start
+    setting on (oracle ora_warm_start :1092-1094), keeping scaling and rho."""
+    cfg = scenarios.static_config(N=20, K=3, batch=8, identical=False, seed=517)
+    pat, v = cfg["pattern"], cfg["values"]
+    B = v["q"].shape[0]
+    s = impc.default_settings(verbose=0, adaptive_rho_interval=25, warm_start=0)
+    rng = np.random.default_rng(11)
+    q2 = v["q"] * (1 + 0.05 * rng.standard_normal(v["q"].shape))
+    b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], B)
+    try:
+        b.set_kernel(kernel)
+        b.set_settings(s)
+        b.set_values(v["Px"], v["q"], v["Ax"], v["l"], v["u"])
+        if kernel == impc.KERNEL_STRUCTURED:
+            b.set_persistent(True)
+        b.solve()
+        r1 = b.get()
+        xw = r1[0] * 1.01
+        yw = r1[1] * 0.99
+        b.update_lin_cost(q2)
+        b.warm_start(xw, yw)
+        b.solve()
+        r2 = b.get()
+        b.update_lin_cost(v["q"])  # warm_start is on now: the next solve resumes
+        b.solve()
+        r3 = b.get()
+    finally:
+        b.close()
+    os_ = ora.settings_from(s)
+    for i in range(B):
+        w = ora.Workspace(pat, v["Px"][i], v["q"][i], v["Ax"][i], v["l"][i], v["u"][i], os_)
+        check(r1[0][i], r1[2][i], w.solve())
+        w.update_lin_cost(q2[i])
+        w.warm_start(xw[i], yw[i])
+        check(r2[0][i], r2[2][i], w.solve())
+        w.update_lin_cost(v["q"][i])
+        check(r3[0][i], r3[2][i], w.solve())
+        w.close()
