@@ -51,6 +51,9 @@ namespace impc {
 #define IMPC_NOCHUNK 1
 #endif
 
+#ifndef IMPC_RFOLD  // fold the recursion's subtraction into the first product (rstep): measured slower, off
+#define IMPC_RFOLD 0
+#endif
 #ifndef IMPC_PSTRIDE_PAD
 #define IMPC_PSTRIDE_PAD 1
 #endif
@@ -842,8 +845,18 @@ struct WaveQP {
     // (STRIDE) or contiguous 8-lane sum.
     template <bool STRIDE>
     IMPC_WF double rstep(double f, double c, double v) {
+#if IMPC_RFOLD
+        // c - sum_q f_q v_q with c folded into the products: the lane at reduction index 0 forms
+        // fma(f, -v, c), the others f (-v); the select acts on the prefetched c, off the chain,
+        // and the chain loses its final subtraction.
+        const int l = L & 63;
+        const bool own = STRIDE ? (l >> 3) == 0 : (l & 7) == 0;
+        const double p = __builtin_fma(f, -v, own ? c : 0.0);
+        return STRIDE ? wv.sum_stride8(p) : wv.sum_contig8(p);
+#else
         const double p = prod_nc(f, v);
         return c - (STRIDE ? wv.sum_stride8(p) : wv.sum_contig8(p));
+#endif
     }
 
     // Sweeps with a compile-time step count WC (= WSPEC) are fully unrolled: every LDS wait is
