@@ -46,10 +46,14 @@ $(LIBDIR)/impc_qp_prof.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symb
 		$(ROOT)/include/impc_fanout.h $(ROOT)/include/impc_predict.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -DIMPC_SECTION_PROF -c $< -o $@
-$(PROFLIB): $(LIBDIR)/impc_qp_prof.o $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o
+$(PROFLIB): $(LIBDIR)/impc_qp_prof.o $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o $(LIBDIR)/minsnap.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ -o $@
 
 $(LIBDIR)/symbolic.o: $(CSRC)/symbolic.cpp $(CSRC)/symbolic.hpp
+	@mkdir -p $(LIBDIR)
+	$(CXX) $(HOSTFLAGS) -c $< -o $@
+
+$(LIBDIR)/minsnap.o: $(CSRC)/minsnap.cpp $(ROOT)/include/impc_minsnap.h $(ROOT)/include/impc_mpc.h
 	@mkdir -p $(LIBDIR)
 	$(CXX) $(HOSTFLAGS) -c $< -o $@
 
@@ -61,7 +65,7 @@ $(LIBDIR)/mpc_structure.o: $(CSRC)/mpc_structure.cpp $(CSRC)/mpc_structure.hpp
 	@mkdir -p $(LIBDIR)
 	$(CXX) $(HOSTFLAGS) -c $< -o $@
 
-$(LIB): $(LIBDIR)/impc_qp.o $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o
+$(LIB): $(LIBDIR)/impc_qp.o $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o $(LIBDIR)/minsnap.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ -o $@
 
 $(ORACLE): $(ROOT)/oracle/osqp_oracle.c
@@ -87,7 +91,7 @@ $(SHIMT): $(ROOT)/tests/native/shim_test.cpp $(ROOT)/include/OsqpEigen/OsqpEigen
 
 # kernel experiments (tools/ only): make variant V=name DEFS="-DX=1" -> lib/libimpc_qp_<name>.so,
 # selected at run time with IMPC_LIB_VARIANT=<name>
-variant: $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o
+variant: $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o $(LIBDIR)/minsnap.o
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(CSRC)/impc_qp.hip -o $(LIBDIR)/impc_qp_$(V).o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(LIBDIR)/impc_qp_$(V).o $^ -o $(LIBDIR)/libimpc_qp_$(V).so
 

@@ -134,6 +134,19 @@ _sig("impc_select_best", C.c_int, _P, C.POINTER(SelectParams), C.c_int64, _P, _P
      _dp, _dp, _dp, _P, _P, _dp, _dp)
 _sig("impc_select_best_device", C.c_int, _P, C.POINTER(SelectParams), C.c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P,
      _P, _P, _P, _P, _P, _P, _P, _P)
+class MinsnapParams(C.Structure):
+    """impc_minsnap_params (include/impc_minsnap.h)."""
+    _fields_ = [("poly_degree", C.c_int32), ("diff_degree", C.c_int32), ("continuity_degree", C.c_int32),
+                ("desired_vel", C.c_double), ("soft_constraint", C.c_int32), ("sc_deviation", C.c_double * 3)]
+
+
+_sig("impc_minsnap_dims", C.c_int, C.POINTER(MinsnapParams), C.c_int32, C.POINTER(Dims))
+_sig("impc_minsnap_build_pattern", C.c_int, C.POINTER(MinsnapParams), C.c_int32, _i64p, _i64p, _i64p, _i64p)
+_sig("impc_minsnap_build_values", C.c_int, C.POINTER(MinsnapParams), C.c_int64, C.c_int32, _dp, _dp, _dp, _dp, _dp,
+     _dp, _dp, _dp, _dp, _dp, _dp)
+_sig("impc_minsnap_build_bounds", C.c_int, C.POINTER(MinsnapParams), C.c_int64, C.c_int32, _dp, _dp, _dp, _dp, _dp,
+     _dp, _dp)
+_sig("impc_minsnap_unscale", C.c_int, C.POINTER(MinsnapParams), C.c_int64, C.c_int32, _dp, _dp)
 _sig("impc_mpc_dims", C.c_int, C.POINTER(MpcParams), C.c_int32, C.c_int32, C.POINTER(Dims))
 _sig("impc_mpc_build_pattern", C.c_int, C.POINTER(MpcParams), C.c_int32, C.c_int32, _i64p, _i64p, _i64p, _i64p)
 _sig("impc_mpc_build_values", C.c_int, C.POINTER(MpcParams), C.c_int64, _dp, _dp, _dp, _dp, C.c_int32, _dp, _dp,
@@ -187,7 +200,8 @@ EXPORTED = [
     "impc_mpc_build_pattern", "impc_mpc_build_values", "impc_mpc_warm_start", "impc_mpc_builder_create",
     "impc_mpc_builder_destroy", "impc_mpc_build_values_device", "impc_intent_fanout", "impc_intent_fanout_device",
     "impc_fanout_candidates_device", "impc_intent_params_from_config", "impc_intent_prob", "impc_intent_prob_device",
-    "impc_predict_traj", "impc_predict_traj_device",
+    "impc_predict_traj", "impc_predict_traj_device", "impc_minsnap_dims", "impc_minsnap_build_pattern",
+    "impc_minsnap_build_values", "impc_minsnap_build_bounds", "impc_minsnap_unscale",
 ]
 
 

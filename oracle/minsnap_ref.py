@@ -1,0 +1,162 @@
+"""TEST INFRASTRUCTURE ONLY -- pure-Python restatement of polyTrajSolver's minimum-snap QP
+(reference trajectory_planner/include/trajectory_planner/polyTrajSolver.cpp), the checker for
+impc_minsnap_* (intent-mpc_amd/csrc/minsnap.cpp).  Never imported by the product.
+
+Follows, entry by entry and in the reference's insertion order:
+  updatePath / getConstraintNum  :54-63, :156-160
+  avgTimeAllocation              :125-138  (getPoseDistance, utils.h:69-72)
+  constructP                     :241-307  (only the uncommented loop, :256-270)
+  constructQ                     :309-312
+  constructA                     :314-585  (corridor rows :559-585 not restated)
+  constructBound                 :587-847  (corridor rows not restated)
+  solveX/Y/Z                     :870-905  (coefficient rescaling)
+Values use math.pow / math.sqrt (the same libm calls as the reference's pow / sqrt).
+"""
+import math
+
+import numpy as np
+
+
+def time_allocation(path, desired_vel):
+    """avgTimeAllocation :125-138."""
+    T = [0.0]
+    total = 0.0
+    for i in range(1, len(path)):
+        a, b = path[i], path[i - 1]
+        dist = math.sqrt(math.pow(a[0] - b[0], 2) + math.pow(a[1] - b[1], 2) + math.pow(a[2] - b[2], 2))
+        total += dist / desired_vel
+        T.append(total)
+    return T
+
+
+def constraint_num(S, cont):
+    """getConstraintNum :156-160."""
+    return (2 + S - 1 + S - 1) + (2 + S - 1) + (2 + S - 1) + (S - 1) * (cont - 2)
+
+
+def build(path, deg=7, diff=4, cont=3, desired_vel=1.0, soft=False, sc_dev=(0.0, 0.0, 0.0), init_vel=(0, 0, 0),
+          end_vel=(0, 0, 0), init_acc=(0, 0, 0), end_acc=(0, 0, 0)):
+    """Returns dict(P: {(r,c): v} upper triangle, A: {(r,c): v} in insertion order, l, u [3][m],
+    T, n, m)."""
+    cont = max(cont, 2)
+    W = len(path)
+    S = W - 1
+    D = deg + 1
+    n, m = D * S, constraint_num(S, cont)
+    T = time_allocation(path, desired_vel)
+    P = {}
+    for s in range(S):  # constructP :256-270 (both triangles inserted; OsqpEigen keeps the upper)
+        for i in range(diff, deg + 1):
+            for j in range(diff, deg + 1):
+                f = 1.0
+                for d in range(diff):
+                    f *= float(i - d) * (j - d)
+                f /= float(i + j - diff * 2 + 1)
+                if i <= j:
+                    P[(s * D + i, s * D + j)] = f
+    A = {}
+    r = 0
+
+    def ins(row, col, v):
+        assert (row, col) not in A
+        A[(row, col)] = v
+
+    # position: endpoints :322-345, waypoints :346-360, C0 continuity :362-384
+    for d in range(D):
+        f = math.pow(0.0, d)
+        if f != 0:
+            ins(r, d, f)
+    r += 1
+    for d in range(D):
+        f = math.pow(1.0, d)
+        if f != 0:
+            ins(r, (S - 1) * D + d, f)
+    r += 1
+    for i in range(S - 1):
+        for d in range(D):
+            f = math.pow(1.0, d)
+            if f != 0:
+                ins(r, D * i + d, f)
+        r += 1
+    for i in range(S - 1):
+        for d in range(D):
+            lf, rf = math.pow(1.0, d), math.pow(0.0, d)
+            if lf != 0:
+                ins(r, D * i + d, lf)
+            if rf != 0:
+                ins(r, D * (i + 1) + d, -rf)
+        r += 1
+
+    def endpoints(order):
+        nonlocal r
+        for base, t in ((0, 0.0), ((S - 1) * D, 1.0)):
+            for d in range(D):
+                if d < order:
+                    continue
+                if order == 1:
+                    f = d * math.pow(t, d - 1)
+                else:
+                    f = d * (d - 1) * math.pow(t, d - 2)
+                if f != 0:
+                    ins(r, base + d, f)
+            r += 1
+
+    def continuity(order):
+        nonlocal r
+        for i in range(S - 1):
+            dtL, dtR = T[i + 1] - T[i], T[i + 2] - T[i + 1]
+            for d in range(D):
+                if d < order:
+                    continue
+                fac = 1
+                for k in range(order):
+                    fac *= d - k
+                lf = fac * math.pow(1.0, d - order)
+                rf = fac * math.pow(0.0, d - order)
+                if lf != 0:
+                    ins(r, D * i + d, lf * dtR if order == 1 else lf * math.pow(dtR, order))
+                if rf != 0:
+                    ins(r, D * (i + 1) + d, -rf * dtL if order == 1 else -rf * math.pow(dtL, order))
+            r += 1
+
+    endpoints(1)  # velocity :388-415
+    continuity(1)  # :417-441
+    endpoints(2)  # acceleration :446-474
+    continuity(2)  # :476-502
+    if cont >= 3:
+        continuity(3)  # jerk :504-528
+    if cont >= 4:
+        continuity(4)  # snap :530-555
+    assert r == m
+    l, u = np.zeros((3, m)), np.zeros((3, m))
+    for a in range(3):
+        rows = [(path[0][a], path[0][a]), (path[-1][a], path[-1][a])]
+        for i in range(S - 1):
+            w = path[i + 1][a]
+            rows.append((w - sc_dev[a], w + sc_dev[a]) if soft else (w, w))
+        rows += [(0.0, 0.0)] * (S - 1)
+        rows += [(init_vel[a], init_vel[a]), (end_vel[a], end_vel[a])] + [(0.0, 0.0)] * (S - 1)
+        rows += [(init_acc[a], init_acc[a]), (end_acc[a], end_acc[a])] + [(0.0, 0.0)] * (S - 1)
+        rows += [(0.0, 0.0)] * ((S - 1) * (cont - 2))
+        l[a] = [x[0] for x in rows]
+        u[a] = [x[1] for x in rows]
+    return dict(P=P, A=A, l=l, u=u, T=T, n=n, m=m)
+
+
+def to_csc(entries, n):
+    """{(r, c): v} -> (colptr, rowind, values), rows sorted per column."""
+    items = sorted(entries.items(), key=lambda kv: (kv[0][1], kv[0][0]))
+    p = np.zeros(n + 1, np.int64)
+    for (r, c), _ in items:
+        p[c + 1] += 1
+    return np.cumsum(p), np.array([k[0] for k, _ in items], np.int64), np.array([v for _, v in items])
+
+
+def unscale(x, T, deg):
+    """solveX :870-880 for one axis."""
+    x = np.array(x, np.float64)
+    D = deg + 1
+    for s in range(len(T) - 1):
+        for d in range(D):
+            x[s * D + d] /= math.pow(T[s + 1] - T[s], d)
+    return x
