@@ -51,6 +51,16 @@ namespace impc {
 #define IMPC_NOCHUNK 1
 #endif
 
+#ifndef IMPC_PRIO  // raise the wave priority of the stage-recursion wavefront during its sweeps
+#define IMPC_PRIO 0
+#endif
+#if IMPC_PRIO
+#define IMPC_PRIO_HI() __builtin_amdgcn_s_setprio(IMPC_PRIO)
+#define IMPC_PRIO_LO() __builtin_amdgcn_s_setprio(0)
+#else
+#define IMPC_PRIO_HI() ((void)0)
+#define IMPC_PRIO_LO() ((void)0)
+#endif
 #ifndef IMPC_RFOLD  // fold the recursion's subtraction into the first product (rstep): measured slower, off
 #define IMPC_RFOLD 0
 #endif
@@ -1039,10 +1049,12 @@ struct WaveQP {
             if (LD::CHUNK && W == LD::WSPEC) {
                 if constexpr (LD::CHUNK) fwd_chunked(tb, rb);
             } else if ((L >> 6) == rw) {
+                IMPC_PRIO_HI();
                 if (W == LD::WSPEC)
                     fwd_sweep<LD::WSPEC>(tb, rb, W);
                 else
                     fwd_sweep<0>(tb, rb, W);
+                IMPC_PRIO_LO();
             }
             wv.sync();
         }
@@ -1066,12 +1078,14 @@ struct WaveQP {
             if (LD::CHUNK && W == LD::WSPEC) {
                 if constexpr (LD::CHUNK) bwd_chunked(eb, xb);
             } else if ((L >> 6) == rw) {
+                IMPC_PRIO_HI();
                 if (W == LD::WSPEC)
                     bwd_sweep<((LD::WSPEC - 1) & 1) != 0, LD::WSPEC>(eb, xb, W);
                 else if ((W - 1) & 1)
                     bwd_sweep<true, 0>(eb, xb, W);
                 else
                     bwd_sweep<false, 0>(eb, xb, W);
+                IMPC_PRIO_LO();
             }
             wv.sync();
         }
