@@ -195,6 +195,18 @@ struct GpuTeam {
     double *red;  // >= NL/64 doubles of LDS
     __device__ int lane() const { return (int)threadIdx.x; }
     __device__ void sync() { __syncthreads(); }
+    // barrier for LDS-only exchanges: waits for this wave's LDS operations, not its global /
+    // scratch ones (register-spill stores are lane-private and need no wait at the barrier)
+    __device__ void lsync() {
+#if IMPC_LDSBAR
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0), vmcnt / expcnt left at their maxima
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+#else
+        __syncthreads();
+#endif
+    }
     __device__ double bcast(double v, int src) {
         int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
         int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);

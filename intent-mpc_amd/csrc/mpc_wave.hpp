@@ -51,6 +51,9 @@ namespace impc {
 #define IMPC_NOCHUNK 1
 #endif
 
+#ifndef IMPC_LDSBAR  // LDS-only barriers inside the ADMM iteration (GpuTeam::lsync)
+#define IMPC_LDSBAR 0
+#endif
 #ifndef IMPC_PRIO  // raise the wave priority of the stage-recursion wavefront during its sweeps
 #define IMPC_PRIO 0
 #endif
@@ -1000,7 +1003,7 @@ struct WaveQP {
                 _Pragma("unroll") for (int e = 0; e < 4; e++) pb[gdst(s, e)] = a[s][e] * vv;
             }
         }
-        wv.sync();
+        wv.lsync();
     }
 
     // --------------------------------------------------------------- one ADMM iteration
@@ -1019,7 +1022,7 @@ struct WaveQP {
                 r += col_gather(v);
                 rb[v] = r;
             }
-            wv.sync();
+            wv.lsync();
         }
         IMPC_SEC(kSecRhs);
         IMPC_REP(kSecS1) {
@@ -1034,7 +1037,7 @@ struct WaveQP {
                 }
                 tb[v] = t;
             }
-            wv.sync();
+            wv.lsync();
         }
         IMPC_SEC(kSecS1);
         IMPC_REP(kSecFwd) {
@@ -1056,7 +1059,7 @@ struct WaveQP {
                     fwd_sweep<0>(tb, rb, W);
                 IMPC_PRIO_LO();
             }
-            wv.sync();
+            wv.lsync();
         }
         IMPC_SEC(kSecFwd);
         IMPC_REP(kSecS3) {
@@ -1068,7 +1071,7 @@ struct WaveQP {
                 _Pragma("unroll") for (int cc = 0; cc < 13; cc++) e += ainv[s][cc] * rk[cc];
                 eb[NL * s + L] = e;
             }
-            wv.sync();
+            wv.lsync();
         }
         IMPC_SEC(kSecS3);
         IMPC_REP(kSecBwd) {
@@ -1087,7 +1090,7 @@ struct WaveQP {
                     bwd_sweep<false, 0>(eb, xb, W);
                 IMPC_PRIO_LO();
             }
-            wv.sync();
+            wv.lsync();
         }
         IMPC_SEC(kSecBwd);
         IMPC_REP(kSecS5) {
@@ -1099,7 +1102,7 @@ struct WaveQP {
                 _Pragma("unroll") for (int j = 0; j < 8; j++) t -= cp[s][j] * xn[j];
                 xb[NL * s + L] = t;
             }
-            wv.sync();
+            wv.lsync();
         }
         IMPC_SEC(kSecS5);
         // update_x and the box rows (update_z / project / update_y)

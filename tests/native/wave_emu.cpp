@@ -30,6 +30,7 @@ struct EmuWave {
     int par = 0, wpar = 0;
     int lane() const { return l; }
     void sync() { sh->bar.arrive_and_wait(); }
+    void lsync() { sh->bar.arrive_and_wait(); }
     void wsync() { sh->wbar[l >> 6].arrive_and_wait(); }
     double *next_buf() {
         double *b = sh->scratch[par];
