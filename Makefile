@@ -17,6 +17,8 @@ HARNDIR := $(ROOT)/tests/native/build
 # register pressure past the 2-waves-per-SIMD budget (measured).
 HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -fno-unroll-loops
 HOSTFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -Wall
+# RCCL (multi-GPU cost all-gather, include/impc_comm.h), from the same ROCm as the HIP runtime
+LDLIBS    := -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 LIB     := $(LIBDIR)/libimpc_qp.so
 PROFLIB := $(LIBDIR)/libimpc_qp_prof.so
@@ -33,8 +35,8 @@ harness: $(HARNESS) $(EMU) $(SHIMT)
 
 $(LIBDIR)/impc_qp.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symbolic.hpp $(CSRC)/mpc_wave.hpp \
 		$(CSRC)/mpc_structure.hpp $(CSRC)/select.hpp $(CSRC)/mpc_build.hpp $(CSRC)/mpc_qp_internal.hpp \
-		$(CSRC)/fanout.hpp $(CSRC)/predict.hpp $(ROOT)/include/impc_qp.h $(ROOT)/include/impc_select.h $(ROOT)/include/impc_mpc.h \
-		$(ROOT)/include/impc_fanout.h $(ROOT)/include/impc_predict.h
+		$(CSRC)/fanout.hpp $(CSRC)/predict.hpp $(CSRC)/comm.hpp $(ROOT)/include/impc_qp.h $(ROOT)/include/impc_select.h \
+		$(ROOT)/include/impc_mpc.h $(ROOT)/include/impc_fanout.h $(ROOT)/include/impc_predict.h $(ROOT)/include/impc_comm.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -42,12 +44,12 @@ $(LIBDIR)/impc_qp.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symbolic.
 prof: $(PROFLIB)
 $(LIBDIR)/impc_qp_prof.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symbolic.hpp $(CSRC)/mpc_wave.hpp \
 		$(CSRC)/mpc_structure.hpp $(CSRC)/select.hpp $(CSRC)/mpc_build.hpp $(CSRC)/mpc_qp_internal.hpp \
-		$(CSRC)/fanout.hpp $(CSRC)/predict.hpp $(ROOT)/include/impc_qp.h $(ROOT)/include/impc_select.h $(ROOT)/include/impc_mpc.h \
+		$(CSRC)/fanout.hpp $(CSRC)/predict.hpp $(CSRC)/comm.hpp $(ROOT)/include/impc_qp.h $(ROOT)/include/impc_select.h $(ROOT)/include/impc_mpc.h \
 		$(ROOT)/include/impc_fanout.h $(ROOT)/include/impc_predict.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -DIMPC_SECTION_PROF -c $< -o $@
 $(PROFLIB): $(LIBDIR)/impc_qp_prof.o $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o $(LIBDIR)/minsnap.o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ -o $@
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ -o $@ $(LDLIBS)
 
 $(LIBDIR)/symbolic.o: $(CSRC)/symbolic.cpp $(CSRC)/symbolic.hpp
 	@mkdir -p $(LIBDIR)
@@ -66,7 +68,7 @@ $(LIBDIR)/mpc_structure.o: $(CSRC)/mpc_structure.cpp $(CSRC)/mpc_structure.hpp
 	$(CXX) $(HOSTFLAGS) -c $< -o $@
 
 $(LIB): $(LIBDIR)/impc_qp.o $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o $(LIBDIR)/minsnap.o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ -o $@
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ -o $@ $(LDLIBS)
 
 $(ORACLE): $(ROOT)/oracle/osqp_oracle.c
 	@mkdir -p $(ORADIR)
@@ -93,7 +95,7 @@ $(SHIMT): $(ROOT)/tests/native/shim_test.cpp $(ROOT)/include/OsqpEigen/OsqpEigen
 # selected at run time with IMPC_LIB_VARIANT=<name>
 variant: $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o $(LIBDIR)/minsnap.o
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(CSRC)/impc_qp.hip -o $(LIBDIR)/impc_qp_$(V).o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(LIBDIR)/impc_qp_$(V).o $^ -o $(LIBDIR)/libimpc_qp_$(V).so
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(LIBDIR)/impc_qp_$(V).o $^ -o $(LIBDIR)/libimpc_qp_$(V).so $(LDLIBS)
 
 clean:
 	rm -rf $(LIBDIR) $(ORADIR) $(HARNDIR)

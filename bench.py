@@ -7,17 +7,27 @@ the warm start, osqp_solve (ADMM to OSQP 0.6.2's termination) and the unscaling 
 i.e. everything mpcPlanner::solveTraj asks OsqpEigen for (mpcPlanner.cpp:475-526).  Inputs
 (P, q, A, l, u and the warm start) are resident in HBM before the timed region.
 
-Workload (BASELINE.json configs[2], the metric's batch=65536): per GPU 8192 planning instances x
-8 intent hypotheses, N=20, 8 predicted dynamic obstacles (hypotheses LEFT+FORWARD / RIGHT+FORWARD
-carry a 9th), synthetic data from impc.scenarios.intent_config, bucketed by obstacle count.
+Workloads (--workload):
+  config3 (default; BASELINE.json configs[2], the metric's batch=65536): per GPU 8192 planning
+      instances x 8 intent hypotheses, N=20, 8 predicted dynamic obstacles (hypotheses
+      LEFT+FORWARD / RIGHT+FORWARD carry a 9th), bucketed by obstacle count.  Weak scaling: every
+      rank solves its own 65,536 QPs; an all_gather of the per-QP records returns the hypothesis
+      costs to every rank after the timed region.
+  config4 (BASELINE.json configs[3]): 262,144 QPs in total (32,768 instances x 8 hypotheses,
+      K ~ U{0..20} obstacles), instances sharded across the ranks in contiguous ranges balanced by
+      Sigma m (impc.distributed.shard_plan).  Strong scaling: the job is fixed, each rank runs one
+      grouped launch over its ~42 pattern buckets per step, and each step ends with one RCCL
+      all_gather of every QP's cost record (the 64-byte impc_info, read straight from HBM).
 
-Multi-GPU: one process per GPU (torchrun), each rank solves its own 65536 QPs (independent
-instances, weak scaling, no data-path collective); an all_gather of the per-QP cost/status
-records returns the hypothesis costs to every rank, outside the timed region.
+Multi-GPU: one process per GPU.  `python bench.py --gpus N` without a torchrun environment
+starts `torch.distributed.run` with N processes itself (before touching the GPU) and exits with
+its code; under torchrun, WORLD_SIZE must equal --gpus.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,7 +38,8 @@ sys.path.insert(0, os.path.join(ROOT, "intent-mpc_amd", "python"))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-PEAK_FP64_TFLOPS = 78.6    # MI355X FP64 vector peak (spec)
+PEAK_FP64_TFLOPS = 78.6    # MI355X FP64 vector peak (spec; 256 CU x 2.4 GHz x 128 flop/clk)
+METRIC = "QP-solves/s + p50 solve latency, N=20 horizon, batch=65536, 1/2/4/8 MI355X"
 
 
 def throughput(world, qps_per_rank, steps, elapsed_s):
@@ -43,9 +54,63 @@ def algorithmic_bytes(n, m, K, N):
     return 8 * (n + 2 * m + 4 * K * W) + 8 * (n + m) + 16
 
 
-def algorithmic_flops(n, m, nnzA, N, iters):
+def flops_per_iter(n, m, nnzA, N):
     """F_iter ~ 754 N + 4 nnzA + 4m + 6n + 10m per ADMM iteration."""
-    return iters * (754 * N + 4 * nnzA + 4 * m + 6 * n + 10 * m) + 3700 * N
+    return 754 * N + 4 * nnzA + 4 * m + 6 * n + 10 * m
+
+
+def algorithmic_flops(n, m, nnzA, N, iters):
+    """F_solve = iters x F_iter + ~3.7k N (factorisation); iters may be an array
+    (one QP each) or a scalar."""
+    it = np.asarray(iters, dtype=np.float64)
+    return float(it.sum() * flops_per_iter(n, m, nnzA, N) + it.size * 3700 * N)
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def relaunch(args_n, argv):
+    """--gpus N outside torchrun: start N ranks with torch.distributed.run as a child process
+    (nothing has touched the GPU yet) and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args_n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + argv
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model
+
+
+def make_batch(impc, ctx, bk, settings, full_values, profile):
+    pat, vals = bk["pattern"], bk["values"]
+    B = vals["q"].shape[0]
+    b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], B)
+    b.set_settings(settings)
+    split = None if full_values else impc.shared_split(vals["Px"], vals["Ax"])
+    nvar = None
+    if split is None:
+        b.set_values(vals["Px"], vals["q"], vals["Ax"], vals["l"], vals["u"])
+    else:
+        Px0, Ax0, var, Axv = split
+        b.set_values_shared(Px0, Ax0, var, Axv, vals["q"], vals["l"], vals["u"])
+        nvar = int(var.size)
+    if bk.get("x_ws") is not None:
+        b.warm_start(bk["x_ws"], np.zeros((B, pat["m"])))
+    b.set_profiling(profile)
+    return b, nvar
 
 
 def main():
@@ -53,203 +118,246 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--instances", type=int, default=8192, help="planning instances per GPU (x8 hypotheses)")
-    ap.add_argument("--cpu-sample", type=int, default=1024, help="QPs solved by the CPU baseline (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--workload", choices=("config3", "config4"), default="config3")
+    ap.add_argument("--instances", type=int, default=8192, help="config3: planning instances per GPU (x8 hypotheses)")
+    ap.add_argument("--total-qps", type=int, default=262144, help="config4: QPs of the whole job")
+    ap.add_argument("--cpu-sample", type=int, default=8192, help="QPs solved by the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="CPU baseline threads (the GPU box's CPU share per GPU is 16)")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--full-values", action="store_true",
                     help="ship every QP's full CSC values (default: shared P / dynamics / box values, "
                          "per-QP obstacle rows, impc_batch_set_values_shared)")
     args = ap.parse_args()
 
-    import impc
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(relaunch(args.gpus, sys.argv[1:]))
     from impc import distributed as D
-    from impc import scenarios
-
     rank, local_rank, world = D.env()
-    dist = D.init("nccl", local_rank) if world > 1 else None
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
 
+    import impc
+    from impc import scenarios
+    # host traffic (rendezvous, barriers, max over ranks) on gloo; the device records move over
+    # RCCL through the solver library's communicator (impc_comm.h) -- this process never starts
+    # PyTorch's own HIP runtime
+    dist = D.init("gloo", local_rank) if world > 1 else None
 
-    t_gen = time.time()
-    buckets = scenarios.intent_config(N=20, K=8, instances=args.instances, hyps=8, seed=D.rank_seed(3000, rank))
-    t_gen = time.time() - t_gen
     settings = impc.default_settings(verbose=0)
+    t_gen = time.time()
+    if args.workload == "config3":
+        buckets = scenarios.intent_config(N=20, K=8, instances=args.instances, hyps=8,
+                                          seed=D.rank_seed(3000, rank))
+        bks = [bk for _, bk in sorted(buckets.items())]
+    else:
+        Kinst, w = scenarios.config4_plan(total_qps=args.total_qps)
+        bounds = D.shard_plan(w, world)
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+        bks = scenarios.config4_rank(lo, hi, Kinst)
+        share = [float(w[bounds[r]:bounds[r + 1]].sum()) for r in range(world)]
+    t_gen = time.time() - t_gen
 
-    ctx = impc.Context(local_rank if world > 1 else 0)
-    batches, nvar = [], {}
-    for K, bk in sorted(buckets.items()):
-        pat, vals = bk["pattern"], bk["values"]
-        B = vals["q"].shape[0]
-        b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], B)
-        b.set_settings(settings)
-        split = None if args.full_values else impc.shared_split(vals["Px"], vals["Ax"])
-        if split is None:
-            b.set_values(vals["Px"], vals["q"], vals["Ax"], vals["l"], vals["u"])
+    ctx = impc.Context(local_rank)
+    batches, nvar = [], []
+    for bk in bks:
+        b, nv = make_batch(impc, ctx, bk, settings, args.full_values, profile=True)
+        batches.append((bk, b))
+        if nv is not None:
+            nvar.append(nv)
+    total_qps = sum(b.B for _, b in batches)
+    structured = all(b.stats()["kernel"] == impc.KERNEL_STRUCTURED for _, b in batches)
+    grouped = structured and len(batches) > 1
+    # every rank's QP count (config 4's shards differ) and the RCCL communicator of the cost gather
+    counts = [total_qps] * world
+    if dist is not None:
+        import torch
+        t = torch.zeros(world, dtype=torch.int64)
+        t[rank] = total_qps
+        dist.all_reduce(t)
+        counts = [int(c) for c in t]
+    comm = D.make_comm(dist, ctx) if (world > 1 or args.workload == "config4") else None
+    max_qps = max(counts)
+    recv = impc.DeviceArray(ctx, (world * max_qps,), impc.INFO_DTYPE) if comm is not None else None
+    gather_in_step = args.workload == "config4" and not args.no_allgather
+
+    def launch():
+        if grouped:  # one persistent launch over all pattern buckets (impc_batch_solve_group)
+            impc.solve_group([b for _, b in batches])
         else:
-            Px0, Ax0, var, Axv = split
-            b.set_values_shared(Px0, Ax0, var, Axv, vals["q"], vals["l"], vals["u"])
-            nvar[K] = int(var.size)
-        b.warm_start(bk["x_ws"], np.zeros((B, pat["m"])))
-        b.set_profiling(True)
-        batches.append((K, bk, b))
-    total_qps = sum(b.B for _, _, b in batches)
-
-    grouped = all(b.stats()["kernel"] == impc.KERNEL_STRUCTURED for _, _, b in batches) and len(batches) > 1
+            for _, b in batches:
+                b.setup()
+                b.solve()
 
     def step():
-        if grouped:  # one persistent launch over all pattern buckets (impc_batch_solve_group)
-            impc.solve_group([b for _, _, b in batches])
-            return
-        for _, _, b in batches:
-            b.setup()
-            b.solve()
-
-    def sync():
-        ctx.synchronize()  # hipStreamSynchronize + hipDeviceSynchronize
+        ctx.timer_mark()
+        launch()
+        ctx.timer_mark()
+        if gather_in_step:  # every QP's cost record to every rank, one ncclAllGather
+            comm.gather_info([b for _, b in batches], max_qps, recv.ptr)
 
     for _ in range(args.warmup):
         step()
-    sync()
+    ctx.synchronize()
+    ctx.timer_read()  # drop the warm-up marks
     if dist is not None:
         dist.barrier()
     # timed region: barrier + device sync on both sides
     t0 = time.perf_counter()
-    kt = {K: [0.0, 0.0, 0.0] for K, _, _ in batches}
     for _ in range(args.steps):
         step()
-    sync()
+    ctx.synchronize()
     if dist is not None:
         dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    # per-kernel durations of the last step (HIP events on the solver stream)
-    for K, _, b in batches:
-        kt[K] = list(b.timings())
+    elapsed = time.perf_counter() - t0
+    kernel_ms = [float(v) for v in ctx.timer_read()]  # HIP events around each launch, on its stream
+    elapsed = D.max_over_ranks(dist, elapsed)
+    ms_per_step = 1000.0 * elapsed / args.steps
+    launch_ms = float(np.mean(kernel_ms))
+
     # per-QP device solve latency of the last step (structured kernel; work-queue pick-up to results)
     try:
-        lat = np.concatenate([b.qp_latency() for _, _, b in batches])
+        lat = np.concatenate([b.qp_latency() for _, b in batches])
         qp_lat = {"p50": float(np.percentile(lat, 50)), "p90": float(np.percentile(lat, 90)),
                   "p99": float(np.percentile(lat, 99)), "max": float(lat.max()), "unit": "ms",
                   "what": "per-QP device solve latency (dequeue to results written), last timed step"}
     except impc.ImpcError:
         qp_lat = None
-    elapsed = D.max_over_ranks(dist, elapsed)
-    ms_per_step = 1000.0 * elapsed / args.steps
 
     # results + parity-relevant statistics (outside the timed region)
     iters_all, status_all, rho_all, recs = [], [], [], []
-    for K, bk, b in batches:
+    alg_bytes = alg_flops = 0.0
+    for bk, b in batches:
         x, y, info = b.get()
+        pat = bk["pattern"]
         iters_all.append(info["iter"])
         status_all.append(info["status_val"])
         rho_all.append(info["rho_updates"])
         recs.append(D.make_records(rank, bk["inst"], bk["hyp"], info))
+        alg_bytes += b.B * algorithmic_bytes(pat["n"], pat["m"], bk["K"], bk["N"])
+        alg_flops += algorithmic_flops(pat["n"], pat["m"], int(pat["Ap"][-1]), bk["N"], info["iter"])
     iters_all = np.concatenate(iters_all)
     status_all = np.concatenate(status_all)
 
-    # device-side candidate scoring + selection of every instance's replan (SURVEY.md 8f row 1,
-    # mpcPlanner.cpp:771-887), on the solutions still in HBM; timed on its own
-    sel = select_candidates(impc, scenarios, ctx, buckets, batches, pd_params=settings_params(buckets))
-    if not args.no_allgather:
-        D.gather_records(dist, np.concatenate(recs))  # hypothesis costs to every rank
+    sel = None
+    if args.workload == "config3":
+        # device-side candidate scoring + selection of every instance's replan (SURVEY.md 8f row 1,
+        # mpcPlanner.cpp:771-887), on the solutions still in HBM; timed on its own
+        sel = select_candidates(impc, scenarios, ctx, buckets, dict((bk["K"], b) for bk, b in batches),
+                                pd_params=bks[0]["params"])
+        if comm is not None and not args.no_allgather:  # hypothesis costs to every rank
+            comm.gather_info([b for _, b in batches], max_qps, recv.ptr)
+    gathered = None
+    if recv is not None and not args.no_allgather:
+        allinfo = D.unpad(recv.get(), counts)
+        mine = np.concatenate([r[:, 4] for r in recs])
+        off = sum(counts[:rank])
+        gathered = {"records": int(allinfo.size), "ranks": world,
+                    "own_block_matches": bool(np.array_equal(allinfo["status_val"][off:off + total_qps], mine))}
 
-    value = throughput(world, total_qps, args.steps, elapsed)
+    global_batch = int(sum(counts))
+    value = global_batch * args.steps / elapsed  # every rank's QPs, each timed step, max-over-ranks time
 
-    # roofline of the dominant kernel, SURVEY.md 8(d) algorithmic bytes
-    kernel_name = ("k_mpc_wave_group" if grouped else "k_mpc_wave") \
-        if all(b.stats()["kernel"] == impc.KERNEL_STRUCTURED for _, _, b in batches) else "k_solve"
-    solve_ms = sum(kt[K][1] for K in kt)
-    setup_ms = sum(kt[K][0] for K in kt)
-    alg_bytes = 0.0
-    alg_flops = 0.0
-    for K, bk, b in batches:
-        pat = bk["pattern"]
-        alg_bytes += b.B * algorithmic_bytes(pat["n"], pat["m"], K, 20)
-    mean_iter = float(iters_all.mean())
-    for K, bk, b in batches:
-        pat = bk["pattern"]
-        alg_flops += b.B * algorithmic_flops(pat["n"], pat["m"], int(pat["Ap"][-1]), 20, mean_iter)
-    achieved = alg_bytes / (solve_ms * 1e-3) / 1e9 if solve_ms > 0 else None
-    values_mode = "shared" if nvar and len(nvar) == len(batches) else "full"
+    # roofline of the dominant kernel: FP64 compute/latency bound, so the headline
+    # fraction is the algorithmic FP64 rate over the vector peak; the HBM fraction and the
+    # PMC-measured traffic ride along
+    kernel_name = ("k_mpc_wave_group" if grouped else "k_mpc_wave") if structured else "k_solve"
+    tflops = alg_flops / (launch_ms * 1e-3) / 1e12
+    gbs = alg_bytes / (launch_ms * 1e-3) / 1e9
+    values_mode = "shared" if len(nvar) == len(batches) else "full"
+    nvar_desc = {str(bk["K"]): nv for (bk, _), nv in zip(batches, nvar)} if values_mode == "shared" else None
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_k_solve.json")
     if os.path.exists(pmc_path):
         try:
             pm = json.load(open(pmc_path))
             if pm.get("qps_per_launch") == total_qps and pm.get("kernel") == kernel_name and \
-                    pm.get("values", "full") == values_mode:
+                    pm.get("values", "full") == values_mode and pm.get("workload", "config3") == args.workload:
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        cpu = cpu_baseline(buckets, settings, args.cpu_sample, args.cpu_threads)
+        cpu = cpu_baseline(bks, settings, args.cpu_sample, args.cpu_threads)
 
+    if args.workload == "config3":
+        config = {
+            "workload": "configs[2]: 8192 instances x 8 intent hypotheses per GPU, N=20, 8(+1) dynamic obstacles",
+            "global_batch": global_batch, "batch_per_gpu": total_qps,
+            "buckets": {str(bk["K"]): int(b.B) for bk, b in batches},
+        }
+    else:
+        config = {
+            "workload": "configs[3]: 262144 mixed-K QPs (K ~ U{0..20}) sharded by Sigma m, per-step RCCL "
+                        "all-gather of the cost records",
+            "global_batch": global_batch, "batch_per_gpu": total_qps, "shard_qps": counts,
+            "shard_sigma_m": share, "pattern_buckets": len(batches), "allgather": gathered,
+        }
+    config.update({
+        "horizon": 20,
+        "settings": "OSQP 0.6.2 defaults, adaptive_rho_interval auto->25, warm-started from previous plan",
+        "parallelism": f"independent QPs, {world} rank(s)",
+        "values": values_mode + (f" (P and dynamics/box A entries once per bucket, per-QP A entries {nvar_desc})"
+                                 if values_mode == "shared" else " (every QP's full CSC values)"),
+    })
     line = {
-        "metric": "QP-solves/s + p50 solve latency, N=20 horizon, batch=65536, 1/2/4/8 MI355X",
+        "metric": METRIC,
         "value": value,
         "unit": "QP-solves/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
-        "p50_latency_ms": ms_per_step,
+        "p50_latency_ms": qp_lat["p50"] if qp_lat else None,
+        "step_latency_ms": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if args.workload == "config3" else "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded intent-hypothesis scenarios, SURVEY.md 8d)",
-        "config": {
-            "workload": "configs[2]: 8192 instances x 8 intent hypotheses per GPU, N=20, 8(+1) dynamic obstacles",
-            "global_batch": world * total_qps,
-            "batch_per_gpu": total_qps,
-            "buckets": {str(K): int(b.B) for K, _, b in batches},
-            "horizon": 20,
-            "settings": "OSQP 0.6.2 defaults, adaptive_rho_interval auto->25, warm-started from previous plan",
-            "parallelism": f"independent QPs, {world} rank(s)",
-            "values": values_mode + (f" (P and dynamics/box A entries once per bucket, per-QP A entries {nvar})"
-                                     if values_mode == "shared" else " (every QP's full CSC values)"),
-        },
+        "config": config,
         "qp_latency_ms": qp_lat,
-        "iters": {"mean": mean_iter, "p50": float(np.median(iters_all)), "max": int(iters_all.max()),
+        "iters": {"mean": float(iters_all.mean()), "p50": float(np.median(iters_all)), "max": int(iters_all.max()),
                   "rho_updates_mean": float(np.concatenate(rho_all).mean())},
         "status_counts": {str(int(k)): int(v) for k, v in zip(*np.unique(status_all, return_counts=True))},
-        "kernel_ms": {"setup": setup_ms, "solve": solve_ms,
-                      "outputs": sum(kt[K][2] for K in kt)},
+        "kernel_ms": {"mean": launch_ms, "per_step": kernel_ms,
+                      "what": "HIP events around each timed step's launch, on its stream (rank 0)"},
         "roofline": {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": PEAK_HBM_GBS,
-            "unit": "GB/s",
-            "frac": (achieved / PEAK_HBM_GBS) if achieved else None,
+            "bound": "fp64",
+            "achieved": tflops,
+            "peak": PEAK_FP64_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": tflops / PEAK_FP64_TFLOPS,
             "traffic": traffic,
             "kernel": kernel_name,
-            "algorithmic_bytes_per_launch": alg_bytes,
+            "algorithmic_flops_per_launch": alg_flops,
+            "what": "SURVEY.md 8d F_iter x each QP's iterations + 3.7k N per QP, over the mean event-timed launch",
+            "hbm": {"achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
+                    "algorithmic_bytes_per_launch": alg_bytes, "traffic_bytes_per_launch": traffic},
         },
-        "fp64": {"achieved_tflops": alg_flops / ((solve_ms + setup_ms) * 1e-3) / 1e12 if solve_ms else None,
-                 "peak_tflops": PEAK_FP64_TFLOPS},
         "cpu_baseline": cpu,
         "selection": sel,
+        "cost_allgather": gathered,
         "gen_seconds": t_gen,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
-    for _, _, b in batches:
+    if recv is not None:
+        recv.free()
+    if comm is not None:
+        comm.close()
+    for _, b in batches:
         b.close()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
 
 
-def settings_params(buckets):
-    return next(iter(buckets.values()))["params"]
-
-
-def select_candidates(impc, scenarios, ctx, buckets, batches, pd_params):
+def select_candidates(impc, scenarios, ctx, buckets, batch_by_k, pd_params):
     """impc_select_best over all instances (6 candidates each, all solved QPs count as solveTraj
     successes, as OSQP's exitflag is 0 for every status); returns timing and the pick histogram."""
-    ptrs = {K: b.device_results()[0] for K, _, b in batches}
+    ptrs = {K: b.device_results()[0] for K, b in batch_by_k.items()}
     d = scenarios.selection_arrays(buckets, ptrs)
     I, C, N = d["I"], d["C"], d["N"]
     params = dict(horizon=N, num_candidates=C, max_dynamic=d["kmax"], pred_len=d["L"], num_static=0, prev_len=N,
@@ -267,24 +375,27 @@ def select_candidates(impc, scenarios, ctx, buckets, batches, pd_params):
             "picked_histogram": [int(v) for v in picks]}
 
 
-def cpu_baseline(buckets, settings, sample, threads):
-    """The oracle (C restatement of OSQP 0.6.2, reference per-call pattern) on host cores,
-    over a bounded sample of the same workload (first QPs of each bucket, bucket-proportional)."""
+def cpu_baseline(bks, settings, sample, threads):
+    """The oracle (C restatement of OSQP 0.6.2, reference per-call pattern: setup + warm start +
+    solve per QP) on `threads` host threads of the GPU box, over a bounded sample of the same
+    workload (the first QPs of each bucket, bucket-proportional)."""
     from oracle import osqp_oracle as ora
-    total = sum(bk["values"]["q"].shape[0] for bk in buckets.values())
+    total = sum(bk["values"]["q"].shape[0] for bk in bks)
     s = ora.settings_from(settings)
     t_all, n_all = 0.0, 0
-    for K, bk in sorted(buckets.items()):
+    for bk in bks:
         B = bk["values"]["q"].shape[0]
-        k = max(1, int(round(sample * B / total)))
+        k = min(B, max(1, int(round(sample * B / total))))
         v = bk["values"]
         t = time.perf_counter()
         ora.solve_batch(bk["pattern"], v["Px"][:k], v["q"][:k], v["Ax"][:k], v["l"][:k], v["u"][:k], s,
-                        x_ws=bk["x_ws"][:k], threads=threads)
+                        x_ws=None if bk.get("x_ws") is None else bk["x_ws"][:k], threads=threads)
         t_all += time.perf_counter() - t
         n_all += k
     return {"value": n_all / t_all, "unit": "QP-solves/s", "cores": threads, "kind": "port",
-            "sample": f"{n_all} QPs of the same workload (first of each bucket), one setup+warm-start+solve per QP"}
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_info(),
+            "sample": f"{n_all} QPs of the same workload (first of each bucket), one setup+warm-start+solve "
+                      f"per QP, {threads} threads ({t_all:.1f} s wall)"}
 
 
 if __name__ == "__main__":

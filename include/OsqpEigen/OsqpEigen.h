@@ -13,7 +13,10 @@
  *                                               Matrix, setLower/UpperBound
  *   OsqpEigen::Solver    (Solver.hpp:87-249)    initSolver, setWarmStart, solveProblem, getStatus,
  *                                               getSolution, getDualSolution, clearSolver,
- *                                               updateGradient / updateLower|UpperBound / updateBounds
+ *                                               clearSolverVariables, updateGradient /
+ *                                               updateLower|UpperBound / updateBounds,
+ *                                               updateHessianMatrix / updateLinearConstraintsMatrix,
+ *                                               set|getPrimalVariable, set|getDualVariable
  *   Status / ErrorExitFlag values               (Constants.hpp:14-56, OSQP constants.h:18-51)
  *
  * Each Solver owns a one-QP batch on a process-wide context (device IMPC_DEVICE, default 0); the
@@ -24,9 +27,13 @@
  * a non-convex P surfaces as ErrorExitFlag::NonCvxError from solveProblem instead of a failed
  * initSolver; the update* calls keep OSQP's workspace semantics on both kernels (scaling, rho,
  * factor and iterates carried over: the structured kernel through a persistent workspace,
- * impc_batch_set_persistent, the generic kernel in place).  An update before the first solve,
- * or on a structured batch whose settings exceed the persistent workspace's 20 Ruiz passes,
- * re-runs setup from the new data instead, warm-started from the last solution.
+ * impc_batch_set_persistent, the generic kernel in place).  An update before the first solve
+ * (on either kernel), or on a structured batch whose settings exceed the persistent workspace's
+ * 20 Ruiz passes, re-runs setup from the new data instead, warm-started from the last solution.
+ * The argument types are the reference declarations' (Eigen::Ref, SparseCompressedBase, the
+ * fixed-size Matrix<T, n, 1> templates of Solver.hpp:217-231); this repository compiles the
+ * header against a test-only Eigen stand-in (tests/native/mock_eigen), since Eigen 3.3 is not in
+ * the image -- real-Eigen template deduction is therefore unverified here.
  *
  * Requires Eigen's <Eigen/Dense> and <Eigen/Sparse> (the reference's own dependency) and
  * linking against intent-mpc_amd/lib/libimpc_qp.so.
@@ -167,6 +174,8 @@ public:
     const impc_settings &getSettings() const { return m_s; }
 };
 
+/* Data.hpp:44-151: same member names and argument types (setGradient / set*Bound take
+ * Eigen::Ref<VectorXd> by value, the matrices an Eigen::SparseCompressedBase). */
 class Data {
     int64_t m_n = 0, m_m = 0;
     bool m_hasP = false, m_hasA = false, m_hasq = false, m_hasl = false, m_hasu = false;
@@ -185,64 +194,110 @@ public:
     void clearLinearConstraintsMatrix() { m_hasA = false; Ap.clear(); Ai.clear(); Ax.clear(); }
 
     template <typename Derived>
-    bool setHessianMatrix(const Derived &H) {
+    bool setHessianMatrix(const Eigen::SparseCompressedBase<Derived> &hessianMatrix) {
         if (m_hasP) { detail::debug("the Hessian matrix was already set"); return false; }
-        if ((int64_t)H.rows() != m_n || (int64_t)H.cols() != m_n) { detail::debug("the Hessian matrix has to be n x n"); return false; }
-        detail::to_csc(H, true, Pp, Pi, Px);
+        if ((int64_t)hessianMatrix.rows() != m_n || (int64_t)hessianMatrix.cols() != m_n) {
+            detail::debug("the Hessian matrix has to be n x n");
+            return false;
+        }
+        detail::to_csc(hessianMatrix.derived(), true, Pp, Pi, Px);
         return m_hasP = true;
     }
     template <typename Derived>
-    bool setLinearConstraintsMatrix(const Derived &A) {
+    bool setLinearConstraintsMatrix(const Eigen::SparseCompressedBase<Derived> &linearConstraintsMatrix) {
         if (m_hasA) { detail::debug("the constraint matrix was already set"); return false; }
-        if ((int64_t)A.rows() != m_m || (int64_t)A.cols() != m_n) { detail::debug("the constraint matrix has to be m x n"); return false; }
-        detail::to_csc(A, false, Ap, Ai, Ax);
+        if ((int64_t)linearConstraintsMatrix.rows() != m_m || (int64_t)linearConstraintsMatrix.cols() != m_n) {
+            detail::debug("the constraint matrix has to be m x n");
+            return false;
+        }
+        detail::to_csc(linearConstraintsMatrix.derived(), false, Ap, Ai, Ax);
         return m_hasA = true;
     }
-    template <typename V>
-    bool setGradient(const V &g) {
-        if (!detail::copy_vec(g, m_n, q)) { detail::debug("the gradient has to be n x 1"); return false; }
+    bool setGradient(Eigen::Ref<Eigen::Matrix<double, Eigen::Dynamic, 1>> gradientVector) {
+        if (!detail::copy_vec(gradientVector, m_n, q)) { detail::debug("the gradient has to be n x 1"); return false; }
         return m_hasq = true;
     }
-    template <typename V>
-    bool setLowerBound(const V &lb) {
-        if (!detail::copy_vec(lb, m_m, l)) { detail::debug("the lower bound has to be m x 1"); return false; }
+    bool setLowerBound(Eigen::Ref<Eigen::Matrix<double, Eigen::Dynamic, 1>> lowerBoundVector) {
+        if (!detail::copy_vec(lowerBoundVector, m_m, l)) { detail::debug("the lower bound has to be m x 1"); return false; }
         return m_hasl = true;
     }
-    template <typename V>
-    bool setUpperBound(const V &ub) {
-        if (!detail::copy_vec(ub, m_m, u)) { detail::debug("the upper bound has to be m x 1"); return false; }
+    bool setUpperBound(Eigen::Ref<Eigen::Matrix<double, Eigen::Dynamic, 1>> upperBoundVector) {
+        if (!detail::copy_vec(upperBoundVector, m_m, u)) { detail::debug("the upper bound has to be m x 1"); return false; }
         return m_hasu = true;
+    }
+    bool setBounds(Eigen::Ref<Eigen::Matrix<double, Eigen::Dynamic, 1>> lowerBound,
+                   Eigen::Ref<Eigen::Matrix<double, Eigen::Dynamic, 1>> upperBound) {
+        return setLowerBound(lowerBound) && setUpperBound(upperBound);
     }
     bool isSet() const { return m_n > 0 && m_hasP && m_hasA && m_hasq && m_hasl && m_hasu; }
 };
 
+/* Solver.hpp:87-249: same member names and signatures (Solver.hpp:196-231 templates included). */
 class Solver {
+    using VecRef = Eigen::Ref<const Eigen::Matrix<double, Eigen::Dynamic, 1>>;
     std::unique_ptr<Settings> m_settings;
     std::unique_ptr<Data> m_data;
     impc_batch m_batch = nullptr;
     bool m_solved = false;
     impc_info m_info{};
     Eigen::Matrix<double, Eigen::Dynamic, 1> m_x, m_y;
-
-    bool m_persistent = false;  // structured batch with a persistent workspace
+    // the iterate the next solve starts from, as far as the host knows (last solution or last warm
+    // start, unscaled): osqp_warm_start_x / _y replace one half and keep the other
+    std::vector<double> m_wx, m_wy;
+    bool m_persistent = false;     // structured batch with a persistent workspace
+    bool m_setup_current = false;  // the device workspace is set up on the current data
 
     bool structured() const {
         impc_batch_stats st{};
         return m_batch && impc_batch_get_stats(m_batch, &st) == IMPC_OK && st.kernel == IMPC_KERNEL_STRUCTURED;
     }
-    // restart a structured batch from the current data, warm-started from the last solution
+    // osqp_update_* applies to the set-up workspace in place: a persistent structured batch or a
+    // generic batch, once a solve has set it up on the current data
+    bool in_place() const { return m_setup_current && (m_persistent || !structured()); }
+    bool warm_start_raw(const std::vector<double> &x, const std::vector<double> &y) {
+        int rc = impc_batch_warm_start(m_batch, x.data(), y.data());
+        if (rc) { detail::debug_impc("impc_batch_warm_start", rc); return false; }
+        m_wx = x;
+        m_wy = y;
+        return true;
+    }
+    // osqp_setup again from the current data, warm-started from the last solution (what OsqpEigen
+    // does when an update cannot be applied in place: clearSolver, initSolver, set*Variable)
     bool resetup_from_data() {
         const Data &d = *m_data;
         int rc = impc_batch_set_values(m_batch, d.Px.data(), d.q.data(), d.Ax.data(), d.l.data(), d.u.data());
         if (rc) { detail::debug_impc("impc_batch_set_values", rc); return false; }
-        if (m_solved) {
-            std::vector<double> x((size_t)d.numberOfVariables()), y((size_t)d.numberOfConstraints());
-            for (size_t k = 0; k < x.size(); ++k) x[k] = m_x((int)k);
-            for (size_t k = 0; k < y.size(); ++k) y[k] = m_y((int)k);
-            rc = impc_batch_warm_start(m_batch, x.data(), y.data());
-            if (rc) { detail::debug_impc("impc_batch_warm_start", rc); return false; }
-        }
+        m_setup_current = false;
+        if (m_solved) return warm_start_raw(m_wx, m_wy);
         return true;
+    }
+    template <typename Derived>
+    bool update_matrix(const Eigen::SparseCompressedBase<Derived> &M, bool hessian) {
+        if (!m_batch) { detail::debug("the solver has not been initialized"); return false; }
+        Data &d = *m_data;
+        const int64_t rows = hessian ? d.numberOfVariables() : d.numberOfConstraints();
+        if ((int64_t)M.rows() != rows || (int64_t)M.cols() != d.numberOfVariables()) {
+            detail::debug(hessian ? "the hessian matrix has to be a nxn matrix" : "the constraint matrix has to be m x n");
+            return false;
+        }
+        std::vector<int64_t> p, i;
+        std::vector<double> x;
+        detail::to_csc(M.derived(), hessian, p, i, x);
+        if (p != (hessian ? d.Pp : d.Ap) || i != (hessian ? d.Pi : d.Ai)) {
+            // new sparsity pattern: a new batch (OsqpEigen: clearSolver + initSolver + warm start)
+            std::vector<double> wx = m_wx, wy = m_wy;
+            const bool had = m_solved;
+            if (hessian) { d.Pp = p; d.Pi = i; d.Px = x; } else { d.Ap = p; d.Ai = i; d.Ax = x; }
+            clearSolver();
+            if (!initSolver()) return false;
+            return had ? warm_start_raw(wx, wy) : true;
+        }
+        std::vector<double> &dst = hessian ? d.Px : d.Ax;
+        std::vector<double> old = dst;
+        dst = x;
+        if (resetup_from_data()) return true;
+        dst = old;
+        return false;
     }
 
 public:
@@ -278,7 +333,10 @@ public:
         m_persistent = structured() && impc_batch_set_persistent(m_batch, 1) == IMPC_OK;
         m_x.setZero(d.numberOfVariables());
         m_y.setZero(d.numberOfConstraints());
+        m_wx.assign((size_t)d.numberOfVariables(), 0.0);
+        m_wy.assign((size_t)d.numberOfConstraints(), 0.0);
         m_solved = false;
+        m_setup_current = false;
         return true;
     }
 
@@ -287,20 +345,21 @@ public:
         m_batch = nullptr;
         m_solved = false;
         m_persistent = false;
+        m_setup_current = false;
     }
 
     bool clearSolverVariables() {
         if (!m_batch) return false;
         // osqp cold start: zero iterates (a persistent workspace would otherwise resume from its own)
-        if (m_persistent) {
-            std::vector<double> x((size_t)m_data->numberOfVariables(), 0.0), y((size_t)m_data->numberOfConstraints(), 0.0);
-            return impc_batch_warm_start(m_batch, x.data(), y.data()) == IMPC_OK;
-        }
+        std::vector<double> x((size_t)m_data->numberOfVariables(), 0.0), y((size_t)m_data->numberOfConstraints(), 0.0);
+        if (m_persistent) return warm_start_raw(x, y);
+        m_wx = x;
+        m_wy = y;
         return impc_batch_warm_start(m_batch, nullptr, nullptr) == IMPC_OK;
     }
 
-    template <typename X, typename Y>
-    bool setWarmStart(const X &primalVariable, const Y &dualVariable) {
+    template <typename T, int n, int m>
+    bool setWarmStart(const Eigen::Matrix<T, n, 1> &primalVariable, const Eigen::Matrix<T, m, 1> &dualVariable) {
         if (!m_batch) { detail::debug("the solver is not initialized"); return false; }
         std::vector<double> x, y;
         if (!detail::copy_vec(primalVariable, m_data->numberOfVariables(), x) ||
@@ -308,16 +367,52 @@ public:
             detail::debug("warm start has the wrong size");
             return false;
         }
-        int rc = impc_batch_warm_start(m_batch, x.data(), y.data());
-        if (rc) { detail::debug_impc("impc_batch_warm_start", rc); return false; }
-        return true;
+        return warm_start_raw(x, y);
     }
 
-    template <typename X>
-    bool setPrimalVariable(const X &primalVariable) {
-        Eigen::Matrix<double, Eigen::Dynamic, 1> y;
-        y.setZero(m_data->numberOfConstraints());
-        return setWarmStart(primalVariable, y);
+    /* osqp_warm_start_x: x replaced, y kept */
+    template <typename T, int n>
+    bool setPrimalVariable(const Eigen::Matrix<T, n, 1> &primalVariable) {
+        if (!m_batch) { detail::debug("the solver is not initialized"); return false; }
+        std::vector<double> x;
+        if (!detail::copy_vec(primalVariable, m_data->numberOfVariables(), x)) {
+            detail::debug("the size of the primal variable vector has to be equal to the number of variables");
+            return false;
+        }
+        return warm_start_raw(x, m_wy);
+    }
+
+    /* osqp_warm_start_y: y replaced, x kept */
+    template <typename T, int m>
+    bool setDualVariable(const Eigen::Matrix<T, m, 1> &dualVariable) {
+        if (!m_batch) { detail::debug("the solver is not initialized"); return false; }
+        std::vector<double> y;
+        if (!detail::copy_vec(dualVariable, m_data->numberOfConstraints(), y)) {
+            detail::debug("the size of the dual variable vector has to be equal to the number of constraints");
+            return false;
+        }
+        return warm_start_raw(m_wx, y);
+    }
+
+    /* Returns the unscaled iterate the next solve starts from (OsqpEigen copies OSQP's scaled
+     * internal work->x / work->y here; no reference caller reads it). */
+    template <typename T, int n>
+    bool getPrimalVariable(Eigen::Matrix<T, n, 1> &primalVariable) {
+        if (!m_batch) { detail::debug("the solver is not initialized"); return false; }
+        const int64_t nv = m_data->numberOfVariables();
+        if (n == Eigen::Dynamic) primalVariable.resize(nv, 1);
+        else if (n != nv) { detail::debug("the size of the vector has to be equal to the number of variables"); return false; }
+        for (int64_t k = 0; k < nv; ++k) primalVariable((Eigen::Index)k) = (T)m_wx[(size_t)k];
+        return true;
+    }
+    template <typename T, int m>
+    bool getDualVariable(Eigen::Matrix<T, m, 1> &dualVariable) {
+        if (!m_batch) { detail::debug("the solver is not initialized"); return false; }
+        const int64_t mc = m_data->numberOfConstraints();
+        if (m == Eigen::Dynamic) dualVariable.resize(mc, 1);
+        else if (m != mc) { detail::debug("the size of the vector has to be equal to the number of constraints"); return false; }
+        for (int64_t k = 0; k < mc; ++k) dualVariable((Eigen::Index)k) = (T)m_wy[(size_t)k];
+        return true;
     }
 
     ErrorExitFlag solveProblem() {
@@ -332,9 +427,12 @@ public:
         std::vector<double> x((size_t)m_data->numberOfVariables()), y((size_t)m_data->numberOfConstraints());
         rc = impc_batch_get(m_batch, x.data(), y.data(), &m_info);
         if (rc) { detail::debug_impc("impc_batch_get", rc); return ErrorExitFlag::WorkspaceNotInitError; }
-        for (size_t k = 0; k < x.size(); ++k) m_x((int)k) = x[k];
-        for (size_t k = 0; k < y.size(); ++k) m_y((int)k) = y[k];
+        for (size_t k = 0; k < x.size(); ++k) m_x((Eigen::Index)k) = x[k];
+        for (size_t k = 0; k < y.size(); ++k) m_y((Eigen::Index)k) = y[k];
+        m_wx = x;
+        m_wy = y;
         m_solved = true;
+        m_setup_current = true;
         if (m_info.setup_exitflag == IMPC_NONCVX_ERROR) return ErrorExitFlag::NonCvxError;
         return ErrorExitFlag::NoError;
     }
@@ -348,32 +446,71 @@ public:
     double getObjValue() const { return m_info.obj_val; }
     int64_t getIterations() const { return m_info.iter; }
 
-    template <typename V>
-    bool updateGradient(const V &gradient) {
-        if (!m_batch) return false;
-        if (!detail::copy_vec(gradient, m_data->numberOfVariables(), m_data->q)) return false;
-        if (structured() && !(m_persistent && m_solved)) return resetup_from_data();
-        return impc_batch_update_lin_cost(m_batch, m_data->q.data()) == IMPC_OK;
+    /* osqp_update_lin_cost; before the workspace is set up (no solve yet, or after a re-setup)
+     * the new vector is taken by a fresh setup.  Data keeps the old vector if the update fails. */
+    bool updateGradient(const VecRef &gradient) {
+        if (!m_batch) { detail::debug("the solver has not been initialized"); return false; }
+        std::vector<double> q;
+        if (!detail::copy_vec(gradient, m_data->numberOfVariables(), q)) { detail::debug("the gradient has to be n x 1"); return false; }
+        if (!in_place()) {
+            std::vector<double> old = m_data->q;
+            m_data->q = q;
+            if (resetup_from_data()) return true;
+            m_data->q = old;
+            return false;
+        }
+        int rc = impc_batch_update_lin_cost(m_batch, q.data());
+        if (rc) { detail::debug_impc("impc_batch_update_lin_cost", rc); return false; }
+        m_data->q = q;
+        return true;
     }
-    template <typename L, typename U>
-    bool updateBounds(const L &lowerBound, const U &upperBound) {
-        if (!m_batch) return false;
+    /* osqp_update_bounds, with the same fallback */
+    bool updateBounds(const VecRef &lowerBound, const VecRef &upperBound) {
+        if (!m_batch) { detail::debug("the solver has not been initialized"); return false; }
         const int64_t m = m_data->numberOfConstraints();
-        if (!detail::copy_vec(lowerBound, m, m_data->l) || !detail::copy_vec(upperBound, m, m_data->u)) return false;
-        if (structured() && !(m_persistent && m_solved)) return resetup_from_data();
-        return impc_batch_update_bounds(m_batch, m_data->l.data(), m_data->u.data()) == IMPC_OK;
+        std::vector<double> l, u;
+        if (!detail::copy_vec(lowerBound, m, l) || !detail::copy_vec(upperBound, m, u)) {
+            detail::debug("the bounds have to be m x 1");
+            return false;
+        }
+        if (!in_place()) {
+            std::vector<double> ol = m_data->l, ou = m_data->u;
+            m_data->l = l;
+            m_data->u = u;
+            if (resetup_from_data()) return true;
+            m_data->l = ol;
+            m_data->u = ou;
+            return false;
+        }
+        int rc = impc_batch_update_bounds(m_batch, l.data(), u.data());
+        if (rc) { detail::debug_impc("impc_batch_update_bounds", rc); return false; }
+        m_data->l = l;
+        m_data->u = u;
+        return true;
     }
-    template <typename L>
-    bool updateLowerBound(const L &lowerBound) {
-        Eigen::Matrix<double, Eigen::Dynamic, 1> u((int)m_data->numberOfConstraints());
-        for (int64_t k = 0; k < m_data->numberOfConstraints(); ++k) u((int)k) = m_data->u[(size_t)k];
+    bool updateLowerBound(const VecRef &lowerBound) {
+        Eigen::Matrix<double, Eigen::Dynamic, 1> u((Eigen::Index)m_data->numberOfConstraints());
+        for (int64_t k = 0; k < m_data->numberOfConstraints(); ++k) u((Eigen::Index)k) = m_data->u[(size_t)k];
         return updateBounds(lowerBound, u);
     }
-    template <typename U>
-    bool updateUpperBound(const U &upperBound) {
-        Eigen::Matrix<double, Eigen::Dynamic, 1> l((int)m_data->numberOfConstraints());
-        for (int64_t k = 0; k < m_data->numberOfConstraints(); ++k) l((int)k) = m_data->l[(size_t)k];
+    bool updateUpperBound(const VecRef &upperBound) {
+        Eigen::Matrix<double, Eigen::Dynamic, 1> l((Eigen::Index)m_data->numberOfConstraints());
+        for (int64_t k = 0; k < m_data->numberOfConstraints(); ++k) l((Eigen::Index)k) = m_data->l[(size_t)k];
         return updateBounds(l, upperBound);
+    }
+
+    /* Solver.tpp:15-113 / :116-212.  Same pattern: the new values are set up afresh and the solve
+     * resumes from the last solution (OSQP's osqp_update_P / _A re-scale and refactor but keep the
+     * scaled iterates; here the unscaled iterate is carried into the new scaling instead -- the same
+     * fixed point, a different first iteration).  New pattern: a new batch, warm-started, as
+     * OsqpEigen re-initialises its solver.  No reference caller updates P or A. */
+    template <typename Derived>
+    bool updateHessianMatrix(const Eigen::SparseCompressedBase<Derived> &hessianMatrix) {
+        return update_matrix(hessianMatrix, true);
+    }
+    template <typename Derived>
+    bool updateLinearConstraintsMatrix(const Eigen::SparseCompressedBase<Derived> &linearConstraintsMatrix) {
+        return update_matrix(linearConstraintsMatrix, false);
     }
 };
 

@@ -46,7 +46,8 @@ struct DevSym {
 };
 
 // Per-QP scalar slots (interleaved like every other array).
-enum : int32_t { SC_C = 0, SC_CINV, SC_RHO, SC_SETUP_ERR, SC_NSCAL };
+// SC_T0: device clock at the start of osqp_setup (a first solve's time limit counts setup time)
+enum : int32_t { SC_C = 0, SC_CINV, SC_RHO, SC_SETUP_ERR, SC_T0, SC_NSCAL };
 
 // Batch-interleaved per-QP arrays.
 struct DevWork {
@@ -527,8 +528,10 @@ IMPC_HD uint64_t device_clock_100mhz() {
 // ---------------------------------------------------------------------------- osqp_solve
 // Runs the ADMM loop from the current iterates, sets the info record and the interleaved
 // unscaled outputs xo / yo (store_solution + unscale_solution).
+// first_run: the first solve after qp_setup -- as OSQP 0.6.2's osqp_solve, its time limit counts
+// setup_time + the solve's own time (later solves: the solve's own time)
 IMPC_HD void qp_solve(const DevSym &sy, const DevWork &wk, const DevSettings &st, int lane, int64_t qp_index,
-                      int64_t rho_updates0) {
+                      int64_t rho_updates0, int first_run = 0) {
     const int64_t S = wk.S;
     const int32_t n = sy.n, m = sy.m;
     impc_info &out = wk.info[qp_index];
@@ -563,7 +566,7 @@ IMPC_HD void qp_solve(const DevSym &sy, const DevWork &wk, const DevSettings &st
     }
     const double alpha = st.alpha, oma = (double)1.0 - st.alpha, sigma = st.sigma;
     const int32_t chk = st.check_termination;
-    const uint64_t t0 = device_clock_100mhz();
+    const uint64_t t0 = first_run ? (uint64_t)IMPC_AT(wk.scal, SC_T0) : device_clock_100mhz();
     int can_check = 0;
     int64_t iter;
     for (iter = 1; iter <= st.max_iter; iter++) {

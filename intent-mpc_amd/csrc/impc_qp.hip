@@ -24,6 +24,7 @@
 #include "../../include/impc_mpc.h"
 #include "../../include/impc_fanout.h"
 #include "../../include/impc_predict.h"
+#include "../../include/impc_comm.h"
 #include "mpc_qp_internal.hpp"
 #include "admm_core.hpp"
 #include "mpc_structure.hpp"
@@ -106,14 +107,17 @@ __global__ __launch_bounds__(kBlock) void k_setup(impc::DevSym sy, impc::DevWork
                                                   int has_ws) {
     const int lane = blockIdx.x * kBlock + threadIdx.x;
     if (lane >= B) return;
+    const int64_t S = wk.S;
+    IMPC_AT(wk.scal, impc::SC_T0) = (double)impc::device_clock_100mhz();  // setup_time starts here
     impc::qp_setup(sy, wk, st, lane, has_ws);
 }
 
+// first_run: the first solve after k_setup (its time limit counts the setup time, OSQP 0.6.2)
 __global__ __launch_bounds__(kBlock) void k_solve(impc::DevSym sy, impc::DevWork wk, impc::DevSettings st,
-                                                  int64_t B) {
+                                                  int64_t B, int first_run) {
     const int lane = blockIdx.x * kBlock + threadIdx.x;
     if (lane >= B) return;
-    impc::qp_solve(sy, wk, st, lane, lane, 0);
+    impc::qp_solve(sy, wk, st, lane, lane, 0, first_run);
 }
 
 // osqp_warm_start (osqp.h:157) on a set-up workspace: scaling, rho and factor stay
@@ -391,6 +395,10 @@ struct impc_ctx_s {
     GroupEntry *d_group = nullptr;
     int group_cap = 0;
     std::vector<GroupEntry> h_group;
+    // caller-stream bookkeeping (ctx_order_launch / ctx_note_launch / ctx_quiesce)
+    hipEvent_t ev_order = nullptr;
+    std::vector<hipEvent_t> ev_pool, ev_pending;
+    std::vector<hipEvent_t> timer_marks;  // impc_ctx_timer_mark
 };
 
 // Every host->device transfer and fill below goes through the context's stream and has finished
@@ -414,6 +422,50 @@ static int fill0_sync(hipStream_t st, void *dst, size_t bytes) {
         int rc_ = (expr);       \
         if (rc_) return rc_;    \
     } while (0)
+
+// Caller streams (impc_batch_setup / _solve / _solve_group accept one) are ordered against the
+// context's own stream in both directions: a launch on a caller stream first waits for what is
+// already queued on the context stream (device-to-device value copies, in-place updates and warm
+// starts), and every entry point that rewrites batch inputs, workspaces or the group-entry table
+// first waits for every launch issued on a caller stream (an event recorded after each one), so
+// no kernel in flight on another stream reads half-replaced data.
+static int ctx_order_launch(impc_ctx ctx, hipStream_t st) {
+    if (st == ctx->stream) return IMPC_OK;
+    if (!ctx->ev_order) HIP_OK(hipEventCreateWithFlags(&ctx->ev_order, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(ctx->ev_order, ctx->stream));
+    HIP_OK(hipStreamWaitEvent(st, ctx->ev_order, 0));
+    return IMPC_OK;
+}
+static int ctx_note_launch(impc_ctx ctx, hipStream_t st) {
+    if (st == ctx->stream) return IMPC_OK;
+    // recycle the events of launches that have completed (keeps the pending list short)
+    for (size_t k = 0; k < ctx->ev_pending.size();) {
+        if (hipEventQuery(ctx->ev_pending[k]) == hipSuccess) {
+            ctx->ev_pool.push_back(ctx->ev_pending[k]);
+            ctx->ev_pending[k] = ctx->ev_pending.back();
+            ctx->ev_pending.pop_back();
+        } else {
+            k++;
+        }
+    }
+    hipEvent_t e = nullptr;
+    if (!ctx->ev_pool.empty()) {
+        e = ctx->ev_pool.back();
+        ctx->ev_pool.pop_back();
+    } else {
+        HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    HIP_OK(hipEventRecord(e, st));
+    ctx->ev_pending.push_back(e);
+    return IMPC_OK;
+}
+static int ctx_quiesce(impc_ctx ctx) {
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    for (hipEvent_t e : ctx->ev_pending) HIP_OK(hipEventSynchronize(e));
+    ctx->ev_pool.insert(ctx->ev_pool.end(), ctx->ev_pending.begin(), ctx->ev_pending.end());
+    ctx->ev_pending.clear();
+    return IMPC_OK;
+}
 
 struct impc_batch_s {
     impc_ctx ctx = nullptr;
@@ -457,7 +509,7 @@ struct impc_batch_s {
     double *d_work = nullptr;
     impc::DevSym dsym{};
     impc::DevWork dwk{};
-    bool generic_dirty = true, generic_setup_done = false;
+    bool generic_dirty = true, generic_setup_done = false, generic_first_run = false;
     // profiling
     bool profile = false;
     hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -671,6 +723,7 @@ int generic_setup(impc_batch b, hipStream_t st) {
     }
     b->generic_dirty = false;
     b->generic_setup_done = true;
+    b->generic_first_run = true;
     return IMPC_OK;
 }
 
@@ -680,8 +733,11 @@ int generic_solve(impc_batch b, hipStream_t st) {
         int rc = generic_setup(b, st);
         if (rc) return rc;
     }
+    const int first_run = b->generic_first_run ? 1 : 0;
+    b->generic_first_run = false;
     if (b->profile) HIP_OK(hipEventRecord(b->ev[2], st));
-    hipLaunchKernelGGL(k_solve, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk, b->dst, b->B);
+    hipLaunchKernelGGL(k_solve, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk, b->dst, b->B,
+                       first_run);
     HIP_OK(hipGetLastError());
     if (b->profile) HIP_OK(hipEventRecord(b->ev[3], st));
     int rc = deinterleave(b, b->dwk.xo, b->d_xout, b->n, st);
@@ -916,8 +972,13 @@ int impc_ctx_create(int device, impc_ctx *out) {
 int impc_ctx_destroy(impc_ctx ctx) {
     if (!ctx) return IMPC_OK;
     (void)hipSetDevice(ctx->device);
+    (void)ctx_quiesce(ctx);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->d_group) (void)hipFree(ctx->d_group);
+    for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ctx->ev_pending) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ctx->timer_marks) (void)hipEventDestroy(e);
+    if (ctx->ev_order) (void)hipEventDestroy(ctx->ev_order);
     delete ctx;
     return IMPC_OK;
 }
@@ -993,7 +1054,7 @@ int impc_batch_destroy(impc_batch b) {
     if (!b) return IMPC_OK;
     if (b->ctx) {
         (void)hipSetDevice(b->ctx->device);
-        (void)hipStreamSynchronize(b->ctx->stream);
+        (void)ctx_quiesce(b->ctx);
     }
     for (hipEvent_t e : b->ev)
         if (e) (void)hipEventDestroy(e);
@@ -1045,6 +1106,7 @@ int impc_batch_set_values(impc_batch b, const double *Px, const double *q, const
             return fail(IMPC_DATA_VALIDATION_ERROR, msg);
         }
     HIP_OK(hipSetDevice(b->ctx->device));
+    IMPC_TRY(ctx_quiesce(b->ctx));  // no solve in flight on any stream reads the arrays replaced below
     const size_t B = (size_t)b->B;
     IMPC_TRY(h2d_sync(b->ctx->stream, b->in_Px, Px, sizeof(double) * b->nnzP * B));
     IMPC_TRY(h2d_sync(b->ctx->stream, b->in_q, q, sizeof(double) * b->n * B));
@@ -1082,7 +1144,7 @@ int impc_batch_set_values_shared(impc_batch b, const double *Px, const double *A
         }
     HIP_OK(hipSetDevice(b->ctx->device));
     hipStream_t st = b->ctx->stream;
-    HIP_OK(hipStreamSynchronize(st));  // no solve in flight reads the arrays replaced below
+    IMPC_TRY(ctx_quiesce(b->ctx));  // no solve in flight on any stream reads the arrays replaced below
     if (!b->d_shPx) {
         HIP_OK(hipMalloc((void **)&b->d_shPx, sizeof(double) * std::max<int64_t>(b->nnzP, 1)));
         HIP_OK(hipMalloc((void **)&b->d_shAx, sizeof(double) * std::max<int64_t>(b->nnzA, 1)));
@@ -1119,6 +1181,7 @@ int impc_batch_set_values_device(impc_batch b, const double *Px, const double *q
     if ((b->nnzP && !Px) || !q || (b->nnzA && !Ax) || (b->m && (!l || !u)))
         return fail(IMPC_INVALID_ARGUMENT, "null value array");
     HIP_OK(hipSetDevice(b->ctx->device));
+    IMPC_TRY(ctx_quiesce(b->ctx));  // the copies below are ordered on the context stream only
     hipStream_t st = b->ctx->stream;
     const size_t B = (size_t)b->B;
     if (b->nnzP) HIP_OK(hipMemcpyAsync(b->in_Px, Px, sizeof(double) * b->nnzP * B, hipMemcpyDeviceToDevice, st));
@@ -1138,6 +1201,7 @@ int impc_batch_set_values_device(impc_batch b, const double *Px, const double *q
 int impc_batch_warm_start(impc_batch b, const double *x, const double *y) {
     if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
     HIP_OK(hipSetDevice(b->ctx->device));
+    IMPC_TRY(ctx_quiesce(b->ctx));
     if (!x) {
         b->has_ws = false;
         b->generic_dirty = true;
@@ -1175,7 +1239,10 @@ int impc_batch_setup(impc_batch b, void *stream) {
     if (!b->values_set) return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "values not set");
     HIP_OK(hipSetDevice(b->ctx->device));
     if (use_structured(b)) return IMPC_OK;  // the wave kernel runs setup and solve per QP in one launch
-    return generic_setup(b, pick(b, stream));
+    hipStream_t st = pick(b, stream);
+    IMPC_TRY(ctx_order_launch(b->ctx, st));
+    IMPC_TRY(generic_setup(b, st));
+    return ctx_note_launch(b->ctx, st);
 }
 
 int impc_batch_solve(impc_batch b, void *stream) {
@@ -1183,8 +1250,9 @@ int impc_batch_solve(impc_batch b, void *stream) {
     if (!b->values_set) return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "values not set");
     HIP_OK(hipSetDevice(b->ctx->device));
     hipStream_t st = pick(b, stream);
-    if (use_structured(b)) return structured_solve(b, st);
-    return generic_solve(b, st);
+    IMPC_TRY(ctx_order_launch(b->ctx, st));
+    IMPC_TRY(use_structured(b) ? structured_solve(b, st) : generic_solve(b, st));
+    return ctx_note_launch(b->ctx, st);
 }
 
 int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
@@ -1224,20 +1292,22 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
     }
     if (total == 0) return IMPC_OK;
     // upload the entries only when they change (repeated solves of one group launch back to back);
-    // the device copy must not change under an in-flight kernel, so an update waits for the stream
+    // the device copy must not change under an in-flight kernel, so an update first waits for every
+    // launch on every stream this context has used
     const bool same = ctx->h_group.size() == entries.size() &&
                       std::memcmp(ctx->h_group.data(), entries.data(), sizeof(GroupEntry) * (size_t)count) == 0;
     if (!same) {
-        HIP_OK(hipStreamSynchronize(st));
+        IMPC_TRY(ctx_quiesce(ctx));
         if (count > ctx->group_cap) {
             if (ctx->d_group) HIP_OK(hipFree(ctx->d_group));
             ctx->d_group = nullptr;
             HIP_OK(hipMalloc((void **)&ctx->d_group, sizeof(GroupEntry) * (size_t)count));
             ctx->group_cap = count;
         }
-        IMPC_TRY(h2d_sync(st, ctx->d_group, entries.data(), sizeof(GroupEntry) * (size_t)count));
+        IMPC_TRY(h2d_sync(ctx->stream, ctx->d_group, entries.data(), sizeof(GroupEntry) * (size_t)count));
         ctx->h_group = entries;
     }
+    IMPC_TRY(ctx_order_launch(ctx, st));
     HIP_OK(hipMemsetAsync(b0->d_counter, 0, 256, st));
     if (b0->profile) HIP_OK(hipEventRecord(b0->ev[2], st));
     int rc;
@@ -1251,6 +1321,7 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
         default: return fail(IMPC_UNSUPPORTED, "no structured kernel for this size");
     }
     if (rc) return rc;
+    IMPC_TRY(ctx_note_launch(ctx, st));
     for (int k = 0; k < count; k++) structured_solved(bs[k]);
     if (b0->profile) {
         HIP_OK(hipEventRecord(b0->ev[3], st));
@@ -1294,6 +1365,7 @@ int impc_batch_update_lin_cost(impc_batch b, const double *q) {
             return fail(IMPC_WORKSPACE_NOT_INIT_ERROR,
                         "structured kernel: impc_batch_set_persistent(b, 1) and one solve before updates");
         HIP_OK(hipSetDevice(b->ctx->device));
+        IMPC_TRY(ctx_quiesce(b->ctx));
         IMPC_TRY(h2d_sync(b->ctx->stream, b->in_q, q, sizeof(double) * b->n * b->B));
         b->q_by_update = true;
         b->generic_dirty = true;
@@ -1301,6 +1373,8 @@ int impc_batch_update_lin_cost(impc_batch b, const double *q) {
     }
     if (!b->generic_setup_done || b->generic_dirty)
         return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "setup has not run on current data");
+    HIP_OK(hipSetDevice(b->ctx->device));
+    IMPC_TRY(ctx_quiesce(b->ctx));
     int rc = upload_interleaved(b, q, b->in_q, const_cast<double *>(b->dwk.q), b->n);
     if (rc) return rc;
     hipLaunchKernelGGL(k_update_q, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, b->ctx->stream, b->dsym, b->dwk,
@@ -1318,6 +1392,7 @@ int impc_batch_update_bounds(impc_batch b, const double *l, const double *u) {
         for (int64_t k = 0; k < b->m * b->B; k++)
             if (l[k] > u[k]) return fail(IMPC_DATA_VALIDATION_ERROR, "lower bound greater than upper bound");
         HIP_OK(hipSetDevice(b->ctx->device));
+        IMPC_TRY(ctx_quiesce(b->ctx));
         if (b->m) {
             IMPC_TRY(h2d_sync(b->ctx->stream, b->in_l, l, sizeof(double) * b->m * b->B));
             IMPC_TRY(h2d_sync(b->ctx->stream, b->in_u, u, sizeof(double) * b->m * b->B));
@@ -1329,6 +1404,8 @@ int impc_batch_update_bounds(impc_batch b, const double *l, const double *u) {
         return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "setup has not run on current data");
     for (int64_t k = 0; k < b->m * b->B; k++)
         if (l[k] > u[k]) return fail(IMPC_DATA_VALIDATION_ERROR, "lower bound greater than upper bound");
+    HIP_OK(hipSetDevice(b->ctx->device));
+    IMPC_TRY(ctx_quiesce(b->ctx));
     int rc = upload_interleaved(b, l, b->in_l, const_cast<double *>(b->dwk.l), b->m);
     if (!rc) rc = upload_interleaved(b, u, b->in_u, const_cast<double *>(b->dwk.u), b->m);
     if (rc) return rc;
@@ -1392,7 +1469,7 @@ int impc_batch_get_qp_latency(impc_batch b, double *ms) {
     if (!b || !ms) return fail(IMPC_INVALID_ARGUMENT, "null batch or output");
     if (!b->qpt_valid) return fail(IMPC_INVALID_ARGUMENT, "no profiled structured-kernel solve");
     HIP_OK(hipSetDevice(b->ctx->device));
-    HIP_OK(hipStreamSynchronize(b->ctx->stream));
+    IMPC_TRY(ctx_quiesce(b->ctx));
     std::vector<unsigned long long> t((size_t)b->B * 2);
     HIP_OK(hipMemcpy(t.data(), b->d_qpt, sizeof(unsigned long long) * t.size(), hipMemcpyDeviceToHost));
     for (int64_t k = 0; k < b->B; k++) ms[k] = (double)(t[2 * k + 1] - t[2 * k]) * 1e-5;  // 100 MHz ticks
@@ -1471,14 +1548,14 @@ int impc_device_free(impc_ctx ctx, void *ptr) {
 int impc_copy_to_device(impc_ctx ctx, void *dst, const void *src, int64_t bytes) {
     if (!ctx || (bytes > 0 && (!dst || !src)) || bytes < 0) return fail(IMPC_INVALID_ARGUMENT, "invalid argument");
     HIP_OK(hipSetDevice(ctx->device));
-    HIP_OK(hipStreamSynchronize(ctx->stream));
+    IMPC_TRY(ctx_quiesce(ctx));
     IMPC_TRY(h2d_sync(ctx->stream, dst, src, (size_t)bytes));
     return IMPC_OK;
 }
 int impc_copy_to_host(impc_ctx ctx, void *dst, const void *src, int64_t bytes) {
     if (!ctx || (bytes > 0 && (!dst || !src)) || bytes < 0) return fail(IMPC_INVALID_ARGUMENT, "invalid argument");
     HIP_OK(hipSetDevice(ctx->device));
-    HIP_OK(hipStreamSynchronize(ctx->stream));
+    IMPC_TRY(ctx_quiesce(ctx));
     if (bytes) HIP_OK(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyDeviceToHost));
     return IMPC_OK;
 }
@@ -1494,3 +1571,6 @@ int impc_copy_to_host(impc_ctx ctx, void *dst, const void *src, int64_t bytes) {
 
 // ---------------------------------------------------------------- on-device MPC -> QP assembly
 #include "mpc_build.hpp"
+
+// ---------------------------------------------------------------- RCCL communicator, step timer
+#include "comm.hpp"

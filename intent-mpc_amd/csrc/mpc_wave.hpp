@@ -1385,6 +1385,9 @@ struct WaveQP {
     IMPC_WF void solve(int64_t b) {
         const int n = T.n, m = T.m;
         const uint64_t t_begin = io.qpt ? device_clock_100mhz() : 0;
+        // time_limit clock: from the start of the QP's setup (load, scaling, factorisation), as
+        // OSQP 0.6.2 counts setup_time + solve time on a first run (every solveTraj call is one)
+        const uint64_t t0 = device_clock_100mhz();
         rw = (int)(b % (NL / 64));  // spread the serial recursions of co-resident QPs over SIMDs
         IMPC_SEC_START();
         clear_exchange();
@@ -1482,7 +1485,6 @@ struct WaveQP {
         int64_t info_iter = 0;
         const int chk = st.check_termination;
         int can_check = 0;
-        const uint64_t t0 = device_clock_100mhz();
         // countdowns instead of iter % interval (no integer division in the loop)
         int32_t chk_left = chk, rho_left = st.rho_interval;
         for (iter = 1; iter <= st.max_iter; iter++) {

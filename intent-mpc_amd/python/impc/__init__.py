@@ -121,6 +121,16 @@ _sig("impc_device_alloc", C.c_int, _P, C.c_int64, C.POINTER(_P))
 _sig("impc_device_free", C.c_int, _P, _P)
 _sig("impc_copy_to_device", C.c_int, _P, _P, _P, C.c_int64)
 _sig("impc_copy_to_host", C.c_int, _P, _P, _P, C.c_int64)
+# include/impc_comm.h
+COMM_ID_BYTES = 128
+_sig("impc_comm_unique_id", C.c_int, C.POINTER(C.c_ubyte))
+_sig("impc_comm_create", C.c_int, _P, C.POINTER(C.c_ubyte), C.c_int, C.c_int, C.POINTER(_P))
+_sig("impc_comm_destroy", C.c_int, _P)
+_sig("impc_comm_allgather", C.c_int, _P, _P, _P, C.c_int64, _P)
+_sig("impc_comm_gather_info", C.c_int, _P, C.POINTER(_P), C.c_int, C.c_int64, _P, _P)
+_sig("impc_comm_max", C.c_int, _P, C.POINTER(C.c_double))
+_sig("impc_ctx_timer_mark", C.c_int, _P, _P)
+_sig("impc_ctx_timer_read", C.c_int, _P, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_int64))
 
 
 class SelectParams(C.Structure):
@@ -202,6 +212,8 @@ EXPORTED = [
     "impc_fanout_candidates_device", "impc_intent_params_from_config", "impc_intent_prob", "impc_intent_prob_device",
     "impc_predict_traj", "impc_predict_traj_device", "impc_minsnap_dims", "impc_minsnap_build_pattern",
     "impc_minsnap_build_values", "impc_minsnap_build_bounds", "impc_minsnap_unscale",
+    "impc_comm_unique_id", "impc_comm_create", "impc_comm_destroy", "impc_comm_allgather", "impc_comm_gather_info",
+    "impc_comm_max", "impc_ctx_timer_mark", "impc_ctx_timer_read",
 ]
 
 
@@ -245,6 +257,17 @@ class Context:
 
     def synchronize(self):
         _check(lib.impc_ctx_synchronize(self.h), "impc_ctx_synchronize")
+
+    def timer_mark(self, stream=None):
+        """impc_ctx_timer_mark: a HIP event on the launch stream (context stream if None)."""
+        _check(lib.impc_ctx_timer_mark(self.h, _P(stream) if stream else None), "impc_ctx_timer_mark")
+
+    def timer_read(self, max_pairs=4096):
+        """impc_ctx_timer_read: ms between marks 2k and 2k+1 (synchronises, clears the marks)."""
+        ms = np.zeros(max_pairs)
+        n = C.c_int64()
+        _check(lib.impc_ctx_timer_read(self.h, ms.ctypes.data_as(_dp), max_pairs, C.byref(n)), "impc_ctx_timer_read")
+        return ms[: n.value]
 
     def close(self):
         if self.h:
@@ -299,6 +322,11 @@ class Batch:
     def warm_start(self, x=None, y=None):
         xa = None if x is None else np.ascontiguousarray(x, dtype=np.float64)
         ya = None if y is None else np.ascontiguousarray(y, dtype=np.float64)
+        # the C side copies B*n / B*m doubles from these pointers: shapes are checked here
+        if xa is not None and xa.size != self.B * self.n:
+            raise ValueError(f"warm_start: x has {xa.size} values, expected B*n = {self.B * self.n}")
+        if ya is not None and ya.size != self.B * self.m:
+            raise ValueError(f"warm_start: y has {ya.size} values, expected B*m = {self.B * self.m}")
         _check(lib.impc_batch_warm_start(self.h, _d(xa), _d(ya)), "impc_batch_warm_start")
 
     def setup(self, stream=None):
@@ -331,11 +359,16 @@ class Batch:
 
     def update_lin_cost(self, q):
         qa = np.ascontiguousarray(q, dtype=np.float64)
+        if qa.size != self.B * self.n:
+            raise ValueError(f"update_lin_cost: q has {qa.size} values, expected B*n = {self.B * self.n}")
         _check(lib.impc_batch_update_lin_cost(self.h, _d(qa)), "impc_batch_update_lin_cost")
 
     def update_bounds(self, l, u):
         la = np.ascontiguousarray(l, dtype=np.float64)
         ua = np.ascontiguousarray(u, dtype=np.float64)
+        if la.size != self.B * self.m or ua.size != self.B * self.m:
+            raise ValueError(f"update_bounds: l / u have {la.size} / {ua.size} values, expected B*m = "
+                             f"{self.B * self.m}")
         _check(lib.impc_batch_update_bounds(self.h, _d(la), _d(ua)), "impc_batch_update_bounds")
 
     def stats(self):
@@ -538,6 +571,52 @@ class DeviceArray:
         if self.ptr:
             lib.impc_device_free(self.ctx.h, _P(self.ptr))
             self.ptr = None
+
+
+def comm_unique_id():
+    """impc_comm_unique_id (ncclGetUniqueId): 128 bytes for rank 0 to hand to every rank."""
+    buf = (C.c_ubyte * COMM_ID_BYTES)()
+    _check(lib.impc_comm_unique_id(buf), "impc_comm_unique_id")
+    return bytes(buf)
+
+
+class Comm:
+    """RCCL communicator on a context's device (include/impc_comm.h): the cost-record all-gather of
+    the multi-GPU path."""
+
+    def __init__(self, ctx, uid, rank, world):
+        self.ctx, self.rank, self.world = ctx, int(rank), int(world)
+        buf = (C.c_ubyte * COMM_ID_BYTES).from_buffer_copy(bytes(uid))
+        h = _P()
+        _check(lib.impc_comm_create(ctx.h, buf, self.rank, self.world, C.byref(h)), "impc_comm_create")
+        self.h = h
+
+    def gather_info(self, batches, max_qps, recv_ptr, stream=None):
+        """impc_comm_gather_info: this rank's batches' impc_info records, packed to max_qps and
+        all-gathered into recv_ptr (device, world * max_qps records), on `stream`."""
+        arr = (_P * len(batches))(*[b.h for b in batches])
+        _check(lib.impc_comm_gather_info(self.h, arr, len(batches), int(max_qps), _P(recv_ptr),
+                                         _P(stream) if stream else None), "impc_comm_gather_info")
+
+    def allgather(self, send_ptr, recv_ptr, nbytes, stream=None):
+        _check(lib.impc_comm_allgather(self.h, _P(send_ptr), _P(recv_ptr), int(nbytes), _P(stream) if stream else None),
+               "impc_comm_allgather")
+
+    def max(self, v):
+        d = C.c_double(float(v))
+        _check(lib.impc_comm_max(self.h, C.byref(d)), "impc_comm_max")
+        return d.value
+
+    def close(self):
+        if self.h:
+            lib.impc_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def solve_group(batches, stream=None):

@@ -24,9 +24,16 @@ def _x0(rng, nb):
     return pos, vel
 
 
-def _xref(rng, pos, N):
+# Reference-path spacing per 0.1 s step: U(0.5, 2.5) m, i.e. 5-25 m/s -- the live
+# benchmark path's raw points are 2.5 m apart and getReferenceTraj (mpcPlanner.cpp:1199-1231)
+# samples them one per step, so most of this range is faster than vmax = 5 m/s and the QPs track a
+# reference they cannot reach (iteration counts against the spacing).
+STEP_RANGE = (0.5, 2.5)
+
+
+def _xref(rng, pos, N, step_range=STEP_RANGE):
     nb = pos.shape[0]
-    step = rng.uniform(0.5, 2.5, nb)  # m per 0.1 s step (ref_trajectory_dynus_benchmark.txt spacing)
+    step = rng.uniform(step_range[0], step_range[1], nb)  # m per 0.1 s step
     xr = np.zeros((nb, N, 8))
     k = np.arange(N)
     xr[:, :, 0] = pos[:, None, 0] + k[None, :] * step[:, None]
@@ -87,7 +94,7 @@ def predict_intents(p0, v0, steps=PRED_STEPS, ts=0.1, omega=0.6, stop_time=1.0):
     return out
 
 
-def intent_config(N=20, K=8, instances=8192, hyps=8, seed=3000, params=None):
+def intent_config(N=20, K=8, instances=8192, hyps=8, seed=3000, params=None, step_range=STEP_RANGE):
     """Config 3: `instances` planning instances x `hyps` hypotheses, K dynamic obstacles each.
 
     Hypotheses 0-5 are mpcPlanner::getIntentComb's six combinations for the closest obstacle
@@ -101,7 +108,7 @@ def intent_config(N=20, K=8, instances=8192, hyps=8, seed=3000, params=None):
     ts = pd["ts"]
     I = instances
     pos, vel = _x0(rng, I)
-    xref = _xref(rng, pos, N)
+    xref = _xref(rng, pos, N, step_range)
     prev = _prev_plan(pos, vel, N, ts)
     obp = np.stack([pos[:, None, 0] + rng.uniform(3, 15, (I, K)), rng.uniform(-4, 4, (I, K)),
                     rng.uniform(1.0, 3.0, (I, K))], axis=2)
@@ -178,12 +185,12 @@ def intent_config(N=20, K=8, instances=8192, hyps=8, seed=3000, params=None):
     return out
 
 
-def first_call_config(N=20, batch=1, seed=1000, params=None):
+def first_call_config(N=20, batch=1, seed=1000, params=None, step_range=STEP_RANGE):
     """Config 1: the first makePlan() QP -- no obstacles, cold start (mpcPlanner.cpp:543-569)."""
     p, pd = params if params is not None else mpc_params(horizon=N)
     rng = np.random.default_rng(seed)
     pos, vel = _x0(rng, batch)
-    xref = _xref(rng, pos, N)
+    xref = _xref(rng, pos, N, step_range)
     pat = mpc_pattern(p, 0, 0)
     vals = mpc_values(p, pos, vel, xref, None)
     return dict(pattern=pat, values=vals, x_ws=None, params=pd, K=0, N=N)
@@ -216,3 +223,59 @@ def selection_arrays(buckets, ptr_by_bucket, C=6):
         rows[K] = (i, h, r)
     return dict(I=I, N=N, C=C, kmax=kmax, L=L, x_ptrs=x_ptrs, dyn_pos=dyn_pos, dyn_size=dyn_size,
                 dyn_count=dyn_count, prev=inst["prev"], xref=inst["xref"], prob=inst["prob"], rows=rows)
+
+
+# ---------------------------------------------------------------- config 4 (mixed K, sharded)
+def config4_plan(total_qps=262144, hyps=8, kmax=20, N=20, seed=4000):
+    """BASELINE.json configs[3]: total_qps QPs = total_qps / hyps planning instances, each with
+    K ~ U{0..kmax} predicted dynamic obstacles and `hyps` intent hypotheses (two of them carry K + 1
+    obstacle rows, as getIntentComb's two-intent candidates; K = 0 instances have no obstacle to
+    branch on and solve `hyps` obstacle-free QPs).  Returns (K per instance, weight per instance):
+    the weight is the instance's summed constraint count Sigma m, the shard-balancing measure."""
+    I = total_qps // hyps
+    K = np.random.default_rng(seed).integers(0, kmax + 1, I)
+    m = lambda k: 21 * N - 5 + k * (N - 1)
+    w = np.where(K > 0, (hyps - 2) * m(K) + 2 * m(K + 1), hyps * m(0))
+    return K, w
+
+
+def config4_rank(lo, hi, K, hyps=8, N=20, seed=4000, params=None):
+    """The QP buckets of planning instances [lo, hi) of a config4_plan (one rank's shard).  Each
+    bucket is one (generating K, obstacle count) pair -- pattern, values, warm start, and the
+    GLOBAL instance index + hypothesis of every QP.  Seeds depend on the instance range only, so a
+    shard's QPs are the same whatever process generates them."""
+    out = []
+    Ks = np.asarray(K)[lo:hi]
+    for k in np.unique(Ks):
+        idx = lo + np.nonzero(Ks == k)[0]                    # global instance ids with this K
+        sd = seed + 101 * int(k) + 7919 * int(lo)
+        if k == 0:
+            c = first_call_config(N=N, batch=hyps * idx.size, seed=sd, params=params)
+            c.update(inst=np.repeat(idx, hyps), hyp=np.tile(np.arange(hyps), idx.size))
+            out.append(c)
+            continue
+        for kk, bk in sorted(intent_config(N=N, K=int(k), instances=idx.size, hyps=hyps, seed=sd,
+                                           params=params).items()):
+            bk = dict(bk)
+            bk["inst"] = idx[bk["inst"]]
+            out.append(bk)
+    return out
+
+
+def receding_update(bk, shift=1, params=None):
+    """Config 5's receding window (BASELINE.json configs[4]) for a bucket of intent_config: the next
+    replan's QP values -- xRef shifted by `shift` steps along the path (extended at its last
+    spacing) and x0 moved to the previous plan's state `shift` -- with the same linearisation
+    points (the previous plan), so P and A are unchanged and the step is a legal
+    osqp_update_lin_cost (q) + osqp_update_bounds (l, u) on a persistent workspace
+    (polyTrajSolver.cpp:225-237's pattern, OsqpEigen Solver.hpp:151-182)."""
+    N = bk["N"]
+    inst = bk["inst"]
+    d = bk["instances"]
+    xref, prev = d["xref"][inst], d["prev"][inst]
+    step = xref[:, -1, :] - xref[:, -2, :]
+    ext = xref[:, -1:, :] + step[:, None, :] * np.arange(1, shift + 1)[None, :, None]
+    xr2 = np.concatenate([xref[:, shift:], ext], axis=1)
+    p, _ = params if params is not None else mpc_params(horizon=N)
+    return mpc_values(p, prev[:, shift, 0:3], prev[:, shift, 3:6], xr2, prev, dyn_pos=bk["dyn_pos"],
+                      dyn_size=bk["dyn_size"])

@@ -10,12 +10,20 @@ Follows, entry by entry and in the reference's insertion order:
   constructA                     :314-585  (corridor rows :559-585 not restated)
   constructBound                 :587-847  (corridor rows not restated)
   solveX/Y/Z                     :870-905  (coefficient rescaling)
-Values use math.pow / math.sqrt (the same libm calls as the reference's pow / sqrt).
+Values use math.pow / math.sqrt (the same libm calls as the reference's pow / sqrt), except pow(x, 2), which
+GCC folds to x * x in the reference build (_sq).
 """
 import math
 
 import numpy as np
 
+
+
+def _sq(v):
+    """pow(v, 2) of the reference C++: GCC folds pow(x, 2.0) to x * x at every optimisation level
+    (no -ffast-math needed), so the reference binary squares by one correctly rounded multiply --
+    libm's pow (math.pow) can differ from it by an ulp."""
+    return v * v
 
 def time_allocation(path, desired_vel):
     """avgTimeAllocation :125-138."""
@@ -23,7 +31,7 @@ def time_allocation(path, desired_vel):
     total = 0.0
     for i in range(1, len(path)):
         a, b = path[i], path[i - 1]
-        dist = math.sqrt(math.pow(a[0] - b[0], 2) + math.pow(a[1] - b[1], 2) + math.pow(a[2] - b[2], 2))
+        dist = math.sqrt(_sq(a[0] - b[0]) + _sq(a[1] - b[1]) + _sq(a[2] - b[2]))
         total += dist / desired_vel
         T.append(total)
     return T

@@ -29,6 +29,13 @@ NX = 8  # mpcPlanner.h:42
 NU = 5  # mpcPlanner.h:43
 
 
+
+def _sq(v):
+    """pow(v, 2) of the reference C++: GCC folds pow(x, 2.0) to x * x at every optimisation level
+    (no -ffast-math needed), so the reference binary squares by one correctly rounded multiply --
+    libm's pow (math.pow) can differ from it by an ulp."""
+    return v * v
+
 def f32(v):
     """`float value = v;` in the reference."""
     return float(np.float32(v))
@@ -102,7 +109,7 @@ def build_qp(params, curr_pos, curr_vel, xref, lin_states=None, static_obs=(), d
         A[d][d] = 1.0
         A[d][3 + d] = 1.0 * ts
         A[3 + d][3 + d] = 1.0
-        B[d][d] = ((1.0 * 1) / 2) * math.pow(ts, 2)
+        B[d][d] = ((1.0 * 1) / 2) * _sq(ts)
         B[3 + d][d] = 1.0 * ts
     B[6][3] = 1.0
     B[7][4] = 1.0
@@ -112,8 +119,8 @@ def build_qp(params, curr_pos, curr_vel, xref, lin_states=None, static_obs=(), d
     vmax, amax = params["max_vel"], params["max_acc"]
     xMin = [-inf, params["y_range_min"], params["z_range_min"], -vmax, -vmax, -vmax, -inf, -inf]
     xMax = [inf, params["y_range_max"], params["z_range_max"], vmax, vmax, vmax, inf, inf]
-    skslimit = 1.0 - math.pow((1 - params["static_slack"]), 2)
-    skdlimit = 1.0 - math.pow((1 - params["dynamic_slack"]), 2)
+    skslimit = 1.0 - _sq((1 - params["static_slack"]))
+    skdlimit = 1.0 - _sq((1 - params["dynamic_slack"]))
     uMin = [-amax, -amax, -amax, 0.0, 0.0]
     uMax = [amax, amax, amax, skdlimit, skslimit]
 
@@ -179,14 +186,14 @@ def build_qp(params, curr_pos, curr_vel, xref, lin_states=None, static_obs=(), d
         ox, oy, oz = oxyz[i][j]
         sx, sy, sz = osize[i][j]
         yw = yaw[i][j]
-        fxx = (2 * ((cx - ox) * math.cos(yw) + (cy - oy) * math.sin(yw)) / math.pow(sx, 2) * math.cos(yw)
-               + 2 * (-(cx - ox) * math.sin(yw) + (cy - oy) * math.cos(yw)) / math.pow(sy, 2) * (-math.sin(yw)))
-        fyy = (2 * ((cx - ox) * math.cos(yw) + (cy - oy) * math.sin(yw)) / math.pow(sx, 2) * math.sin(yw)
-               + 2 * (-(cx - ox) * math.sin(yw) + (cy - oy) * math.cos(yw)) / math.pow(sy, 2) * (math.cos(yw)))
-        fzz = 2 * ((cz - oz)) / math.pow(sz, 2)
-        fxyz = (math.pow((cx - ox) * math.cos(yw) + (cy - oy) * math.sin(yw), 2) / math.pow(sx, 2)
-                + math.pow(-(cx - ox) * math.sin(yw) + (cy - oy) * math.cos(yw), 2) / math.pow(sy, 2)
-                + math.pow((cz - oz), 2) / math.pow(sz, 2))
+        fxx = (2 * ((cx - ox) * math.cos(yw) + (cy - oy) * math.sin(yw)) / _sq(sx) * math.cos(yw)
+               + 2 * (-(cx - ox) * math.sin(yw) + (cy - oy) * math.cos(yw)) / _sq(sy) * (-math.sin(yw)))
+        fyy = (2 * ((cx - ox) * math.cos(yw) + (cy - oy) * math.sin(yw)) / _sq(sx) * math.sin(yw)
+               + 2 * (-(cx - ox) * math.sin(yw) + (cy - oy) * math.cos(yw)) / _sq(sy) * (math.cos(yw)))
+        fzz = 2 * ((cz - oz)) / _sq(sz)
+        fxyz = (_sq((cx - ox) * math.cos(yw) + (cy - oy) * math.sin(yw)) / _sq(sx)
+                + _sq(-(cx - ox) * math.sin(yw) + (cy - oy) * math.cos(yw)) / _sq(sy)
+                + _sq((cz - oz)) / _sq(sz))
         return fxx, fyy, fzz, fxyz, (cx, cy, cz)
 
     obs_base = (W + 1) * NX + NX * (W + 1) + NU * W + H * W

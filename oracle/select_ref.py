@@ -20,6 +20,13 @@ FORWARD, LEFT, RIGHT, STOP = 0, 1, 2, 3
 NUM_CONSISTENCY_STEP = 10  # :781
 
 
+
+def _sq(v):
+    """pow(v, 2) of the reference C++: GCC folds pow(x, 2.0) to x * x at every optimisation level
+    (no -ffast-math needed), so the reference binary squares by one correctly rounded multiply --
+    libm's pow (math.pow) can differ from it by an ulp."""
+    return v * v
+
 def consistency_score(states, prev_states, first_time):
     """states, prev_states: lists of 8-vectors (prev may be empty)."""
     if first_time or len(prev_states) == 0 or len(states) == 0:
@@ -58,13 +65,13 @@ def safety_score(states, static_obs, dyn_pos, dyn_size, dyn_safety, static_safet
         px, py = states[i][0], states[i][1]
         for j in range(len(dyn_pos)):
             ox, oy = dyn_pos[j][i][0], dyn_pos[j][i][1]
-            max_size = math.sqrt(math.pow(dyn_size[j][i][0], 2) + math.pow(dyn_size[j][i][1], 2))
+            max_size = math.sqrt(_sq(dyn_size[j][i][0]) + _sq(dyn_size[j][i][1]))
             d = math.sqrt((px - ox) ** 2 + (py - oy) ** 2)
             w = 1 - math.tanh(c / (dyn_safety + max_size) * d)
             dist += d * w
             total_w += w
         for cen, size in static_obs:
-            max_size = math.sqrt(math.pow(size[0] / 2, 2) + math.pow(size[1] / 2, 2))
+            max_size = math.sqrt(_sq(size[0] / 2) + _sq(size[1] / 2))
             d = math.sqrt((px - cen[0]) ** 2 + (py - cen[1]) ** 2)
             w = 1 - math.tanh(c / (static_safety + max_size) * d)
             dist += d * w

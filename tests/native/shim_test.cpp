@@ -76,11 +76,12 @@ static void structured_case() {
     solver.settings()->setWarmStart(true);
     solver.data()->setNumberOfVariables((int)n);
     solver.data()->setNumberOfConstraints((int)m);
+    Eigen::VectorXd qv = vec(q), lv = vec(l), uv = vec(u);  // Data's setters take Ref<VectorXd>: lvalues
     CHECK(solver.data()->setHessianMatrix(P));
-    CHECK(solver.data()->setGradient(vec(q)));
+    CHECK(solver.data()->setGradient(qv));
     CHECK(solver.data()->setLinearConstraintsMatrix(A));
-    CHECK(solver.data()->setLowerBound(vec(l)));
-    CHECK(solver.data()->setUpperBound(vec(u)));
+    CHECK(solver.data()->setLowerBound(lv));
+    CHECK(solver.data()->setUpperBound(uv));
     CHECK(solver.initSolver());
 
     impc_ctx ctx = nullptr;
@@ -100,7 +101,7 @@ static void structured_case() {
     impc_info info{};
     for (int step = 0; step < 3; step++) {
         if (step == 1) {
-            CHECK(solver.updateGradient(vec(q2)));
+            CHECK(solver.updateGradient(vec(q2)));  // Ref<const VectorXd>: temporaries bind
             CHECK(impc_batch_update_lin_cost(b, q2.data()) == IMPC_OK);
         } else if (step == 2) {
             CHECK(solver.updateBounds(vec(l3), vec(u3)));
@@ -191,8 +192,51 @@ int main(int argc, char **argv) {
         CHECK(solver.solveProblem() == OsqpEigen::ErrorExitFlag::NoError);
         CHECK(solver.getStatus() == OsqpEigen::Status::Solved);
         CHECK(std::fabs(solver.getSolution()(1) - 0.6) < 2e-3);
+        // reference-declared accessors: the iterate the next solve starts from, fixed-size templates
+        Eigen::Matrix<double, 2, 1> xp;
+        Eigen::Matrix<double, Eigen::Dynamic, 1> yd;
+        CHECK(solver.getPrimalVariable(xp) && std::fabs(xp(1) - 0.6) < 2e-3);
+        CHECK(solver.getDualVariable(yd) && yd.size() == 3);
+        Eigen::Matrix<double, 3, 1> y3;
+        y3(0) = y3(1) = y3(2) = 0.0;
+        CHECK(solver.setDualVariable(y3));  // osqp_warm_start_y: x kept
+        CHECK(solver.getPrimalVariable(xp) && std::fabs(xp(1) - 0.6) < 2e-3);
+        // same-pattern Hessian update: P = [[4,1],[1,2]] -> [[8,2],[2,4]] with q doubled is the same QP
+        // up to a factor 2 in the objective: x* unchanged
+        Eigen::SparseMatrix<double> P2(2, 2);
+        P2.insert(0, 0) = 8.0;
+        P2.insert(1, 0) = 2.0;
+        P2.insert(0, 1) = 2.0;
+        P2.insert(1, 1) = 4.0;
+        Eigen::VectorXd q2(2);
+        q2(0) = q2(1) = 2.0;
+        CHECK(solver.updateHessianMatrix(P2));
+        CHECK(solver.updateGradient(q2));
+        CHECK(solver.solveProblem() == OsqpEigen::ErrorExitFlag::NoError);
+        CHECK(std::fabs(solver.getSolution()(1) - 0.6) < 2e-3);
         solver.clearSolver();
         CHECK(!solver.isInitialized());
+        // an update before the first solve on the generic kernel (the demo QP's pattern is not
+        // stage-structured): taken by the setup, as OsqpEigen's update after initSolver
+        OsqpEigen::Solver s2;
+        s2.settings()->setVerbosity(false);
+        s2.data()->setNumberOfVariables(2);
+        s2.data()->setNumberOfConstraints(3);
+        CHECK(s2.data()->setHessianMatrix(P));
+        CHECK(s2.data()->setGradient(q));
+        CHECK(s2.data()->setLinearConstraintsMatrix(A));
+        CHECK(s2.data()->setLowerBound(l));
+        CHECK(s2.data()->setUpperBound(u));
+        CHECK(s2.initSolver());
+        CHECK(s2.updateBounds(l2, u2));
+        CHECK(s2.updateGradient(q));
+        CHECK(s2.solveProblem() == OsqpEigen::ErrorExitFlag::NoError);
+        CHECK(s2.getStatus() == OsqpEigen::Status::Solved);
+        CHECK(std::fabs(s2.getSolution()(1) - 0.6) < 2e-3);
+        // a wrongly sized update is refused and leaves the data as it was
+        Eigen::VectorXd bad2(4);
+        CHECK(!s2.updateGradient(bad2));
+        CHECK(s2.data()->q.size() == 2 && s2.data()->q[0] == 1.0);
         structured_case();
     }
     std::printf("%s: %d failure(s)\n", gpu ? "gpu" : "cpu", fails);

@@ -60,7 +60,7 @@ def test_version_string():
 def test_no_device_fails_loudly():
     """Without a GPU the context cannot be created and the error says why (no CPU fallback)."""
     import torch
-    if torch.cuda.is_available():
+    if torch.cuda.device_count() > 0:  # counts without starting torch's own HIP runtime
         pytest.skip("a GPU is present")
     with pytest.raises(impc.ImpcError) as e:
         impc.Context(0)

@@ -109,3 +109,16 @@ def test_batched_builder_matches_per_instance():
         _, one = product(p, *r[2:])
         for k in one:
             np.testing.assert_array_equal(vals[k][i], one[k])
+
+
+def test_yawed_static_rows_bit_exact_many_draws():
+    """Obstacle-row bounds l = 1 - f(c) + grad f(c) . c of yawed static obstacles over many draws:
+    the reference's pow(v, 2) is one correctly rounded multiply in its GCC build (pow(x, 2.0) is
+    folded to x * x), which libm's pow misses by an ulp now and then -- the oracle squares as the
+    reference binary does (oracle/mpc_qp_ref.py _sq)."""
+    for seed in range(40, 80):
+        p, pd, *inp = case(seed=seed, S=4, K=2)
+        pat, vals = product(p, *inp)
+        ref = ref_qp(pd, *inp)
+        for name, r in (("l", ref["l"]), ("Ax", ref["A"][2]), ("q", ref["q"])):
+            assert np.array_equal(vals[name], r), (seed, name)

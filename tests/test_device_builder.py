@@ -1,5 +1,6 @@
-"""On-device MPC -> QP assembly (impc_mpc_build_values_device) against the host
-builder (impc_mpc_build_values, itself bit-exact with oracle/mpc_qp_ref.py, tests/test_builder.py).
+"""On-device MPC -> QP assembly (impc_mpc_build_values_device) against the oracle
+restatement of mpcPlanner's assembly (oracle/mpc_qp_ref.py, mpcPlanner.cpp:891-1197) directly, QP by
+QP, and against the host builder (impc_mpc_build_values) for the whole batch.
 
 Dynamic obstacles (yaw 0) and everything outside the obstacle rows are bit-identical; static
 obstacles with a yaw go through the device cos/sin and may differ by a few ulp.
@@ -11,6 +12,7 @@ import pytest
 
 import impc
 from impc import scenarios
+from oracle import mpc_qp_ref
 
 pytestmark = pytest.mark.gpu
 
@@ -37,6 +39,16 @@ def inputs(seed, nb, N, S, K, L, lin=True):
     return pos, vel, xref, ls, sc, ss, sy, dp, ds
 
 
+def oracle_qp(pd, arrays, i, S, K):
+    """QP i of the batch as oracle/mpc_qp_ref.build_qp assembles it."""
+    pos, vel, xref, ls, sc, ss, sy, dp, ds = arrays
+    static = [(sc[i, j], ss[i, j], sy[i, j]) for j in range(S)] if S else []
+    dpos = [list(dp[i, k]) for k in range(K)] if K else []
+    dsz = [list(ds[i, k]) for k in range(K)] if K else []
+    r = mpc_qp_ref.build_qp(pd, pos[i], vel[i], xref[i], None if ls is None else ls[i], static, dpos, dsz)
+    return dict(Px=r["P"][2], q=r["q"], Ax=r["A"][2], l=r["l"], u=r["u"])
+
+
 def device_build(ctx, p, S, K, L, nb, arrays):
     pos, vel, xref, ls, sc, ss, sy, dp, ds = arrays
     n, m, nnzP, nnzA = impc.mpc_dims(p, S, K)
@@ -56,11 +68,15 @@ def device_build(ctx, p, S, K, L, nb, arrays):
 @pytest.mark.parametrize("S,K,lin", [(0, 8, True), (0, 3, False), (0, 0, False)])
 def test_dynamic_obstacles_bit_identical(ctx, S, K, lin):
     N, L, nb = 20, 31, 37
-    p, _ = impc.mpc_params(horizon=N)
+    p, pd = impc.mpc_params(horizon=N)
     arrays = inputs(10 + K, nb, N, S, K, L, lin)
     dev, outs = device_build(ctx, p, S, K, L, nb, arrays)
     for o in outs:
         o.free()
+    for i in (0, 1, nb // 2, nb - 1):  # the oracle, QP by QP: bit for bit
+        ref = oracle_qp(pd, arrays, i, S, K)
+        for name, a in zip(("Px", "q", "Ax", "l", "u"), dev):
+            assert np.array_equal(a[i], ref[name]), (i, name)
     pos, vel, xref, ls, sc, ss, sy, dp, ds = arrays
     ref = impc.mpc_values(p, pos, vel, xref, ls, dyn_pos=dp if K else None, dyn_size=ds if K else None)
     for name, a in zip(("Px", "q", "Ax", "l", "u"), dev):
@@ -69,11 +85,18 @@ def test_dynamic_obstacles_bit_identical(ctx, S, K, lin):
 
 def test_static_obstacles_with_yaw_within_ulps(ctx):
     N, S, K, L, nb = 20, 4, 2, 31, 23
-    p, _ = impc.mpc_params(horizon=N)
+    p, pd = impc.mpc_params(horizon=N)
     arrays = inputs(77, nb, N, S, K, L, True)
     dev, outs = device_build(ctx, p, S, K, L, nb, arrays)
     for o in outs:
         o.free()
+    for i in (0, nb - 1):  # the oracle, QP by QP: device cos/sin within an ulp-level tolerance
+        ref = oracle_qp(pd, arrays, i, S, K)
+        for name, a in zip(("Px", "q", "Ax", "l", "u"), dev):
+            r = ref[name]
+            fin = np.isfinite(r)
+            assert np.array_equal(np.isfinite(a[i]), fin) and np.array_equal(a[i][~fin], r[~fin]), (i, name)
+            np.testing.assert_allclose(a[i][fin], r[fin], rtol=1e-13, atol=1e-13, err_msg=name)
     pos, vel, xref, ls, sc, ss, sy, dp, ds = arrays
     ref = impc.mpc_values(p, pos, vel, xref, ls, st_centroid=sc, st_size=ss, st_yaw=sy, dyn_pos=dp, dyn_size=ds)
     for name, a in zip(("Px", "q", "Ax", "l", "u"), dev):

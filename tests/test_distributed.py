@@ -79,3 +79,91 @@ def test_two_rank_gather_and_max():
 def test_rank_seed_weak_scaling_invariant():
     assert D.rank_seed(3000, 0) == 3000
     assert len({D.rank_seed(3000, r) for r in range(8)}) == 8
+
+
+def test_shard_plan_balances_sigma_m():
+    """Config 4's instance sharding: contiguous ranges, every rank within one
+    instance's weight of the ideal Sigma m share, ranges cover every instance once."""
+    from impc import scenarios
+    K, w = scenarios.config4_plan(total_qps=262144)
+    assert K.min() == 0 and K.max() == 20 and w.size == 32768
+    for world in (1, 2, 4, 8):
+        b = D.shard_plan(w, world)
+        assert b[0] == 0 and b[-1] == w.size and (np.diff(b) > 0).all()
+        share = np.array([w[b[r]:b[r + 1]].sum() for r in range(world)])
+        assert abs(share - w.sum() / world).max() <= w.max()
+    # a skewed weight vector still splits within one instance of the ideal cut
+    w2 = np.concatenate([np.full(10, 100.0), np.ones(1000)])
+    b2 = D.shard_plan(w2, 2)
+    s2 = [w2[:b2[1]].sum(), w2[b2[1]:].sum()]
+    assert abs(s2[0] - s2[1]) <= 2 * 100.0
+
+
+def _config4_worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(WORLD))
+    try:
+        import sys
+        here = os.path.dirname(os.path.abspath(__file__))
+        sys.path[:0] = [here, os.path.dirname(here)]
+        from helpers import oracle
+        import impc
+        from impc import scenarios
+        r, lr, w = D.env()
+        dist = D.init("gloo", lr)
+        # bench.py --workload config4's rank path at a small job size, the oracle solving on CPU
+        Kinst, wt = scenarios.config4_plan(total_qps=96, kmax=6)
+        bounds = D.shard_plan(wt, w)
+        lo, hi = int(bounds[r]), int(bounds[r + 1])
+        bks = scenarios.config4_rank(lo, hi, Kinst)
+        counts = [8 * int(bounds[k + 1] - bounds[k]) for k in range(w)]
+        s = impc.default_settings(verbose=0, adaptive_rho_interval=25)
+        recs = []
+        for bk in bks:
+            _, _, info = oracle(bk, s)
+            rec = np.zeros((bk["values"]["q"].shape[0], 8))
+            rec[:, 0] = r
+            rec[:, 1] = bk["inst"]
+            rec[:, 2] = bk["hyp"]
+            rec[:, 3] = info["obj_val"]
+            rec[:, 4] = info["status_val"]
+            rec[:, 5] = info["iter"]
+            rec[:, 6] = bk["K"]
+            recs.append(rec)
+        allrec = D.gather_costs(dist, np.concatenate(recs), counts)
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((r, np.concatenate(recs), allrec, (Kinst, bounds, counts)))
+    except Exception as e:  # surface the failure in the parent
+        import traceback
+        q.put((rank, traceback.format_exc(), None, None))
+
+
+def test_two_rank_config4_shard_and_gather():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_config4_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(WORLD):
+        r, rec, allrec, plan = q.get(timeout=300)
+        assert allrec is not None, rec
+        out[r] = (rec, allrec, plan)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    Kinst, bounds, counts = out[0][2]
+    all0, all1 = out[0][1], out[1][1]
+    np.testing.assert_array_equal(all0, all1)                        # every rank holds every cost
+    np.testing.assert_array_equal(all0, np.concatenate([out[0][0], out[1][0]]))
+    assert all0.shape[0] == sum(counts) == 96                      # the whole job, no padding left
+    # every instance: 8 hypotheses on the rank that owns its range, with its planned K
+    for i in range(Kinst.size):
+        rows = all0[all0[:, 1] == i]
+        owner = int(np.searchsorted(bounds, i, side="right") - 1)
+        assert sorted(rows[:, 2]) == list(range(8)) and (rows[:, 0] == owner).all()
+        k = Kinst[i]
+        assert set(rows[:, 6]) <= ({0} if k == 0 else {k, k + 1})
+    assert (all0[:, 4] != 0).all()                                   # every QP solved (a status set)
