@@ -1190,6 +1190,18 @@ void ora_get_iterates(const ora_ws *w, c_float *x, c_float *y) {
     for (c_int i = 0; i < w->m; i++) y[i] = w->scaled ? w->E[i] * w->y[i] * w->cinv : w->y[i];
 }
 
+/* The state osqp_setup leaves in the workspace (types.h:182-289): rho_vec, constr_type, the
+ * scaling vectors D, E and the cost scale c -- compared in tests/test_oracle.py with the facts the
+ * survey's probe read from the reference libosqp.so's OSQPWorkspace after osqp_setup (SURVEY.md
+ * 8a row a9). */
+void ora_get_setup(const ora_ws *w, c_float *rho_vec, c_int *constr_type, c_float *D, c_float *E, c_float *c) {
+    if (rho_vec) memcpy(rho_vec, w->rho_vec, sizeof(c_float) * (size_t)w->m);
+    if (constr_type) memcpy(constr_type, w->constr_type, sizeof(c_int) * (size_t)w->m);
+    for (c_int i = 0; D && i < w->n; i++) D[i] = w->scaled ? w->D[i] : 1.0;
+    for (c_int i = 0; E && i < w->m; i++) E[i] = w->scaled ? w->E[i] : 1.0;
+    if (c) *c = w->scaled ? w->c : 1.0;
+}
+
 void ora_cleanup(ora_ws *w) {
     if (!w) return;
     csc_free(w->P);

@@ -54,6 +54,7 @@ def lib():
         L.ora_update_lin_cost.argtypes = [C.c_void_p, dp]
         L.ora_update_bounds.argtypes = [C.c_void_p, dp, dp]
         L.ora_cleanup.argtypes = [C.c_void_p]
+        L.ora_get_setup.argtypes = [C.c_void_p, dp, ip, dp, dp, dp]
         L.ora_cleanup.restype = None
         _lib = L
     return _lib
@@ -131,6 +132,15 @@ class Workspace:
 
     def update_bounds(self, l, u):
         lib().ora_update_bounds(self.h, _d(np.ascontiguousarray(l, float)), _d(np.ascontiguousarray(u, float)))
+
+    def setup_state(self):
+        """rho_vec, constr_type, D, E and c as osqp_setup left them (ora_get_setup)."""
+        rho = np.empty(max(self.m, 1))
+        ct = np.empty(max(self.m, 1), np.int64)
+        D, E = np.empty(self.n), np.empty(max(self.m, 1))
+        c = C.c_double()
+        lib().ora_get_setup(self.h, _d(rho), _i(ct), _d(D), _d(E), C.byref(c))
+        return dict(rho_vec=rho[: self.m], constr_type=ct[: self.m], D=D, E=E[: self.m], c=c.value)
 
     def solve(self):
         lib().ora_solve_ws(self.h)

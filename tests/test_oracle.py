@@ -158,3 +158,49 @@ def test_no_adaptive_rho():
                        eps_abs=1e-9, eps_rel=1e-9, max_iter=100000, adaptive_rho=0)
     assert info["status_val"] == 1 and info["rho_updates"] == 0
     assert np.allclose(x, [0.3, 0.7], atol=1e-7)
+
+
+def test_setup_state_matches_libosqp_probe_facts():
+    """The only reference-side facts about osqp_setup's internals (the survey's
+    probe read them from the vendored libosqp.so's OSQPWorkspace on an N=20, K=10 mpcPlanner QP):
+    constr_type 1 / rho_vec 100 on the dynamics (equality) rows, -1 / 1e-6 on the box rows bounded
+    by +-inf on both sides (x position and the two dummy states), 0 / 0.1 on the finite box, slack
+    and obstacle rows; cost scale c of order 1e-3; D and E in roughly [0.1, 10]."""
+    import impc
+    from impc import scenarios
+    cfg = scenarios.static_config(N=20, K=10, batch=1, seed=2000)
+    pat, v = cfg["pattern"], cfg["values"]
+    N, n, m = 20, pat["n"], pat["m"]
+    w = ora.Workspace(pat, v["Px"][0], v["q"][0], v["Ax"][0], v["l"][0], v["u"][0],
+                      ora.settings_from(impc.default_settings(verbose=0)))
+    st = w.setup_state()
+    w.close()
+    ct, rho = st["constr_type"], st["rho_vec"]
+    dyn = slice(0, 8 * N)
+    assert (ct[dyn] == 1).all() and np.allclose(rho[dyn], 100.0)
+    box = np.arange(8 * N, 8 * N + n)
+    state_box = box[: 8 * N].reshape(N, 8)
+    loose = state_box[:, [0, 6, 7]].ravel()                    # x position, the two dummy states
+    assert (ct[loose] == -1).all() and np.allclose(rho[loose], 1e-6)
+    finite = np.concatenate([state_box[:, 1:6].ravel(), box[8 * N:], np.arange(8 * N + n, m)])
+    assert (ct[finite] == 0).all() and np.allclose(rho[finite], 0.1)
+    assert 1e-4 < st["c"] < 1e-2
+    for vec in (st["D"], st["E"]):
+        assert 0.05 < vec.min() and vec.max() < 20.0
+
+
+def test_reachable_reference_needs_fewer_iterations():
+    """the synthetic reference (0.5-2.5 m per 0.1 s step, mostly beyond
+    vmax = 5 m/s) explains the iteration counts above the survey's libosqp probe (125 at K = 0):
+    with a reachable reference the same first-call QPs converge in far fewer iterations."""
+    import impc
+    from impc import scenarios
+    s = impc.default_settings(verbose=0)
+    it = {}
+    for step in (0.3, 2.5):
+        cfg = scenarios.first_call_config(batch=16, seed=11, step_range=(step, step))
+        v = cfg["values"]
+        _, _, info = ora.solve_batch(cfg["pattern"], v["Px"], v["q"], v["Ax"], v["l"], v["u"],
+                                     ora.settings_from(s), threads=4)
+        it[step] = float(info["iter"].mean())
+    assert it[0.3] <= 200 and it[2.5] >= 1.5 * it[0.3], it
