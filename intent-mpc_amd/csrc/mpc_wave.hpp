@@ -70,6 +70,12 @@ namespace impc {
 #ifndef IMPC_PSTRIDE_PAD
 #define IMPC_PSTRIDE_PAD 1
 #endif
+#ifndef IMPC_PAIR  // pair-blocked stage recursions on the default horizon (WaveLds::PAIR): built,
+#define IMPC_PAIR 0  // measured slower (profiles/r02/exp/README.md), off
+#endif
+#ifndef IMPC_PCAP_REG  // pair sweeps: keep the stage results in registers until the sweep ends (1)
+#define IMPC_PCAP_REG 0  // or store each one as it is produced (0: measured faster, fewer spills)
+#endif
 
 struct WaveTables {
     int32_t n, m, mg, N, W, CG, nnzP, nnzA;
@@ -137,7 +143,9 @@ struct WaveLds {
     // for the one-variable-per-lane shape, N = 40 for the long-horizon shape)
     static constexpr int WSPEC = VS == 1 ? 19 : 39;
     // exchange vector length: zero tail past NMAX, and room for the factorisation scratch
-    static constexpr int NP = (NMAX + 192 > (779 + NL * GS + NMAX + 3) / 4) ? NMAX + 192 : (779 + NL * GS + NMAX + 3) / 4;
+    // (the sweeps' two-steps-ahead prefetches read at most 13 (W + 4) + 8 past the start), and
+    // room for the factorisation's dense stage scratch (FA .. DIAGX below)
+    static constexpr int NP = (NMAX + 48 > (779 + NMAX + 3) / 4) ? NMAX + 48 : (779 + NMAX + 3) / 4;
     static constexpr int F_OFF = 0;                         // [WMAX][64]
     static constexpr int R_OFF = F_OFF + WMAX * 64;         // rbuf
     static constexpr int T_OFF = R_OFF + NP;                // tbuf
@@ -159,7 +167,16 @@ struct WaveLds {
     // is full).  Layout of each: [var slots NMAX][box rows NMAX][general slots NL GS].
     static constexpr bool ONCHIP = VS == 1;
     static constexpr int VEC_N = 2 * NMAX + NL * GS;
-    static constexpr int SCL_OFF = PSI_OFF + PSI_N;         // D, E (scaling)
+    // Pair-blocked stage recursions (default horizon of the one-variable-per-lane shape): the
+    // 8-dim recursions step over two stages at a time along the even stages, with the products
+    // H_k = F_{k+1} F_k and M_k = F_{k+1} G_k[:, 8:] (k = 0, 2, .., WSPEC - 3) formed by the
+    // factorisation; the odd stages come off the chain as independent side products.
+    static constexpr bool PAIR = VS == 1 && NL == 256 && IMPC_PAIR && !CHUNK;
+    static constexpr int NH = (WSPEC - 1) / 2;              // chain steps (9 at WSPEC = 19)
+    static_assert(!PAIR || (WSPEC & 1), "pair blocking needs an odd stage count");
+    static constexpr int H_OFF = PSI_OFF + PSI_N;           // [NH][64] H_k, recursion layout
+    static constexpr int M_OFF = H_OFF + (PAIR ? 64 * NH : 0);  // [NH][40] M_k, row-major 8 x 5
+    static constexpr int SCL_OFF = M_OFF + (PAIR ? 40 * NH : 0);  // D, E (scaling)
     static constexpr int DLT_OFF = SCL_OFF + (ONCHIP ? VEC_N : 0);  // dx, dy (check iterations)
     static constexpr int P_OFF = DLT_OFF + (ONCHIP ? VEC_N : 0);    // products, column-slot layout (size below)
     // chunk-boundary exchange of the recursions (inside the team reduction scratch, past red[0..3])
@@ -175,14 +192,16 @@ struct WaveLds {
     // entry slots; a stride that is not a multiple of 16 doubles puts those ds_write_b64 (bank =
     // dword mod 32, 16-lane groups) on distinct banks.  Reads stay lane-contiguous.
     static IMPC_WF int stride(int n) { return ((n + 63) & ~63) + IMPC_PSTRIDE_PAD; }
+    // the factorisation uses it as (4g + e) scratch followed by the general rows' rho (RHOG_P)
     static IMPC_WF int p_size(int CG, int n) {
-        const int c = cg4(CG) * stride(n), f = 4 * NL * GS;
+        const int c = cg4(CG) * stride(n), f = 5 * NL * GS;
         return c > f ? c : f;
     }
     static IMPC_WF int size(int CG, int n) { return P_OFF + p_size(CG, n) + 8; }
     // factorisation aliases (inside R..X region and the products buffer)
     static constexpr int FA = R_OFF, FL = FA + 169, FI = FL + 169, FB = FI + 169, FG = FB + 104, FE = FG + 104,
-                         RHOG = FE + 64, DIAGX = RHOG + NL * GS;
+                         DIAGX = FE + 64;
+    static constexpr int RHOG_P = 4 * NL * GS;  // general rows' rho, inside the products region
     static_assert(DIAGX + NMAX <= RED_OFF, "factorisation scratch does not fit");
 };
 
@@ -266,6 +285,15 @@ struct WaveQP {
         asm volatile("" : "+v"(l));
 #endif
         return l;
+    }
+
+    // a per-lane value the optimiser must treat as freshly computed (see lane_o)
+    IMPC_WF static void opaque(int &v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("" : "+v"(v));
+#else
+        (void)v;
+#endif
     }
 
     // team-uniform: R stays in scalar registers, and each row's rho / 1/rho is selected from it
@@ -520,7 +548,8 @@ struct WaveQP {
     // Returns 1 if a pivot is not positive (OSQP_NONCVX_ERROR).
     IMPC_WF int factorize() {
         const int n = T.n, W = Wst(), N = W + 1;
-        double *w = pbuf(), *rhog = lds + LD::RHOG, *diagx = lds + LD::DIAGX;
+        double *w = pbuf(), *rhog = pbuf() + LD::RHOG_P, *diagx = lds + LD::DIAGX;
+        const bool pair = LD::PAIR && W == LD::WSPEC;
         double *A = lds + LD::FA, *Li = lds + LD::FL, *Ai = lds + LD::FI, *Bb = lds + LD::FB, *G = lds + LD::FG,
                *E = lds + LD::FE, *Fm = F();
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
@@ -630,8 +659,14 @@ struct WaveQP {
                     double s = 0.0;
                     for (int t = 0; t < 13; t++) s += G[13 * i + t] * Bb[13 * j + t];
                     E[8 * i + j] = s;
-                    // recursion layout: lane (i,j) of step k reads F_k[j][i] (k even) / F_k[i][j]
-                    Fm[64 * k + 8 * i + j] = (k & 1) ? G[13 * i + j] : G[13 * j + i];
+                    // recursion layout: lane (i,j) of step k reads F_k[j][i] when the column index
+                    // sits on i (k even, or pair_col_i(k) when pair-blocked), F_k[i][j] otherwise
+                    const bool ci = pair ? pair_col_i(k) : !(k & 1);
+                    Fm[64 * k + 8 * i + j] = ci ? G[13 * j + i] : G[13 * i + j];
+                } else if (pair && L < 104 && !(k & 1) && k < 2 * LD::NH) {
+                    // G_k[:, 8:] of the even stages, for M_k = F_{k+1} G_k[:, 8:] once F_{k+1} exists
+                    const int p = L - 64, q = p / 5, cc = p % 5;
+                    lds[LD::M_OFF + 40 * (k >> 1) + p] = G[13 * q + 8 + cc];
                 }
                 _Pragma("unroll") for (int s = 0; s < VS; s++) {
                     if (!vok[s]) continue;
@@ -649,11 +684,211 @@ struct WaveQP {
                 _Pragma("unroll") for (int j = 0; j < 8; j++) cp[s][j] = 0.0;
         if constexpr (LD::CHUNK)
             if (W == LD::WSPEC) chunk_operators();
+        if constexpr (LD::PAIR)
+            if (pair) pair_operators();
         bad = (int)wv.max((double)bad);  // set by lane 0 only: team-wide, so every wavefront agrees
         clear_exchange();
         zero_products();  // the (4g + e) factorisation scratch shared the products region
         (void)n;
         return bad;
+    }
+
+    // ---------------------------------------------------- pair-blocked stage recursions
+    // Forward: a_{k+1} = t_{k+1} - F_k a_k.  Over two stages, a_{k+2} = u_{k+2} + H_k a_k with
+    // u_{k+2} = t_{k+2} - F_{k+1} t_{k+1} (formed in S1) and H_k = F_{k+1} F_k, so the dependent
+    // chain runs over the even stages (a_0 -> a_2 -> .. -> a_{W-1}: (W - 1) / 2 steps) and each step
+    // also yields the odd stage a_{k+1} = t_{k+1} - F_k a_k from the same input: an independent
+    // second reduction that fills the chain's latency.  Backward likewise: x_k = v_k + H_k' x_{k+2}
+    // with v_k = e_k - F_k' e_{k+1} (the V phase) and the side x_{k+1} = e_{k+1} - F_{k+1}' x_{k+2}.
+    // Layout: the vector of even stage k = 2c sits at index i when c is even (j when odd); the
+    // matrices of stages k and k + 1 are stored with their column index on that index
+    // (pair_col_i), so every step reduces over its input's index and lands on the other one.
+    static IMPC_WF constexpr bool pair_col_i(int k) { return ((k >> 1) & 1) == 0; }
+    // F_k[r][c] in the pair layout
+    IMPC_WF double Fp(int k, int r, int c) const {
+        return pair_col_i(k) ? lds[LD::F_OFF + 64 * k + 8 * c + r] : lds[LD::F_OFF + 64 * k + 8 * r + c];
+    }
+
+    // H_k = F_{k+1} F_k (in the layout of step k) and M_k = F_{k+1} G_k[:, 8:] (row-major; the M
+    // slots hold G_k[:, 8:] until here), k = 0, 2, .., 2 (NH - 1)
+    IMPC_WF void pair_operators() {
+        wv.sync();
+        double *Hm = lds + LD::H_OFF, *Mm = lds + LD::M_OFF;
+        for (int p = L; p < 64 * LD::NH; p += NL) {
+            const int c = p >> 6, e = p & 63, k = 2 * c, i = e >> 3, j = e & 7;
+            const int r = pair_col_i(k) ? j : i, col = pair_col_i(k) ? i : j;
+            double a = 0.0;
+            for (int q = 0; q < 8; q++) a += Fp(k + 1, r, q) * Fp(k, q, col);
+            Hm[p] = a;
+        }
+        constexpr int NM = 40 * LD::NH, MR = (NM + NL - 1) / NL;
+        double mv[MR];
+        _Pragma("unroll") for (int t = 0; t < MR; t++) {
+            const int p = L + NL * t;
+            double a = 0.0;
+            if (p < NM) {
+                const int c = p / 40, e = p % 40, r = e / 5, cc = e % 5;
+                for (int q = 0; q < 8; q++) a += Fp(2 * c + 1, r, q) * Mm[40 * c + 5 * q + cc];
+            }
+            mv[t] = a;
+        }
+        wv.sync();
+        _Pragma("unroll") for (int t = 0; t < MR; t++)
+            if (L + NL * t < NM) Mm[L + NL * t] = mv[t];
+        wv.sync();
+    }
+
+    // Stage s's value r sits in the 8 lanes that share its index.  IMPC_PCAP_REG = 0: the lane
+    // whose other index is 0 stores it to buf right away (the others to their discard slot).
+    // IMPC_PCAP_REG = 1: the lane whose other index is s mod 8 keeps it in slot s / 8 of the array
+    // for values on index i (ci) or j (cj) and pcap_store writes them after the sweep (no LDS
+    // store per step, but 6 more live doubles: measured slower through register spills).
+    static constexpr int PQ = (LD::WSPEC + 8) / 8;
+    template <bool OUT_I>
+    IMPC_WF void pcap(double (&ci)[PQ], double (&cj)[PQ], double r, int s, int i, int j, double *buf, double *junk) {
+#if IMPC_PCAP_REG
+        (void)buf, (void)junk;
+        if (OUT_I) {
+            if (j == (s & 7)) ci[s >> 3] = r;
+        } else {
+            if (i == (s & 7)) cj[s >> 3] = r;
+        }
+#else
+        (void)ci, (void)cj;
+        if (OUT_I)
+            *(j == 0 ? buf + 13 * s + i : junk) = r;
+        else
+            *(i == 0 ? buf + 13 * s + j : junk) = r;
+#endif
+    }
+    // store the captured stages s0 .. s1 (stage s at 13 s + its index; out_i(s): on index i)
+    template <class OUTI>
+    IMPC_WF void pcap_store(const double (&ci)[PQ], const double (&cj)[PQ], double *buf, int s0, int s1, int i,
+                            int j, OUTI out_i) {
+        if (!IMPC_PCAP_REG) return;
+        double *junk = lds + LD::JUNK_OFF + lane_o();
+        _Pragma("unroll") for (int q = 0; q < PQ; q++) {
+            const int si = 8 * q + j, sj = 8 * q + i;
+            *((si >= s0 && si <= s1 && out_i(si)) ? buf + 13 * si + i : junk) = ci[q];
+            *((sj >= s0 && sj <= s1 && !out_i(sj)) ? buf + 13 * sj + j : junk) = cj[q];
+        }
+    }
+
+    // S2, pair-blocked (W = WSPEC): from a_0 = t_0 (index i), stages 1 .. W into rb; tb holds
+    // u_k on the even stages k >= 2 (S1).  Operands are loaded two steps ahead.
+    IMPC_WF void fwd_pair(const double *tb, double *rb) {
+        constexpr int NH = LD::NH, W = LD::WSPEC;
+        constexpr bool last_on_i = (NH & 1) == 0;  // input index of the final side step
+        const double *Fm = F(), *Hm = lds + LD::H_OFF;
+        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;
+        double *junk = lds + LD::JUNK_OFF + lo;
+        double ci[PQ], cj[PQ];
+        if (IMPC_PCAP_REG) _Pragma("unroll") for (int q = 0; q < PQ; q++) ci[q] = cj[q] = 0.0;
+        double a = tb[i];
+        // operands of step c: H_{2c}, F_{2c}, u_{2c+2}, t_{2c+1} (u, t on the step's output index);
+        // step NH is the final side step (F_{W-1}, t_W)
+        auto ld = [&](int c, double &h, double &f, double &u, double &t) {
+            const int k = 2 * c, xo = (c & 1) == 0 ? j : i;
+            if (c < NH) {
+                h = Hm[64 * c + l];
+                f = Fm[64 * k + l];
+                u = tb[13 * (k + 2) + xo];
+                t = tb[13 * (k + 1) + xo];
+            } else if (c == NH) {
+                f = Fm[64 * (W - 1) + l];
+                t = tb[13 * W + xo];
+            }
+        };
+        double h0 = 0, f0 = 0, u0 = 0, t0 = 0, h1 = 0, f1 = 0, u1 = 0, t1 = 0;
+        ld(0, h0, f0, u0, t0);
+        ld(1, h1, f1, u1, t1);
+        _Pragma("unroll") for (int c = 0; c < NH; c++) {
+            const int k = 2 * c;
+            const bool on_i = (c & 1) == 0;  // this step's input index (its outputs: the other)
+            const double h = h0, f = f0, u = u0, t = t0;
+            h0 = h1, f0 = f1, u0 = u1, t0 = t1;
+            ld(c + 2, h1, f1, u1, t1);
+            const double pc = prod_nc(h, a), ps = prod_nc(f, a);
+            double rc, rs;
+            if (on_i) {
+                rc = wv.sum_stride8(pc);
+                rs = wv.sum_stride8(ps);
+            } else {
+                rc = wv.sum_contig8(pc);
+                rs = wv.sum_contig8(ps);
+            }
+            const double as = t - rs;  // a_{k+1}
+            a = u + rc;                // a_{k+2}
+            if (on_i) {
+                pcap<false>(ci, cj, as, k + 1, i, j, rb, junk);
+                pcap<false>(ci, cj, a, k + 2, i, j, rb, junk);
+            } else {
+                pcap<true>(ci, cj, as, k + 1, i, j, rb, junk);
+                pcap<true>(ci, cj, a, k + 2, i, j, rb, junk);
+            }
+        }
+        const double ps = prod_nc(f0, a);
+        const double aw = t0 - (last_on_i ? wv.sum_stride8(ps) : wv.sum_contig8(ps));
+        pcap<!last_on_i>(ci, cj, aw, W, i, j, rb, junk);
+        pcap_store(ci, cj, rb, 1, W, i, j, [](int s) { return s == W ? !last_on_i : (((s - 1) >> 1) & 1) == 1; });
+    }
+
+    // S4, pair-blocked (W = WSPEC): from x_W = e_W, stages W-1 .. 0 into xb; eb holds v_k on the
+    // even stages k <= W - 3 (V phase).  Operands are loaded two steps ahead.
+    IMPC_WF void bwd_pair(const double *eb, double *xb) {
+        constexpr int NH = LD::NH, W = LD::WSPEC;
+        constexpr bool last_on_i = (NH & 1) == 0;  // x_{W-1} sits on index i (else j)
+        const double *Fm = F(), *Hm = lds + LD::H_OFF;
+        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;
+        double *junk = lds + LD::JUNK_OFF + lo;
+        double ci[PQ], cj[PQ];
+        if (IMPC_PCAP_REG) _Pragma("unroll") for (int q = 0; q < PQ; q++) ci[q] = cj[q] = 0.0;
+        // operands of step c (x_{2c+2} -> x_{2c}, x_{2c+1}): H_{2c}, F_{2c+1}, v_{2c}, e_{2c+1}, on
+        // the step's output index (i for even c)
+        auto ld = [&](int c, double &h, double &f, double &v, double &e) {
+            if (c < 0) return;
+            const int xo = (c & 1) == 0 ? i : j;
+            h = Hm[64 * c + l];
+            f = Fm[64 * (2 * c + 1) + l];
+            v = eb[13 * (2 * c) + xo];
+            e = eb[13 * (2 * c + 1) + xo];
+        };
+        double h0 = 0, f0 = 0, v0 = 0, e0 = 0, h1 = 0, f1 = 0, v1 = 0, e1 = 0;
+        ld(NH - 1, h0, f0, v0, e0);
+        ld(NH - 2, h1, f1, v1, e1);
+        // x_{W-1} = e_{W-1} - F_{W-1}' x_W, reduced over x_W's index
+        double x;
+        {
+            const double xW = eb[13 * W + (last_on_i ? j : i)], ew = eb[13 * (W - 1) + (last_on_i ? i : j)];
+            const double p = prod_nc(Fm[64 * (W - 1) + l], xW);
+            x = ew - (last_on_i ? wv.sum_contig8(p) : wv.sum_stride8(p));
+            pcap<last_on_i>(ci, cj, x, W - 1, i, j, xb, junk);
+        }
+        _Pragma("unroll") for (int c = NH - 1; c >= 0; c--) {
+            const bool out_i = (c & 1) == 0;
+            const double h = h0, f = f0, v = v0, e = e0;
+            h0 = h1, f0 = f1, v0 = v1, e0 = e1;
+            ld(c - 2, h1, f1, v1, e1);
+            const double pc = prod_nc(h, x), ps = prod_nc(f, x);
+            double rc, rs;
+            if (out_i) {  // input on index j
+                rc = wv.sum_contig8(pc);
+                rs = wv.sum_contig8(ps);
+            } else {
+                rc = wv.sum_stride8(pc);
+                rs = wv.sum_stride8(ps);
+            }
+            const double xs = e - rs;  // x_{2c+1}
+            x = v + rc;                // x_{2c}
+            if (out_i) {
+                pcap<true>(ci, cj, xs, 2 * c + 1, i, j, xb, junk);
+                pcap<true>(ci, cj, x, 2 * c, i, j, xb, junk);
+            } else {
+                pcap<false>(ci, cj, xs, 2 * c + 1, i, j, xb, junk);
+                pcap<false>(ci, cj, x, 2 * c, i, j, xb, junk);
+            }
+        }
+        pcap_store(ci, cj, xb, 0, W - 1, i, j, [](int s) { return s == W - 1 ? last_on_i : ((s >> 1) & 1) == 0; });
     }
 
     // ------------------------------------------------------- chunked stage recursions
@@ -1009,6 +1244,7 @@ struct WaveQP {
     // --------------------------------------------------------------- one ADMM iteration
     IMPC_WF void iterate(bool need_delta) {
         const int n = T.n, W = Wst();
+        const bool pair = LD::PAIR && W == LD::WSPEC;
         double *rb = rbuf(), *tb = tbuf(), *eb = ebuf(), *xb = xbuf();
         const double sigma = st.sigma, alpha = st.alpha, oma = (double)1.0 - st.alpha;
         IMPC_REP(kSecRhs) {
@@ -1035,6 +1271,23 @@ struct WaveQP {
                     const double *rp = rb + 13 * (vs_[s] - 1) + 8;
                     _Pragma("unroll") for (int cc = 0; cc < 5; cc++) t -= cp[s][cc] * rp[cc];
                 }
+                if constexpr (LD::PAIR) {
+                    // pair-blocked forward: on the even stages k >= 2 the chain takes
+                    // u_k = t_k - F_{k-1} t_{k-1} = t_k - F_{k-1} r_{k-1}[:8] + M_{k-2} r_{k-2}[8:]
+                    int k = vs_[s];
+                    if (pair && k >= 2 && !(k & 1)) {
+                        int r = vr_[s];
+                        opaque(k);  // per-lane addresses formed here, not hoisted out of the ADMM loop
+                        opaque(r);
+                        const double *r1 = rb + 13 * (k - 1), *r2 = rb + 13 * (k - 2) + 8;
+                        const double *Mk = lds + LD::M_OFF + 40 * ((k - 2) >> 1) + 5 * r;
+                        double fa = 0.0, fb = 0.0, mb = 0.0;
+                        _Pragma("unroll") for (int q = 0; q < 4; q++) fa += Fp(k - 1, r, q) * r1[q];
+                        _Pragma("unroll") for (int q = 4; q < 8; q++) fb += Fp(k - 1, r, q) * r1[q];
+                        _Pragma("unroll") for (int cc = 0; cc < 5; cc++) mb += Mk[cc] * r2[cc];
+                        t = (t - (fa + fb)) + mb;
+                    }
+                }
                 tb[v] = t;
             }
             wv.lsync();
@@ -1053,7 +1306,13 @@ struct WaveQP {
                 if constexpr (LD::CHUNK) fwd_chunked(tb, rb);
             } else if ((L >> 6) == rw) {
                 IMPC_PRIO_HI();
-                if (W == LD::WSPEC)
+                if constexpr (LD::PAIR) {
+                    if (pair) fwd_pair(tb, rb);
+                    else if (W == LD::WSPEC)
+                        fwd_sweep<LD::WSPEC>(tb, rb, W);
+                    else
+                        fwd_sweep<0>(tb, rb, W);
+                } else if (W == LD::WSPEC)
                     fwd_sweep<LD::WSPEC>(tb, rb, W);
                 else
                     fwd_sweep<0>(tb, rb, W);
@@ -1072,6 +1331,24 @@ struct WaveQP {
                 eb[NL * s + L] = e;
             }
             wv.lsync();
+            if constexpr (LD::PAIR) {
+                // V: v_k = e_k - F_k' e_{k+1} on the even stages k <= W - 3 (pair-blocked backward
+                // chain), in place: each lane reads only the odd stage k + 1 besides its own value
+                if (pair) {
+                    _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                        int k = vs_[s], r = vr_[s];
+                        if (!vok[s] || r >= 8 || (k & 1) || k > W - 3) continue;
+                        opaque(k);
+                        opaque(r);
+                        const double *e1 = eb + 13 * (k + 1);
+                        double va = 0.0, vb = 0.0;
+                        _Pragma("unroll") for (int q = 0; q < 4; q++) va += Fp(k, q, r) * e1[q];
+                        _Pragma("unroll") for (int q = 4; q < 8; q++) vb += Fp(k, q, r) * e1[q];
+                        eb[NL * s + L] = eb[NL * s + L] - (va + vb);
+                    }
+                    wv.lsync();
+                }
+            }
         }
         IMPC_SEC(kSecS3);
         IMPC_REP(kSecBwd) {
@@ -1082,7 +1359,9 @@ struct WaveQP {
                 if constexpr (LD::CHUNK) bwd_chunked(eb, xb);
             } else if ((L >> 6) == rw) {
                 IMPC_PRIO_HI();
-                if (W == LD::WSPEC)
+                if (LD::PAIR && pair) {
+                    if constexpr (LD::PAIR) bwd_pair(eb, xb);
+                } else if (W == LD::WSPEC)
                     bwd_sweep<((LD::WSPEC - 1) & 1) != 0, LD::WSPEC>(eb, xb, W);
                 else if ((W - 1) & 1)
                     bwd_sweep<true, 0>(eb, xb, W);

@@ -83,3 +83,18 @@ def test_structured_emulation_long_horizon():
     cfg = take(scenarios.intent_config(N=40, K=10, instances=1, seed=4040)[10], 1)
     s = impc.default_settings(**S25)
     compare(emulate(cfg, s), oracle(cfg, s))
+
+
+@pytest.mark.parametrize("rho", [0.1, 1e-3])
+def test_structured_emulation_default_horizon_batch(rho):
+    """The default-horizon (W = 19) path of the structured kernel -- pair-blocked stage recursions
+    (mpc_wave.hpp fwd_pair / bwd_pair, H_k / M_k from the factorisation, u_k in S1, v_k in V) --
+    over several QPs of both intent buckets, and with a small initial rho whose adaptive updates
+    refactorise in-kernel (H_k, M_k rebuilt)."""
+    s = impc.default_settings(rho=rho, **S25)
+    for name in ("config3_K8", "config2"):
+        cfg = take(CFG[name], 2)
+        res, ref = emulate(cfg, s), oracle(cfg, s)
+        compare(res, ref)
+        if rho < 0.1:
+            assert ref[2]["rho_updates"].max() >= 1

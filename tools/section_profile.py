@@ -24,7 +24,7 @@ NAMES = ["setup", "factor", "warm", "rhs", "S1", "fwd", "S3", "bwd", "S5", "upda
 
 def main():
     inst = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
-    assert impc.LIB_PATH.endswith("_prof.so")
+    assert "prof" in os.path.basename(impc.LIB_PATH)
     impc.lib.impc_debug_sections.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
     buckets = scenarios.intent_config(instances=inst, seed=3000)
     ctx = impc.Context(0)
