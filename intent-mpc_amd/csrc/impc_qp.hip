@@ -360,7 +360,7 @@ struct GroupEntry {
 // Several structured batches in one persistent launch: one work queue over all their QPs, so
 // the long-running QPs at the end of one batch overlap the next batch's work instead of leaving
 // CUs idle between launches.  A workgroup reloads the pattern tables when it crosses batches.
-template <int NL, int VS, int GS, int WPS, int WF>
+template <int NL, int VS, int GS, int WPS, int WF, bool TIER>
 __global__ __launch_bounds__(NL, WPS) void k_mpc_wave_group(const GroupEntry *__restrict__ g, int count,
                                                             int64_t total, unsigned *counter) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -377,10 +377,10 @@ __global__ __launch_bounds__(NL, WPS) void k_mpc_wave_group(const GroupEntry *__
         int e = 0;
         while (e + 1 < count && (int64_t)b >= g[e + 1].first) e++;
         if (e != cur) {
-            impc::WaveQP<GpuTeam<NL>, NL, VS, GS, WF>::load_tables(wv, g[e].T, smem);
+            impc::WaveQP<GpuTeam<NL>, NL, VS, GS, WF, TIER>::load_tables(wv, g[e].T, smem);
             cur = e;
         }
-        impc::WaveQP<GpuTeam<NL>, NL, VS, GS, WF> qp(wv, g[e].T, g[e].io, g[e].st, smem);
+        impc::WaveQP<GpuTeam<NL>, NL, VS, GS, WF, TIER> qp(wv, g[e].T, g[e].io, g[e].st, smem);
         qp.solve((int64_t)b - g[e].first);
     }
 }
@@ -496,6 +496,7 @@ struct impc_batch_s {
     // ---- structured path
     std::unique_ptr<impc::MpcStructure> ms;
     bool structured_ok = false;
+    bool tier = false;  // two-tier products layout (grouped-kernel instances only)
     int gs = 0;  // general-row slots per lane of the structured kernel
     int vs = 1;  // variable slots per lane (kWaveVS, or kWaveVSLong for long horizons)
     void *d_tables = nullptr;
@@ -775,7 +776,7 @@ template <int VS, int GS, int WF>
 int launch_wave_w(impc_batch b, hipStream_t st, const impc::WaveIO &io) {
     constexpr int WPS = VS == kWaveVS ? IMPC_WAVES_PER_SIMD : 1;
     using LD = impc::WaveLds<kTeam, VS, GS>;
-    const size_t lds = sizeof(double) * (size_t)LD::size(b->ms->CG, b->ms->n);  // products sized by the pattern
+    const size_t lds = sizeof(double) * (size_t)LD::size(b->wt);  // products sized by the pattern
     if (int rc = ensure_lds_attr(k_mpc_wave<kTeam, VS, GS, WPS, WF>, lds)) return rc;
     const int64_t groups = resident_groups<VS>(b->ctx->num_cu, lds, b->B);
     hipLaunchKernelGGL((k_mpc_wave<kTeam, VS, GS, WPS, WF>), dim3((unsigned)groups), dim3(kTeam), lds, st, b->wt, io,
@@ -798,6 +799,7 @@ void structured_solved(impc_batch b) {
 }
 
 int structured_solve(impc_batch b, hipStream_t st) {
+    if (b->tier) return impc_batch_solve_group(&b, 1, st);  // the two-tier instances are grouped ones
     impc::WaveIO io = wave_io(b);
     HIP_OK(hipMemsetAsync(b->d_counter, 0, 256, st));
 #ifdef IMPC_SECTION_PROF
@@ -829,30 +831,29 @@ int structured_solve(impc_batch b, hipStream_t st) {
     return IMPC_OK;
 }
 
-template <int VS, int GS, int WF>
-int launch_group_w(impc_ctx ctx, hipStream_t st, int count, int64_t total, int maxCG, int maxN, unsigned *counter) {
+template <int VS, int GS, int WF, bool TIER>
+int launch_group_w(impc_ctx ctx, hipStream_t st, const GroupEntry *entries, int count, int64_t total, size_t lds,
+                   unsigned *counter) {
     constexpr int WPS = VS == kWaveVS ? IMPC_WAVES_PER_SIMD : 1;
-    using LD = impc::WaveLds<kTeam, VS, GS>;
-    const size_t lds = sizeof(double) * (size_t)LD::size(maxCG, maxN);
-    if (int rc = ensure_lds_attr(k_mpc_wave_group<kTeam, VS, GS, WPS, WF>, lds)) return rc;
+    if (int rc = ensure_lds_attr(k_mpc_wave_group<kTeam, VS, GS, WPS, WF, TIER>, lds)) return rc;
     const int64_t groups = resident_groups<VS>(ctx->num_cu, lds, total);
-    hipLaunchKernelGGL((k_mpc_wave_group<kTeam, VS, GS, WPS, WF>), dim3((unsigned)groups), dim3(kTeam), lds, st,
-                       ctx->d_group, count, total, counter);
+    hipLaunchKernelGGL((k_mpc_wave_group<kTeam, VS, GS, WPS, WF, TIER>), dim3((unsigned)groups), dim3(kTeam), lds, st,
+                       entries, count, total, counter);
     HIP_OK(hipGetLastError());
     return IMPC_OK;
 }
 // spec: every batch of the group has the shape's default horizon
-template <int VS, int GS>
-int launch_group(impc_ctx ctx, hipStream_t st, int count, int64_t total, int maxCG, int maxN, unsigned *counter,
-                 bool spec) {
+template <int VS, int GS, bool TIER = false>
+int launch_group(impc_ctx ctx, hipStream_t st, const GroupEntry *entries, int count, int64_t total, size_t lds,
+                 unsigned *counter, bool spec) {
     constexpr int WS = impc::WaveLds<kTeam, VS, GS>::WSPEC;
-    return spec ? launch_group_w<VS, GS, WS>(ctx, st, count, total, maxCG, maxN, counter)
-                : launch_group_w<VS, GS, 0>(ctx, st, count, total, maxCG, maxN, counter);
+    return spec ? launch_group_w<VS, GS, WS, TIER>(ctx, st, entries, count, total, lds, counter)
+                : launch_group_w<VS, GS, 0, TIER>(ctx, st, entries, count, total, lds, counter);
 }
 
 // dynamic LDS bytes of the structured kernel for a shape (team VS, GS) and pattern (CG, n)
-size_t wave_lds_bytes(int vs, int gs, int CG, int n) {
-    auto sz = [&](auto ld) { return sizeof(double) * (size_t)decltype(ld)::size(CG, n); };
+size_t wave_lds_bytes(int vs, int gs, const impc::WaveTables &T) {
+    auto sz = [&](auto ld) { return sizeof(double) * (size_t)decltype(ld)::size(T); };
     if (vs == kWaveVS)
         return gs == 2 ? sz(impc::WaveLds<kTeam, kWaveVS, 2>{}) : gs == 3 ? sz(impc::WaveLds<kTeam, kWaveVS, 3>{})
                                                                           : sz(impc::WaveLds<kTeam, kWaveVS, 4>{});
@@ -870,14 +871,37 @@ int prepare_structured(impc_batch b) {
     b->vs = b->ms->n <= kTeam * kWaveVS ? kWaveVS : kWaveVSLong;
     const int mg = b->ms->mg;
     b->gs = mg <= 2 * kTeam ? 2 : mg <= 3 * kTeam ? 3 : mg <= 4 * kTeam ? 4 : 0;
-    if (!b->gs || wave_lds_bytes(b->vs, b->gs, b->ms->CG, b->ms->n) > 160 * 1024 - 1024) {
+    const impc::MpcStructure &s = *b->ms;
+    impc::WaveTables &t = b->wt;
+    t.n = s.n;
+    t.m = s.m;
+    t.mg = s.mg;
+    t.N = s.N;
+    t.W = s.W;
+    t.CG = s.CG;
+    t.nnzP = s.nnzP;
+    t.nnzA = s.nnzA;
+    // products layout (mpc_wave.hpp WaveLds): one tier unless it would cost the shape a resident
+    // team per CU, then the heavy columns' overflow in a second tier
+    t.HS = 0;
+    t.T1r = impc::WaveLds<kTeam, kWaveVS, 2>::cg4(s.CG);
+    // (two-tier instances: the one-variable-per-lane shape with 2 or 3 general-row slots)
+    if (b->gs && b->vs == kWaveVS && b->gs <= 3) {
+        const int per_cu = std::max(1, (4 * IMPC_WAVES_PER_SIMD) / (kTeam / 64));
+        const size_t budget = (160 * 1024 - 1024) / (size_t)per_cu;
+        if (wave_lds_bytes(b->vs, b->gs, t) > budget) {
+            t.HS = s.HS;
+            t.T1r = impc::kProdTier1;
+        }
+    }
+    b->tier = t.T1r < impc::WaveLds<kTeam, kWaveVS, 2>::cg4(s.CG);
+    if (!b->gs || wave_lds_bytes(b->vs, b->gs, t) > 160 * 1024 - 1024) {
         b->structured_ok = false;  // the generic kernel takes it
         return IMPC_OK;
     }
-    const impc::MpcStructure &s = *b->ms;
     std::vector<const std::vector<int32_t> *> arrs = {&s.var_orig, &s.var_pdiag, &s.var_boxrow, &s.var_boxpos,
                                                       &s.gen_row,  &s.gen_col,   &s.gen_pos,    &s.colg,
-                                                      &s.term_ptr, &s.term};
+                                                      &s.term_ptr, &s.term,      &s.col_hid};
     std::vector<size_t> offs;
     size_t tot = 0;
     for (auto *a : arrs) {
@@ -890,17 +914,9 @@ int prepare_structured(impc_batch b) {
     HIP_OK(hipMalloc(&b->d_tables, h.size() * 4));
     IMPC_TRY(h2d_sync(b->ctx->stream, b->d_tables, h.data(), h.size() * 4));
     const int32_t *base = (const int32_t *)b->d_tables;
-    impc::WaveTables &t = b->wt;
-    t.n = s.n;
-    t.m = s.m;
-    t.mg = s.mg;
-    t.N = s.N;
-    t.W = s.W;
-    t.CG = s.CG;
-    t.nnzP = s.nnzP;
-    t.nnzA = s.nnzA;
     const int32_t **dst_ptrs[] = {&t.var_orig, &t.var_pdiag, &t.var_boxrow, &t.var_boxpos, &t.gen_row,
-                                  &t.gen_col,  &t.gen_pos,   &t.colg,       &t.term_ptr,   &t.term};
+                                  &t.gen_col,  &t.gen_pos,   &t.colg,       &t.term_ptr,   &t.term,
+                                  &t.col_hid};
     for (size_t k = 0; k < arrs.size(); k++) *dst_ptrs[k] = base + offs[k];
     // per-QP HBM scratch for the scaling vectors: long-horizon shape only (the default shape keeps
     // them in LDS, mpc_wave.hpp WaveLds::ONCHIP)
@@ -1260,37 +1276,56 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
     impc_batch b0 = bs[0];
     if (!b0) return fail(IMPC_INVALID_ARGUMENT, "null batch");
     impc_ctx ctx = b0->ctx;
-    int gs = 0, maxCG = 1, maxN = 1;
-    bool spec = true;
     for (int k = 0; k < count; k++) {
         impc_batch b = bs[k];
         if (!b || b->ctx != ctx) return fail(IMPC_INVALID_ARGUMENT, "group batches must share a context");
         if (!b->values_set) return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "values not set");
         if (!use_structured(b) || b->vs != b0->vs)
             return fail(IMPC_UNSUPPORTED, "grouped solves need structured batches of one team shape");
-        gs = std::max(gs, b->gs);
-        maxCG = std::max(maxCG, b->ms->CG);
-        maxN = std::max(maxN, b->ms->n);
-        spec = spec && b->ms->W == (b->vs == kWaveVS ? impc::WaveLds<kTeam, kWaveVS, 2>::WSPEC
-                                                     : impc::WaveLds<kTeam, kWaveVSLong, 2>::WSPEC);
     }
+    // One persistent launch per kernel class (general-row slots per lane, GS): a bucket never runs
+    // in a wider instance than it needs (more registers, spills) and each launch's LDS is sized by
+    // its own batches, so mixed obstacle counts (config 4, K = 0..21) keep the narrow kernel at two
+    // QPs per CU for most buckets.  Classes run back to back on the stream, entries contiguous.
+    std::vector<int> order((size_t)count);
+    for (int k = 0; k < count; k++) order[(size_t)k] = k;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+        return bs[x]->gs != bs[y]->gs ? bs[x]->gs < bs[y]->gs : (int)bs[x]->tier < (int)bs[y]->tier;
+    });
+    struct Launch {
+        int gs;
+        bool tier;
+        int first, count;
+        int64_t total;
+        size_t lds;
+        bool spec;
+        unsigned *counter;
+    };
+    std::vector<Launch> launches;
     HIP_OK(hipSetDevice(ctx->device));
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
     std::vector<GroupEntry> entries((size_t)count);
     std::memset((void *)entries.data(), 0, sizeof(GroupEntry) * (size_t)count);  // comparable bytes
-    int64_t total = 0;
-    for (int k = 0; k < count; k++) {
-        impc_batch b = bs[k];
-        GroupEntry &e = entries[(size_t)k];
+    for (int p = 0; p < count; p++) {
+        impc_batch b = bs[order[(size_t)p]];
+        if (launches.empty() || launches.back().gs != b->gs || launches.back().tier != b->tier)
+            launches.push_back(Launch{b->gs, b->tier, p, 0, 0, 0, true, b->d_counter});
+        Launch &L = launches.back();
+        L.count++;
+        L.lds = std::max(L.lds, wave_lds_bytes(b->vs, b->gs, b->wt));
+        L.spec = L.spec && b->ms->W == (b->vs == kWaveVS ? impc::WaveLds<kTeam, kWaveVS, 2>::WSPEC
+                                                         : impc::WaveLds<kTeam, kWaveVSLong, 2>::WSPEC);
+        GroupEntry &e = entries[(size_t)p];
         e.T = b->wt;
         e.io = wave_io(b);
         e.st = b->dst;
-        e.first = total;
-        total += b->B;
+        e.first = L.total;
+        L.total += b->B;
         b->ev_solve = false;
         b->ev_setup = false;
     }
-    if (total == 0) return IMPC_OK;
+    for (const Launch &L : launches)
+        if (L.lds > 160 * 1024 - 1024) return fail(IMPC_UNSUPPORTED, "grouped batches exceed the LDS of a CU");
     // upload the entries only when they change (repeated solves of one group launch back to back);
     // the device copy must not change under an in-flight kernel, so an update first waits for every
     // launch on every stream this context has used
@@ -1308,19 +1343,25 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
         ctx->h_group = entries;
     }
     IMPC_TRY(ctx_order_launch(ctx, st));
-    HIP_OK(hipMemsetAsync(b0->d_counter, 0, 256, st));
     if (b0->profile) HIP_OK(hipEventRecord(b0->ev[2], st));
-    int rc;
-    switch (b0->vs * 8 + gs) {
-        case kWaveVS * 8 + 2: rc = launch_group<kWaveVS, 2>(ctx, st, count, total, maxCG, maxN, b0->d_counter, spec); break;
-        case kWaveVS * 8 + 3: rc = launch_group<kWaveVS, 3>(ctx, st, count, total, maxCG, maxN, b0->d_counter, spec); break;
-        case kWaveVS * 8 + 4: rc = launch_group<kWaveVS, 4>(ctx, st, count, total, maxCG, maxN, b0->d_counter, spec); break;
-        case kWaveVSLong * 8 + 2: rc = launch_group<kWaveVSLong, 2>(ctx, st, count, total, maxCG, maxN, b0->d_counter, spec); break;
-        case kWaveVSLong * 8 + 3: rc = launch_group<kWaveVSLong, 3>(ctx, st, count, total, maxCG, maxN, b0->d_counter, spec); break;
-        case kWaveVSLong * 8 + 4: rc = launch_group<kWaveVSLong, 4>(ctx, st, count, total, maxCG, maxN, b0->d_counter, spec); break;
-        default: return fail(IMPC_UNSUPPORTED, "no structured kernel for this size");
+    for (const Launch &L : launches) {
+        if (L.total == 0) continue;
+        HIP_OK(hipMemsetAsync(L.counter, 0, 256, st));
+        const GroupEntry *E = ctx->d_group + L.first;
+        int rc;
+        switch (b0->vs * 8 + L.gs + (L.tier ? 64 : 0)) {
+            case 64 + kWaveVS * 8 + 2: rc = launch_group<kWaveVS, 2, true>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec); break;
+            case 64 + kWaveVS * 8 + 3: rc = launch_group<kWaveVS, 3, true>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec); break;
+            case kWaveVS * 8 + 2: rc = launch_group<kWaveVS, 2>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec); break;
+            case kWaveVS * 8 + 3: rc = launch_group<kWaveVS, 3>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec); break;
+            case kWaveVS * 8 + 4: rc = launch_group<kWaveVS, 4>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec); break;
+            case kWaveVSLong * 8 + 2: rc = launch_group<kWaveVSLong, 2>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec); break;
+            case kWaveVSLong * 8 + 3: rc = launch_group<kWaveVSLong, 3>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec); break;
+            case kWaveVSLong * 8 + 4: rc = launch_group<kWaveVSLong, 4>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec); break;
+            default: return fail(IMPC_UNSUPPORTED, "no structured kernel for this size");
+        }
+        if (rc) return rc;
     }
-    if (rc) return rc;
     IMPC_TRY(ctx_note_launch(ctx, st));
     for (int k = 0; k < count; k++) structured_solved(bs[k]);
     if (b0->profile) {

@@ -86,6 +86,10 @@ std::string MpcStructure::analyse(int64_t n64, int64_t m64, const int64_t *Pp, c
     colg.assign((size_t)n * CG, -1);
     for (int32_t v = 0; v < n; v++)
         for (size_t t = 0; t < cl[v].size(); t++) colg[(size_t)v * CG + t] = cl[v][t];
+    HS = 0;
+    col_hid.assign((size_t)n, -1);
+    for (int32_t v = 0; v < n; v++)
+        if ((int32_t)cl[v].size() > kProdTier1) col_hid[(size_t)v] = HS++;
     // factorisation assembly program: per stage k and destination d (M_kk[r][c] at 13r+c,
     // B_k[i][c] at 169+13i+c) the (g, e, f) triples of rho_g a_ge a_gf
     std::vector<std::vector<int32_t>> dest((size_t)N * kStageDests);

@@ -26,6 +26,11 @@ struct MpcStructure {
     std::vector<int32_t> gen_row;                                      // [mg]
     std::vector<int32_t> gen_col, gen_pos;                             // [4 mg], stage-order col / CSC slot, -1 pad
     std::vector<int32_t> colg;                                         // [n * CG] entry ids g*4+e, -1 pad
+    // products buffer of the structured kernel (mpc_wave.hpp): every column has kProdTier1 slots
+    // in the first tier; the HS columns with more general entries ("heavy": the positions and the
+    // slack of a stage with obstacle rows) continue in a second tier, at their index col_hid
+    int32_t HS = 0;
+    std::vector<int32_t> col_hid;                                      // [n], -1 for light columns
     std::vector<int32_t> term_ptr, term;                               // factorisation assembly program
     // Returns "" when the pattern is stage-structured, else the reason it is not.
     std::string analyse(int64_t n, int64_t m, const int64_t *Pp, const int64_t *Pi, const int64_t *Ap,
@@ -33,5 +38,6 @@ struct MpcStructure {
 };
 
 constexpr int kStageDests = 13 * 13 + 8 * 13;  // M_kk (13x13) + coupling B_k (8x13)
+constexpr int kProdTier1 = 4;                  // first-tier product slots per column
 
 }  // namespace impc

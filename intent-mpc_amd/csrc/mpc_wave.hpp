@@ -81,6 +81,9 @@ struct WaveTables {
     int32_t n, m, mg, N, W, CG, nnzP, nnzA;
     const int32_t *var_orig, *var_pdiag, *var_boxrow, *var_boxpos;
     const int32_t *gen_row, *gen_col, *gen_pos, *colg, *term_ptr, *term;
+    int32_t HS;               // heavy columns (second products tier), MpcStructure::HS; 0: one tier
+    const int32_t *col_hid;   // [n] heavy-column index or -1 (stage order)
+    int32_t T1r;              // first-tier rows: cg4(CG) (one tier) or kProdTier1 (two tiers)
 };
 
 struct WaveIO {
@@ -183,25 +186,33 @@ struct WaveLds {
     static constexpr int XF_OFF = RED_OFF + 8;              // forward: a^_{S(c+1)-1}, c = 0..2
     static constexpr int XB_OFF = RED_OFF + 32;             // backward: x^_{S(c)}, c = 1..3
     static constexpr int CGM = 24;                          // max general entries per column
-    // products region: entry t of column v at t * stride(n) + v (stride = n rounded up to 64), so a
-    // column's gather is CG4 independent conflict-free reads; it doubles as the factorisation's
-    // (4g + e) scratch.  Sized from the pattern at run time, followed by 8 discard slots (index
-    // p_size).
+    // products region: entry t < T1r of column v at t * stride(n) + v (stride = n rounded up to
+    // 64, plus a pad), so a column's gather is independent, conflict-free reads.  When that one
+    // tier (T1r = CG4 rows of all n columns) would cost occupancy, a second tier holds the rest:
+    // T1r = 4 and entry t >= 4 of a heavy column (index h = col_hid) at
+    // 4 stride(n) + (t - 4)(HS + 1) + h -- only the positions and slack of a stage carry one
+    // product per obstacle row, so the second tier is (CG4 - 4) rows of the HS heavy columns
+    // instead of CG4 rows of all n (K = 21: 21 KB instead of 49 KB).  It doubles as the
+    // factorisation's (4g + e) scratch and general-row rho.  Sized from the pattern at run time,
+    // followed by 8 discard slots (index p_size).
+    static constexpr int T1 = kProdTier1;
     static IMPC_WF int cg4(int CG) { return (CG + 3) & ~3; }
     // +PAD: the obstacle rows of one stage write their products to the same column in different
     // entry slots; a stride that is not a multiple of 16 doubles puts those ds_write_b64 (bank =
     // dword mod 32, 16-lane groups) on distinct banks.  Reads stay lane-contiguous.
     static IMPC_WF int stride(int n) { return ((n + 63) & ~63) + IMPC_PSTRIDE_PAD; }
     // the factorisation uses it as (4g + e) scratch followed by the general rows' rho (RHOG_P)
-    static IMPC_WF int p_size(int CG, int n) {
-        const int c = cg4(CG) * stride(n), f = 5 * NL * GS;
+    static IMPC_WF int hsp(int HS) { return HS + 1; }  // second-tier row length
+    static IMPC_WF int p_size(int CG, int n, int HS, int mg, int T1r) {
+        const int c = T1r * stride(n) + (cg4(CG) > T1r ? (cg4(CG) - T1r) * hsp(HS) : 0), f = 5 * mg;
         return c > f ? c : f;
     }
-    static IMPC_WF int size(int CG, int n) { return P_OFF + p_size(CG, n) + 8; }
+    static IMPC_WF int p_size(const WaveTables &T) { return p_size(T.CG, T.n, T.HS, T.mg, T.T1r); }
+    static IMPC_WF int size(const WaveTables &T) { return P_OFF + p_size(T) + 8; }
     // factorisation aliases (inside R..X region and the products buffer)
     static constexpr int FA = R_OFF, FL = FA + 169, FI = FL + 169, FB = FI + 169, FG = FB + 104, FE = FG + 104,
                          DIAGX = FE + 64;
-    static constexpr int RHOG_P = 4 * NL * GS;  // general rows' rho, inside the products region
+    // general rows' rho during the factorisation: products region + 4 mg
     static_assert(DIAGX + NMAX <= RED_OFF, "factorisation scratch does not fit");
 };
 
@@ -246,7 +257,9 @@ IMPC_WF double prod_nc(double a, double b) {
 // WF: the stage count W fixed at compile time (LD::WSPEC, the default horizon: every stage loop
 // and LDS offset becomes a constant and no runtime-W code path shares the kernel's registers), or 0
 // for any W read from the tables.
-template <class WV, int NL, int VS, int GS, int WF = 0>
+// TIER: the batch uses the two-tier products layout (WaveLds, T1r = kProdTier1); a one-tier
+// batch (T1r = CG4) runs the TIER = false instance, whose gathers are the plain CG4-row loops.
+template <class WV, int NL, int VS, int GS, int WF = 0, bool TIER = false>
 struct WaveQP {
     using LD = WaveLds<NL, VS, GS>;
     static_assert(WF == 0 || WF == LD::WSPEC, "WF is 0 or the shape's default horizon");
@@ -260,7 +273,7 @@ struct WaveQP {
     // ---- variable slots
     double x[VS], q[VS], pd[VS], ab[VS], zb[VS], yb[VS], lb[VS], ub[VS], dxv_[VS], dyb_[VS];
     double ainv[VS][13], cp[VS][8];
-    int bt[VS], vs_[VS], vr_[VS];
+    int bt[VS], vs_[VS], vr_[VS], hid_[VS];
     bool vok[VS];
     // ---- general-row slots
     double a[GS][4], z[GS], y[GS], lg[GS], ug[GS], dyg_[GS];
@@ -349,6 +362,7 @@ struct WaveQP {
             vok[s] = v < n;
             vs_[s] = vok[s] ? v / 13 : 0;
             vr_[s] = vok[s] ? v % 13 : 0;
+            hid_[s] = TIER && vok[s] ? T.col_hid[v] : -1;  // second products tier (TIER batches)
             x[s] = q[s] = pd[s] = ab[s] = zb[s] = yb[s] = lb[s] = ub[s] = dxv_[s] = dyb_[s] = 0.0;
             bt[s] = 0;
             if (vok[s]) {
@@ -368,7 +382,7 @@ struct WaveQP {
             z[s] = y[s] = lg[s] = ug[s] = dyg_[s] = 0.0;
             gt[s] = 0;
             const int16_t *gs = (const int16_t *)(lds + LD::GSLOT_OFF);
-            const int pz = LD::p_size(T.CG, T.n);
+            const int pz = LD::p_size(T);
             _Pragma("unroll") for (int e = 0; e < 4; e++) {
                 a[s][e] = 0.0;
                 gc[s][e] = (pz << 16) | LD::NMAX;  // discard slot / zero tail of the x exchange
@@ -397,21 +411,23 @@ struct WaveQP {
     // the discard slot), and a zeroed products region (slots no entry maps to must read 0).
     static IMPC_WF void load_tables(WV &w, const WaveTables &T, double *lds) {
         int16_t *gs = (int16_t *)(lds + LD::GSLOT_OFF);
-        const int pz = LD::p_size(T.CG, T.n);
+        const int pz = LD::p_size(T);
         for (int e = w.lane(); e < 4 * NL * GS; e += NL) gs[e] = (int16_t)pz;
         double *pb = lds + LD::P_OFF;
         for (int e = w.lane(); e < pz + 8; e += NL) pb[e] = 0.0;
         w.sync();
         for (int e = w.lane(); e < T.n * T.CG; e += NL) {
             const int v = e / T.CG, t = e % T.CG, id = T.colg[e];
-            if (id >= 0) gs[id] = (int16_t)(t * LD::stride(T.n) + v);
+            if (id >= 0)
+                gs[id] = (int16_t)(t < T.T1r ? t * LD::stride(T.n) + v
+                                             : T.T1r * LD::stride(T.n) + (t - T.T1r) * LD::hsp(T.HS) + T.col_hid[v]);
         }
         w.sync();
     }
 
     IMPC_WF void zero_products() {
         double *pb = pbuf();
-        const int cnt = LD::p_size(T.CG, T.n) + 8;
+        const int cnt = LD::p_size(T) + 8;
         for (int i = L; i < cnt; i += NL) pb[i] = 0.0;
         wv.sync();
     }
@@ -420,22 +436,41 @@ struct WaveQP {
     IMPC_WF int gcol(int s, int e) const { return gc[s][e] & 0xFFFF; }
     IMPC_WF int gdst(int s, int e) const { return gc[s][e] >> 16; }
 
-    // gather sum over the general entries of column v (column-slot layout, independent reads)
-    IMPC_WF double col_gather(int v) {
+    // gather sum over the general entries of column v (column-slot layout, independent reads;
+    // the sums add groups of four in entry order).  TIER: the first T1 rows, then -- for a heavy
+    // column, h = its second-tier index (hid_, -1 for a light column) -- the second tier
+    IMPC_WF double col_gather(int v, int h) {
         const double *pb = pbuf() + v;
         const int C4 = LD::cg4(T.CG), sd = LD::stride(T.n);
         double s = 0.0;
-        for (int t = 0; t < C4; t += 4) {
-            const double p0 = pb[t * sd], p1 = pb[(t + 1) * sd], p2 = pb[(t + 2) * sd], p3 = pb[(t + 3) * sd];
-            s += (p0 + p1) + (p2 + p3);
+        if constexpr (!TIER) {
+            (void)h;
+            for (int t = 0; t < C4; t += 4) {
+                const double p0 = pb[t * sd], p1 = pb[(t + 1) * sd], p2 = pb[(t + 2) * sd], p3 = pb[(t + 3) * sd];
+                s += (p0 + p1) + (p2 + p3);
+            }
+        } else {
+            static_assert(LD::T1 == 4, "one first-tier group");
+            s += (pb[0] + pb[sd]) + (pb[2 * sd] + pb[3 * sd]);
+            if (h >= 0) {
+                const int hp = LD::hsp(T.HS);
+                const double *q = pbuf() + LD::T1 * sd + h;
+                for (int t = 0; t < C4 - LD::T1; t += 4)
+                    s += (q[t * hp] + q[(t + 1) * hp]) + (q[(t + 2) * hp] + q[(t + 3) * hp]);
+            }
         }
         return s;
     }
-    IMPC_WF double col_gather_max(int v) {
+    IMPC_WF double col_gather_max(int v, int h) {
         const double *pb = pbuf() + v;
         const int C4 = LD::cg4(T.CG), sd = LD::stride(T.n);
         double s = 0.0;
-        for (int t = 0; t < C4; t++) s = dmax(pb[t * sd], s);
+        for (int t = 0; t < (TIER ? LD::T1 : C4); t++) s = dmax(pb[t * sd], s);
+        if (TIER && h >= 0) {
+            const int hp = LD::hsp(T.HS);
+            const double *q = pbuf() + LD::T1 * sd + h;
+            for (int t = 0; t < C4 - LD::T1; t++) s = dmax(q[t * hp], s);
+        }
         return s;
     }
 
@@ -461,7 +496,7 @@ struct WaveQP {
                 // colnorm_sym(P) (diagonal), max with colnorm(A) = max(box, general entries)
                 double d = fabs(pd[s]);
                 double an = dmax(fabs(ab[s]), 0.0);
-                if (vok[s]) an = dmax(col_gather_max(NL * s + L), an);
+                if (vok[s]) an = dmax(col_gather_max(NL * s + L, hid_[s]), an);
                 d = dmax(d, an);
                 d = d < kMinScaling ? 1.0 : d;
                 d = d > kMaxScaling ? kMaxScaling : d;
@@ -548,7 +583,7 @@ struct WaveQP {
     // Returns 1 if a pivot is not positive (OSQP_NONCVX_ERROR).
     IMPC_WF int factorize() {
         const int n = T.n, W = Wst(), N = W + 1;
-        double *w = pbuf(), *rhog = pbuf() + LD::RHOG_P, *diagx = lds + LD::DIAGX;
+        double *w = pbuf(), *rhog = pbuf() + 4 * T.mg, *diagx = lds + LD::DIAGX;
         const bool pair = LD::PAIR && W == LD::WSPEC;
         double *A = lds + LD::FA, *Li = lds + LD::FL, *Ai = lds + LD::FI, *Bb = lds + LD::FB, *G = lds + LD::FG,
                *E = lds + LD::FE, *Fm = F();
@@ -1255,7 +1290,7 @@ struct WaveQP {
                 double vb = rhob(s) * zb[s] - yb[s];
                 double r = sigma * x[s] - q[s];
                 r += ab[s] * vb;
-                r += col_gather(v);
+                r += col_gather(v, hid_[s]);
                 rb[v] = r;
             }
             wv.lsync();
@@ -1470,7 +1505,7 @@ struct WaveQP {
         double dr_u = 0, q_u = 0, aty_u = 0, px_u = 0, dr_p = 0, q_p = 0, aty_p = 0, px_p = 0;
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (!vok[s]) continue;
-            double aty = ab[s] * yb[s] + col_gather(NL * s + L);
+            double aty = ab[s] * yb[s] + col_gather(NL * s + L, hid_[s]);
             double px = pd[s] * x[s];
             double r = q[s] + 1 * px;
             r = r + 1 * aty;
@@ -1547,7 +1582,7 @@ struct WaveQP {
             double mx = 0.0;
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
                 if (!vok[s]) continue;
-                double t = ab[s] * dyb(s) + col_gather(NL * s + L);
+                double t = ab[s] * dyb(s) + col_gather(NL * s + L, hid_[s]);
                 if (unsc) t = (1. / D[s]) * t;
                 mx = dmax(mx, fabs(t));
             }

@@ -96,18 +96,18 @@ struct EmuWave {
     }
 };
 
-template <int VS, int GS, int WF>
+template <int VS, int GS, int WF, bool TIER>
 void run_w(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSettings &st) {
     using LD = impc::WaveLds<NL, VS, GS>;
-    std::vector<double> lds((size_t)LD::size(T.CG, T.n), 0.0);
+    std::vector<double> lds((size_t)LD::size(T), 0.0);
     EmuShared sh;
     std::vector<std::thread> th;
     for (int l = 0; l < NL; l++)
         th.emplace_back([&, l] {
             EmuWave wv{l, &sh};
-            impc::WaveQP<EmuWave, NL, VS, GS, WF>::load_tables(wv, T, lds.data());
+            impc::WaveQP<EmuWave, NL, VS, GS, WF, TIER>::load_tables(wv, T, lds.data());
             for (int64_t b = 0; b < io.B; b++) {
-                impc::WaveQP<EmuWave, NL, VS, GS, WF> qp(wv, T, io, st, lds.data());
+                impc::WaveQP<EmuWave, NL, VS, GS, WF, TIER> qp(wv, T, io, st, lds.data());
                 qp.solve(b);
             }
         });
@@ -118,10 +118,11 @@ void run_w(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSet
 template <int VS, int GS>
 void run(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSettings &st) {
     constexpr int WS = impc::WaveLds<NL, VS, GS>::WSPEC;
+    const bool tier = T.T1r < impc::WaveLds<NL, VS, GS>::cg4(T.CG);
     if (T.W == WS)
-        run_w<VS, GS, WS>(T, io, st);
+        tier ? run_w<VS, GS, WS, true>(T, io, st) : run_w<VS, GS, WS, false>(T, io, st);
     else
-        run_w<VS, GS, 0>(T, io, st);
+        tier ? run_w<VS, GS, 0, true>(T, io, st) : run_w<VS, GS, 0, false>(T, io, st);
 }
 
 }  // namespace
@@ -135,7 +136,10 @@ extern "C" int emu_wave_solve_batch(int64_t n, int64_t m, const int64_t *Pp, con
     impc::WaveTables T{ms.n, ms.m, ms.mg, ms.N, ms.W, ms.CG, ms.nnzP, ms.nnzA,
                        ms.var_orig.data(), ms.var_pdiag.data(), ms.var_boxrow.data(), ms.var_boxpos.data(),
                        ms.gen_row.data(), ms.gen_col.data(), ms.gen_pos.data(), ms.colg.data(),
-                       ms.term_ptr.data(), ms.term.data()};
+                       ms.term_ptr.data(), ms.term.data(), ms.HS, ms.col_hid.data(), impc::kProdTier1};
+    // the emulation takes the two-tier products layout whenever the pattern has heavy columns (the
+    // product uses it where one tier would cost occupancy), so both gathers are covered on the CPU
+    if (ms.HS == 0) T.T1r = impc::WaveLds<NL, 1, 2>::cg4(ms.CG);
     std::vector<double> zx((size_t)B * n, 0.0), zy((size_t)B * m, 0.0), scal((size_t)B * (2 * n + ms.mg), 0.0);
     impc::WaveIO io{B, Px, q, Ax, l, u, xws ? xws : zx.data(), yws ? yws : zy.data(), xws ? 1 : 0,
                     xo, yo, scal.data(), info};
