@@ -26,16 +26,17 @@ ORACLE  := $(ORADIR)/libosqp_oracle.so
 HARNESS := $(HARNDIR)/libimpc_core_cpu.so
 EMU     := $(HARNDIR)/libwave_emu.so
 SHIMT   := $(HARNDIR)/shim_test
+REPLANX := $(HARNDIR)/replan_example
 
 .PHONY: all lib oracle harness prof variant clean
 all: lib oracle harness
 lib: $(LIB)
 oracle: $(ORACLE)
-harness: $(HARNESS) $(EMU) $(SHIMT)
+harness: $(HARNESS) $(EMU) $(SHIMT) $(REPLANX)
 
 $(LIBDIR)/impc_qp.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symbolic.hpp $(CSRC)/mpc_wave.hpp \
 		$(CSRC)/mpc_structure.hpp $(CSRC)/select.hpp $(CSRC)/mpc_build.hpp $(CSRC)/mpc_qp_internal.hpp \
-		$(CSRC)/fanout.hpp $(CSRC)/predict.hpp $(CSRC)/comm.hpp $(ROOT)/include/impc_qp.h $(ROOT)/include/impc_select.h \
+		$(CSRC)/fanout.hpp $(CSRC)/predict.hpp $(CSRC)/comm.hpp $(CSRC)/reftraj.hpp $(ROOT)/include/impc_qp.h $(ROOT)/include/impc_select.h \
 		$(ROOT)/include/impc_mpc.h $(ROOT)/include/impc_fanout.h $(ROOT)/include/impc_predict.h $(ROOT)/include/impc_comm.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -44,7 +45,7 @@ $(LIBDIR)/impc_qp.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symbolic.
 prof: $(PROFLIB)
 $(LIBDIR)/impc_qp_prof.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symbolic.hpp $(CSRC)/mpc_wave.hpp \
 		$(CSRC)/mpc_structure.hpp $(CSRC)/select.hpp $(CSRC)/mpc_build.hpp $(CSRC)/mpc_qp_internal.hpp \
-		$(CSRC)/fanout.hpp $(CSRC)/predict.hpp $(CSRC)/comm.hpp $(ROOT)/include/impc_qp.h $(ROOT)/include/impc_select.h $(ROOT)/include/impc_mpc.h \
+		$(CSRC)/fanout.hpp $(CSRC)/predict.hpp $(CSRC)/comm.hpp $(CSRC)/reftraj.hpp $(ROOT)/include/impc_qp.h $(ROOT)/include/impc_select.h $(ROOT)/include/impc_mpc.h \
 		$(ROOT)/include/impc_fanout.h $(ROOT)/include/impc_predict.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -DIMPC_SECTION_PROF -c $< -o $@
@@ -89,6 +90,13 @@ $(EMU): $(ROOT)/tests/native/wave_emu.cpp $(CSRC)/mpc_wave.hpp $(CSRC)/admm_core
 $(SHIMT): $(ROOT)/tests/native/shim_test.cpp $(ROOT)/include/OsqpEigen/OsqpEigen.h $(LIB)
 	@mkdir -p $(HARNDIR)
 	$(CXX) -O2 -std=c++17 -Wall -I$(ROOT)/tests/native/mock_eigen -I$(ROOT)/include $< -L$(LIBDIR) -limpc_qp \
+		-Wl,-rpath,'$$ORIGIN/../../../intent-mpc_amd/lib' -o $@
+
+# batched makePlanWithPred over the C-ABI only (C++ integration example, driven by the tests)
+$(REPLANX): $(ROOT)/tests/native/replan_example.cpp $(ROOT)/include/impc_qp.h $(ROOT)/include/impc_mpc.h \
+		$(ROOT)/include/impc_fanout.h $(ROOT)/include/impc_select.h $(LIB)
+	@mkdir -p $(HARNDIR)
+	$(CXX) -O2 -std=c++17 -Wall -I$(ROOT)/include $< -L$(LIBDIR) -limpc_qp \
 		-Wl,-rpath,'$$ORIGIN/../../../intent-mpc_amd/lib' -o $@
 
 # kernel experiments (tools/ only): make variant V=name DEFS="-DX=1" -> lib/libimpc_qp_<name>.so,

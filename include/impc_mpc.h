@@ -94,6 +94,27 @@ int impc_mpc_build_values_device(impc_mpc_builder b, int64_t nb, const double *c
 int impc_mpc_warm_start(const impc_mpc_params *p, int64_t nb, const double *prev_states, const double *prev_controls,
                         double *x_ws);
 
+/* mpcPlanner::getXRef / getReferenceTraj (mpcPlanner.cpp:968-981, 1199-1231) for `ni` planning
+ * instances on the device, one thread each.  Instance i follows its input path (updatePath,
+ * :307-314): points path[path_ptr[i] .. path_ptr[i + 1]) of path (x, y, z), and its state
+ * last_idx[i] (lastRefStartIdx_; 0 after updatePath), read and updated in place.  The nearest
+ * path point to curr_pos[i] is searched in [last_idx, min(last_idx + (int)(3.0 / ts), len)) (first
+ * minimum of the Euclidean distance), then `horizon` consecutive points from there, padded with
+ * the last point, become xref[i][k] = (x, y, z, 0, 0, 0, 0, 0) -- an empty path gives curr_pos at
+ * every step (state unchanged).  DEVICE pointers: path_ptr [ni + 1] int64, path [*][3],
+ * curr_pos [ni][3], last_idx [ni] int32, xref [ni][repeat][horizon][8] (each instance's reference
+ * written `repeat` times, the layout of a replan's per-candidate copies).  Asynchronous on
+ * `stream` (NULL = the context's stream). */
+int impc_reference_traj_device(impc_ctx ctx, int32_t horizon, double ts, int64_t ni, const int64_t *path_ptr,
+                               const double *path, const double *curr_pos, int32_t *last_idx, int32_t repeat,
+                               double *xref, void *stream);
+
+/* Per-candidate copies of per-instance device rows (makePlanWithPred hands every candidate of a
+ * replan the same x0, xRef and linearisation point, mpcPlanner.cpp:609-628): dst row r * repeat + c
+ * = src row r, rows of row_bytes bytes (a multiple of 8).  Asynchronous on `stream`. */
+int impc_repeat_rows_device(impc_ctx ctx, const void *src, int64_t rows, int64_t row_bytes, int32_t repeat,
+                            void *dst, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1615,3 +1615,6 @@ int impc_copy_to_host(impc_ctx ctx, void *dst, const void *src, int64_t bytes) {
 
 // ---------------------------------------------------------------- RCCL communicator, step timer
 #include "comm.hpp"
+
+// ---------------------------------------------------------------- reference trajectory (getXRef)
+#include "reftraj.hpp"

@@ -121,6 +121,8 @@ _sig("impc_device_alloc", C.c_int, _P, C.c_int64, C.POINTER(_P))
 _sig("impc_device_free", C.c_int, _P, _P)
 _sig("impc_copy_to_device", C.c_int, _P, _P, _P, C.c_int64)
 _sig("impc_copy_to_host", C.c_int, _P, _P, _P, C.c_int64)
+_sig("impc_reference_traj_device", C.c_int, _P, C.c_int32, C.c_double, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P)
+_sig("impc_repeat_rows_device", C.c_int, _P, _P, C.c_int64, C.c_int64, C.c_int32, _P, _P)
 # include/impc_comm.h
 COMM_ID_BYTES = 128
 _sig("impc_comm_unique_id", C.c_int, C.POINTER(C.c_ubyte))
@@ -212,7 +214,7 @@ EXPORTED = [
     "impc_fanout_candidates_device", "impc_intent_params_from_config", "impc_intent_prob", "impc_intent_prob_device",
     "impc_predict_traj", "impc_predict_traj_device", "impc_minsnap_dims", "impc_minsnap_build_pattern",
     "impc_minsnap_build_values", "impc_minsnap_build_bounds", "impc_minsnap_unscale",
-    "impc_comm_unique_id", "impc_comm_create", "impc_comm_destroy", "impc_comm_allgather", "impc_comm_gather_info",
+    "impc_reference_traj_device", "impc_repeat_rows_device", "impc_comm_unique_id", "impc_comm_create", "impc_comm_destroy", "impc_comm_allgather", "impc_comm_gather_info",
     "impc_comm_max", "impc_ctx_timer_mark", "impc_ctx_timer_read",
 ]
 
@@ -571,6 +573,52 @@ class DeviceArray:
         if self.ptr:
             lib.impc_device_free(self.ctx.h, _P(self.ptr))
             self.ptr = None
+
+
+class ReferencePaths:
+    """Device state of mpcPlanner's reference tracking for `ni` planning instances: their input
+    paths (updatePath, CSR-packed) and lastRefStartIdx_; xref() runs getReferenceTraj / getXRef
+    on the device (impc_reference_traj_device) and advances the state."""
+
+    def __init__(self, ctx, paths, ts, horizon):
+        self.ctx, self.ts, self.horizon, self.ni = ctx, float(ts), int(horizon), len(paths)
+        lens = np.array([len(p) for p in paths], np.int64)
+        ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        flat = np.concatenate([np.asarray(p, np.float64).reshape(-1, 3) for p in paths]) if lens.sum() else \
+            np.zeros((1, 3))
+        self.d_ptr = DeviceArray(ctx, ptr)
+        self.d_path = DeviceArray(ctx, np.ascontiguousarray(flat))
+        self.d_last = DeviceArray(ctx, np.zeros(self.ni, np.int32))  # updatePath: lastRefStartIdx_ = 0
+
+    def xref_device(self, curr_pos_ptr, out_ptr, repeat=1, stream=None):
+        _check(lib.impc_reference_traj_device(self.ctx.h, self.horizon, self.ts, self.ni, _P(self.d_ptr.ptr),
+                                              _P(self.d_path.ptr), _P(curr_pos_ptr), _P(self.d_last.ptr),
+                                              int(repeat), _P(out_ptr), _P(stream) if stream else None),
+               "impc_reference_traj_device")
+
+    def xref(self, curr_pos, repeat=1):
+        """Host convenience: curr_pos [ni][3] -> xref [ni][repeat][horizon][8] (via the device)."""
+        cp = DeviceArray(self.ctx, np.ascontiguousarray(curr_pos, np.float64).reshape(self.ni, 3))
+        out = DeviceArray(self.ctx, (self.ni, repeat, self.horizon, 8))
+        try:
+            self.xref_device(cp.ptr, out.ptr, repeat)
+            return out.get()
+        finally:
+            cp.free()
+            out.free()
+
+    def last_idx(self):
+        return self.d_last.get()
+
+    def close(self):
+        for d in (self.d_ptr, self.d_path, self.d_last):
+            d.free()
+
+
+def repeat_rows_device(ctx, src_ptr, rows, row_bytes, repeat, dst_ptr, stream=None):
+    """impc_repeat_rows_device: dst row r * repeat + c = src row r (device pointers)."""
+    _check(lib.impc_repeat_rows_device(ctx.h, _P(src_ptr), int(rows), int(row_bytes), int(repeat), _P(dst_ptr),
+                                       _P(stream) if stream else None), "impc_repeat_rows_device")
 
 
 def comm_unique_id():

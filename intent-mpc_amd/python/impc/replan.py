@@ -13,7 +13,8 @@ import time
 
 import numpy as np
 
-from . import (Batch, DeviceArray, MpcBuilder, SelectParams, _P, _check, lib, mpc_dims, mpc_pattern, solve_group)
+from . import (Batch, DeviceArray, MpcBuilder, ReferencePaths, SelectParams, _P, _check, lib, mpc_dims, mpc_pattern,
+               repeat_rows_device, solve_group)
 
 
 class DeviceReplan:
@@ -45,19 +46,30 @@ class DeviceReplan:
                                     vals=outs))
 
     def run(self, pos, vel, xref, prev, first_time, prev_count, dyn_cur, pred_pos, pred_size, prob, timings=None):
-        """Returns dict(best_cand, cand_type, cand_slot, ob_idx, x_single, x_pair, info_single, info_pair)."""
+        """Returns dict(best_cand, cand_type, cand_slot, ob_idx, x_single, x_pair, info_single, info_pair,
+        xref).  xref: the reference of every instance [I][N][8], or an impc.ReferencePaths -- the
+        instances' input paths and reference-tracking state, whose getReferenceTraj / getXRef then
+        runs on the device (mpcPlanner.cpp:968-981, 1199-1231) from `pos`."""
         I, K, L, N = self.I, self.K, self.L, self.N
         t = {}
         t0 = time.perf_counter()
         din = [DeviceArray(self.ctx, np.ascontiguousarray(a, dt)) for a, dt in
                ((pos, np.float64), (first_time, np.int8), (prev, np.float64), (prev_count, np.int32),
                 (dyn_cur, np.float64), (pred_pos, np.float64), (pred_size, np.float64), (prob, np.float64))]
-        xref_d = DeviceArray(self.ctx, np.ascontiguousarray(xref, np.float64))
-        # per-candidate copies of the instance inputs: 4 single-intent, 2 two-intent candidates
+        if isinstance(xref, ReferencePaths):
+            xref_d = DeviceArray(self.ctx, (I, N, 8))
+            xref.xref_device(din[0].ptr, xref_d.ptr)
+        else:
+            xref_d = DeviceArray(self.ctx, np.ascontiguousarray(xref, np.float64))
+        vel_d = DeviceArray(self.ctx, np.ascontiguousarray(vel, np.float64))
+        # per-candidate copies of the instance inputs on the device: 4 single-intent, 2 two-intent
         rep = {}
         for cnt in (4, 2):
-            rep[cnt] = [DeviceArray(self.ctx, np.ascontiguousarray(np.repeat(a, cnt, axis=0)))
-                        for a in (pos, vel, xref, prev)]
+            rep[cnt] = []
+            for d in (din[0], vel_d, xref_d, din[2]):
+                r = DeviceArray(self.ctx, (I * cnt,) + tuple(d.shape[1:]))
+                repeat_rows_device(self.ctx, d.ptr, I, d.nbytes // I, cnt, r.ptr)
+                rep[cnt].append(r)
         x_ws = {cnt: np.repeat(np.concatenate([prev.reshape(I, -1), np.zeros((I, 5 * (N - 1)))], axis=1), cnt, axis=0)
                 for cnt in (4, 2)}
         for sh, cnt in zip(self.shapes, (4, 2)):
@@ -98,7 +110,8 @@ class DeviceReplan:
             _P(sel["best_pos"].ptr), _P(sel["scores"].ptr), _P(sel["weighted"].ptr), None),
             "impc_select_best_device")
         self.ctx.synchronize()
-        din.append(xref_d)
+        xref_used = xref_d.get()
+        din += [xref_d, vel_d]
         slot = f["cand_slot"].get()
         t["select_s"] = time.perf_counter() - t0
         for d in din + rep[4] + rep[2]:
@@ -106,7 +119,7 @@ class DeviceReplan:
         if timings is not None:
             timings.update(t)
         out = dict(best_cand=sel["best_cand"].get(), cand_type=f["cand_type"].get(), cand_slot=slot,
-                   ob_idx=f["ob_idx"].get())
+                   ob_idx=f["ob_idx"].get(), xref=xref_used)
         for sh, nm in zip(self.shapes, ("single", "pair")):
             x, y, info = sh["batch"].get()
             out["x_" + nm], out["info_" + nm] = x, info

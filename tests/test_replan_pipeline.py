@@ -60,3 +60,91 @@ def test_device_replan_matches_host_path(ctx):
         for b in batches.values():
             b.close()
     np.testing.assert_array_equal(out["best_cand"], ref["best_cand"])
+
+
+def test_device_replan_from_paths(ctx):
+    """The replan's reference from the instances' input paths on the device (getReferenceTraj /
+    getXRef, impc.ReferencePaths) over two replans: the references equal the restatement's
+    (oracle/reftraj_ref.py, stateful lastRefStartIdx_) and the assembled gradients q equal the host
+    builder's with those references."""
+    from oracle.reftraj_ref import ReferencePath
+    I, K, N = 24, 3, 20
+    buckets = scenarios.intent_config(N=N, K=K, instances=I, hyps=6, seed=708)
+    inst = next(iter(buckets.values()))["instances"]
+    p, pd = impc.mpc_params(horizon=N)
+    L = inst["pred"].shape[3]
+    rng = np.random.default_rng(5)
+    paths = []
+    for i in range(I):
+        d = inst["xref"][i, 1, :3] - inst["xref"][i, 0, :3]
+        start = inst["pos"][i] - 5 * d
+        paths.append(start + d * np.arange(3 * N + int(rng.integers(0, 20)))[:, None])
+    refs = [ReferencePath(pth, pd["ts"], N) for pth in paths]
+    dev = impc.ReferencePaths(ctx, paths, pd["ts"], N)
+    rp = DeviceReplan(ctx, p, pd, I, K, L, impc.default_settings(verbose=0))
+    pred_size = np.broadcast_to(inst["size"], inst["pred"].shape).copy()
+    try:
+        pos = inst["pos"].copy()
+        for step in range(2):
+            out = rp.run(pos, inst["vel"], dev, inst["prev"], np.ones(I, np.int8), np.full(I, N, np.int32),
+                         inst["obp"], inst["pred"], pred_size, inst["prob_all"])
+            exp = np.array([r.xref(pos[i]) for i, r in enumerate(refs)])
+            assert np.array_equal(out["xref"], exp), step
+            rows = np.repeat(np.arange(I), 4)
+            host = impc.mpc_values(p, pos[rows], inst["vel"][rows], exp[rows], inst["prev"][rows],
+                                   dyn_pos=np.zeros((4 * I, K, L, 3)), dyn_size=np.ones((4 * I, K, L, 3)))
+            np.testing.assert_array_equal(out["vals_single"][1], host["q"])
+            pos = pos + 0.5 * inst["vel"]
+    finally:
+        rp.close()
+        dev.close()
+
+
+def test_cpp_replan_example_matches_python_replan(ctx, tmp_path):
+    """tests/native/replan_example.cpp -- the batched makePlanWithPred a C++ planner would write
+    over the C-ABI alone (fan-out, per-candidate copies, assembly, grouped solve, selection) --
+    gives bit for bit the selection and solutions of impc.replan.DeviceReplan on one scenario."""
+    import ctypes as C
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "native", "build", "replan_example")
+    I, K, N = 32, 4, 20
+    buckets = scenarios.intent_config(N=N, K=K, instances=I, hyps=6, seed=709)
+    inst = next(iter(buckets.values()))["instances"]
+    p, pd = impc.mpc_params(horizon=N)
+    L = inst["pred"].shape[3]
+    s = impc.default_settings(verbose=0)
+    pred_size = np.broadcast_to(inst["size"], inst["pred"].shape).copy()
+    first = np.ones(I, np.int8)
+    pcount = np.full(I, N, np.int32)
+    rp = DeviceReplan(ctx, p, pd, I, K, L, s)
+    try:
+        out = rp.run(inst["pos"], inst["vel"], inst["xref"], inst["prev"], first, pcount, inst["obp"], inst["pred"],
+                     pred_size, inst["prob_all"])
+    finally:
+        rp.close()
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
+    with open(fin, "wb") as f:
+        f.write(np.array([I, K, L, N, inst["prev"].shape[1]], np.int32).tobytes())
+        f.write(bytes(p))
+        f.write(bytes(s))
+        f.write(np.array([pd["dynamic_safety_dist"], pd["static_safety_dist"]]).tobytes())
+        for a, dt in ((inst["pos"], np.float64), (inst["vel"], np.float64), (inst["xref"], np.float64),
+                      (inst["prev"], np.float64), (first, np.int8), (pcount, np.int32), (inst["obp"], np.float64),
+                      (inst["pred"], np.float64), (pred_size, np.float64), (inst["prob_all"], np.float64)):
+            f.write(np.ascontiguousarray(a, dt).tobytes())
+    r = subprocess.run([exe, str(fin), str(fout)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    raw = open(fout, "rb").read()
+    best = np.frombuffer(raw[: 4 * I], np.int32)
+    np.testing.assert_array_equal(best, out["best_cand"])
+    off = 4 * I
+    for nm, cnt, kk in (("single", 4, K), ("pair", 2, K + 1)):
+        n = buckets[kk]["pattern"]["n"]
+        x = np.frombuffer(raw[off: off + 8 * cnt * I * n], np.float64).reshape(cnt * I, n)
+        off += 8 * cnt * I * n
+        it = np.frombuffer(raw[off: off + 8 * cnt * I], np.int64)
+        off += 8 * cnt * I
+        np.testing.assert_array_equal(x, out["x_" + nm])
+        np.testing.assert_array_equal(it, out["info_" + nm]["iter"])
+    assert off == len(raw)
