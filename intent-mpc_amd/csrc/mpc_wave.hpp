@@ -73,6 +73,22 @@ namespace impc {
 #ifndef IMPC_PAIR  // pair-blocked stage recursions on the default horizon (WaveLds::PAIR): built,
 #define IMPC_PAIR 0  // measured slower (profiles/r02/exp/README.md), off
 #endif
+// Scheduling hint for the parallel phases' LDS reads: under the kernel's register pressure the
+// machine scheduler otherwise issues them one ds_read2 at a time, each followed by its own
+// lgkmcnt wait (S3 = 7 serialised LDS round trips); this asks for the phase's reads first, then
+// its arithmetic, so the round trips overlap.
+#ifndef IMPC_SGB
+#define IMPC_SGB 1
+#endif
+#if IMPC_SGB && defined(__HIP_DEVICE_COMPILE__)
+#define IMPC_LOADS_FIRST(NR, NV)                            \
+    do {                                                    \
+        __builtin_amdgcn_sched_group_barrier(0x100, NR, 0); \
+        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0); \
+    } while (0)
+#else
+#define IMPC_LOADS_FIRST(NR, NV) ((void)0)
+#endif
 #ifndef IMPC_PCAP_REG  // pair sweeps: keep the stage results in registers until the sweep ends (1)
 #define IMPC_PCAP_REG 0  // or store each one as it is produced (0: measured faster, fewer spills)
 #endif
@@ -282,12 +298,18 @@ struct WaveQP {
     WaveRho R;
     double c = 1.0, cinv = 1.0;
     int rw = 0;  // the wavefront that runs the stage recursions for this QP
+    // settings / pattern scalars the ADMM iteration reads, held in registers (a grouped launch's
+    // tables and settings live in global memory: read in the loop, each is a scalar-memory round
+    // trip after every barrier)
+    double sig_, alp_;
+    int c4_, sd_;
 #if defined(IMPC_SECTION_PROF) && defined(__HIP_DEVICE_COMPILE__)
     uint64_t sec_t0 = 0, sec_acc[kSecCount] = {};
 #endif
 
     IMPC_WF WaveQP(WV &w, const WaveTables &t, const WaveIO &i, const DevSettings &s, double *l)
-        : wv(w), T(t), io(i), st(s), lds(l), L(w.lane()) {}
+        : wv(w), T(t), io(i), st(s), lds(l), L(w.lane()), sig_(s.sigma), alp_(s.alpha), c4_(LD::cg4(t.CG)),
+          sd_(LD::stride(t.n)) {}
 
     // the lane index, opaque to the optimiser: per-lane LDS addresses derived from it are formed
     // where they are used instead of being hoisted out of the ADMM loop (dozens of loop-invariant
@@ -441,7 +463,7 @@ struct WaveQP {
     // column, h = its second-tier index (hid_, -1 for a light column) -- the second tier
     IMPC_WF double col_gather(int v, int h) {
         const double *pb = pbuf() + v;
-        const int C4 = LD::cg4(T.CG), sd = LD::stride(T.n);
+        const int C4 = c4_, sd = sd_;
         double s = 0.0;
         if constexpr (!TIER) {
             (void)h;
@@ -463,7 +485,7 @@ struct WaveQP {
     }
     IMPC_WF double col_gather_max(int v, int h) {
         const double *pb = pbuf() + v;
-        const int C4 = LD::cg4(T.CG), sd = LD::stride(T.n);
+        const int C4 = c4_, sd = sd_;
         double s = 0.0;
         for (int t = 0; t < (TIER ? LD::T1 : C4); t++) s = dmax(pb[t * sd], s);
         if (TIER && h >= 0) {
@@ -1169,7 +1191,7 @@ struct WaveQP {
     template <int WC>
     IMPC_WF void fwd_sweep(const double *tb, double *rb, int W) {
         const double *Fm = lds + LD::F_OFF;
-        const int l = L & 63, i = l >> 3, j = l & 7;
+        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;  // opaque: see lane_o
         double a = tb[i];
         // (F, t) of the next even / odd step, loaded two steps ahead (reads past the last stage
         // stay inside the LDS buffers and are never used)
@@ -1194,7 +1216,7 @@ struct WaveQP {
             cap_store<true>(c0, c1, rb, WC, true, i, j);
         } else {
             // one lane per element writes, the rest write to discard slots (no divergent branch)
-            double *junk = lds + LD::JUNK_OFF + L;
+            double *junk = lds + LD::JUNK_OFF + lo;
             const bool wri = j == 0, wrj = i == 0;
             for (int k = 0; k < W; k += 2) {
                 const double f0 = fe, t0 = te;
@@ -1217,7 +1239,7 @@ struct WaveQP {
     template <bool ODD, int WC>
     IMPC_WF void bwd_sweep(const double *eb, double *xb, int W) {
         const double *Fm = lds + LD::F_OFF;
-        const int l = L & 63, i = l >> 3, j = l & 7;
+        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;
         if constexpr (WC > 0) W = WC;
         // x_W: W = (W-1)+1 has the opposite parity of the first step
         double x = eb[13 * W + (ODD ? i : j)];
@@ -1245,7 +1267,7 @@ struct WaveQP {
             }
             cap_store<ODD>(c0, c1, xb, WC, false, i, j);
         } else {
-            double *junk = lds + LD::JUNK_OFF + L;
+            double *junk = lds + LD::JUNK_OFF + lo;
             const bool wri = j == 0, wrj = i == 0;
             for (int k = W - 1; k >= 0; k -= 2) {
                 const int k2 = k - 2 > 0 ? k - 2 : 0, k3 = k - 3 > 0 ? k - 3 : 0;
@@ -1278,10 +1300,10 @@ struct WaveQP {
 
     // --------------------------------------------------------------- one ADMM iteration
     IMPC_WF void iterate(bool need_delta) {
-        const int n = T.n, W = Wst();
+        const int W = Wst();
         const bool pair = LD::PAIR && W == LD::WSPEC;
         double *rb = rbuf(), *tb = tbuf(), *eb = ebuf(), *xb = xbuf();
-        const double sigma = st.sigma, alpha = st.alpha, oma = (double)1.0 - st.alpha;
+        const double sigma = sig_, alpha = alp_, oma = (double)1.0 - alp_;
         IMPC_REP(kSecRhs) {
             // rhs = sigma x - q + A' v   (stage order)
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
@@ -1304,7 +1326,10 @@ struct WaveQP {
                 double t = rb[v];
                 if (vs_[s] > 0) {
                     const double *rp = rb + 13 * (vs_[s] - 1) + 8;
-                    _Pragma("unroll") for (int cc = 0; cc < 5; cc++) t -= cp[s][cc] * rp[cc];
+                    double rv[5];
+                    _Pragma("unroll") for (int cc = 0; cc < 5; cc++) rv[cc] = rp[cc];
+                    IMPC_LOADS_FIRST(5, 12);
+                    _Pragma("unroll") for (int cc = 0; cc < 5; cc++) t -= cp[s][cc] * rv[cc];
                 }
                 if constexpr (LD::PAIR) {
                     // pair-blocked forward: on the even stages k >= 2 the chain takes
@@ -1361,8 +1386,11 @@ struct WaveQP {
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
                 if (!vok[s]) continue;
                 const double *rk = rb + 13 * vs_[s];
+                double rv[13];
+                _Pragma("unroll") for (int cc = 0; cc < 13; cc++) rv[cc] = rk[cc];
+                IMPC_LOADS_FIRST(7, 20);
                 double e = 0.0;
-                _Pragma("unroll") for (int cc = 0; cc < 13; cc++) e += ainv[s][cc] * rk[cc];
+                _Pragma("unroll") for (int cc = 0; cc < 13; cc++) e += ainv[s][cc] * rv[cc];
                 eb[NL * s + L] = e;
             }
             wv.lsync();
@@ -1413,7 +1441,10 @@ struct WaveQP {
                 if (!vok[s] || vr_[s] < 8) continue;
                 const double *xn = xb + 13 * (vs_[s] + 1);
                 double t = eb[NL * s + L];
-                _Pragma("unroll") for (int j = 0; j < 8; j++) t -= cp[s][j] * xn[j];
+                double xv[8];
+                _Pragma("unroll") for (int j = 0; j < 8; j++) xv[j] = xn[j];
+                IMPC_LOADS_FIRST(5, 16);
+                _Pragma("unroll") for (int j = 0; j < 8; j++) t -= cp[s][j] * xv[j];
                 xb[NL * s + L] = t;
             }
             wv.lsync();
@@ -1435,10 +1466,15 @@ struct WaveQP {
             zb[s] = zn;
         }
         // general rows
+        double xg[GS][4];
+        _Pragma("unroll") for (int s = 0; s < GS; s++) {
+            _Pragma("unroll") for (int e = 0; e < 4; e++) xg[s][e] = gok[s] ? xb[gcol(s, e)] : 0.0;
+        }
+        IMPC_LOADS_FIRST(4 * GS, 8 * GS);
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
             if (!gok[s]) continue;
             double zt = 0.0;
-            _Pragma("unroll") for (int e = 0; e < 4; e++) zt += a[s][e] * xb[gcol(s, e)];
+            _Pragma("unroll") for (int e = 0; e < 4; e++) zt += a[s][e] * xg[s][e];
             double zr = alpha * zt + oma * z[s];
             double zn = dmin(dmax(zr + rhoig_(s) * y[s], lg[s]), ug[s]);
             double dy = rhog_(s) * (zr - zn);
@@ -1451,7 +1487,6 @@ struct WaveQP {
         IMPC_SEC(kSecUpdate);
         IMPC_REP(kSecProducts) write_v_products();
         IMPC_SEC(kSecProducts);
-        (void)n;
     }
 
     // ------------------------------------------------------------ update_info + checks
@@ -1800,17 +1835,22 @@ struct WaveQP {
         const int chk = st.check_termination;
         int can_check = 0;
         // countdowns instead of iter % interval (no integer division in the loop)
-        int32_t chk_left = chk, rho_left = st.rho_interval;
-        for (iter = 1; iter <= st.max_iter; iter++) {
+        // the loop's settings read once into registers (the batch's settings live in global memory
+        // for a grouped launch: read in the loop they cost a scalar-memory round trip each
+        // iteration, after every barrier)
+        const int32_t max_iter = st.max_iter, rho_int = st.adaptive_rho ? st.rho_interval : 0;
+        const bool tlim = st.time_limit > 0;
+        int32_t chk_left = chk, rho_left = rho_int;
+        for (iter = 1; iter <= max_iter; iter++) {
             const bool chk_now = chk && --chk_left == 0;
             if (chk_now) chk_left = chk;
-            const bool rho_now = st.adaptive_rho && st.rho_interval && --rho_left == 0;
-            if (rho_now) rho_left = st.rho_interval;
-            const bool need_delta = chk_now || iter == st.max_iter || st.time_limit > 0;
+            const bool rho_now = rho_int && --rho_left == 0;
+            if (rho_now) rho_left = rho_int;
+            const bool need_delta = chk_now || iter == max_iter || tlim;
             iterate(need_delta);
             // osqp_solve (PROFILING build): checked after the ADMM steps, before can_check is
             // recomputed (so it keeps the previous iteration's value); one team-wide decision
-            if (st.time_limit > 0) {
+            if (tlim) {
                 const double el = wv.max((double)(device_clock_100mhz() - t0) * 1e-8);
                 if (el >= st.time_limit) {
                     status = IMPC_TIME_LIMIT_REACHED;
