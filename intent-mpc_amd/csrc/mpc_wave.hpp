@@ -1,32 +1,42 @@
-// mpc_wave.hpp -- one mpcPlanner QP per NL-lane team (NL = 64 or 128 = 1 or 2 wavefronts),
-// all per-QP state on chip.
+// mpc_wave.hpp -- the structured kernel's body: one mpcPlanner QP per team of NL = 256 lanes
+// (4 wavefronts, one workgroup), all per-QP state on chip, 2 teams per CU.
 //
 // Why: the ADMM of OSQP 0.6.2 (reference osqp.h:78, osqp_solve) runs hundreds to thousands of
 // iterations per QP; each needs one solve with M = P + sigma I + A' R A plus two SpMVs.  Streaming
 // that state from HBM per iteration (the generic one-QP-per-lane kernel) is latency/bandwidth
-// bound.  Here a wave keeps its QP's factor, A values, iterates and bounds in VGPRs and uses LDS
-// only as an exchange buffer, and the waves of the grid pull QPs from a work queue so QPs that
-// need 4000 iterations do not stall the ones that need 200.
+// bound.  Here a team keeps its QP's factor rows, A values, iterates and bounds in VGPRs and the
+// stage-coupling blocks, exchange vectors and the general rows' products in LDS (~50-66 KB per QP
+// at N = 20), and the teams of the grid pull QPs from a work queue so QPs that need 4000
+// iterations do not stall the ones that need 200.
+//
+// Shapes (template VS = variables per lane): VS = 1 (n <= 256, the reference's default horizon
+// N = 20) at 2 waves per SIMD; VS = 3 (n <= 768, N <= 59) at 1 wave per SIMD.  GS = 2..4
+// general-row slots per lane.  WF = the shape's default stage count (19 / 39) as a compile-time
+// constant, or 0 for any horizon.  TIER = the two-tier products layout (WaveLds) for obstacle-heavy
+// patterns whose one-tier products would cost the CU its second team.
 //
 // Data layout (stage order v' = 13k + r, see mpc_structure.hpp):
 //   var slot s of lane L  <-> v' = NL s + L   (VS slots):  x, q, P_jj, the variable's box row
 //       (A value, z, y, l, u, type), row v'%13 of Ainv_k (13) and an 8-wide coupling row
 //   general-row slot s    <-> g = NL s + L    (GS slots): 4 A values + columns, z, y, l, u, type
-//   LDS: F_k (the 8x8 stage-coupling matrices), exchange vectors r / t / e / x~, products buffer
+//   LDS (WaveLds): F_k (the 8x8 stage-coupling blocks), exchange vectors r / t / e / x~, team
+//       reduction scratch, the int16 entry -> product-slot table, D / E and the check deltas
+//       (VS = 1), the products buffer (column-slot layout)
 //
 // Linear solve (block LDL^T of the stage-tridiagonal M, with Ahat_k the Schur complements):
 //   G_k = Bbar_k Ahat_k^{-1} (8 x 13), F_k = G_k[:, :8]
 //   forward : a_0 = r_0[:8],  a_{k+1} = r_{k+1}[:8] - G_k[:, 8:] r_k[8:] - F_k a_k   (8-dim recursion)
 //   middle  : e_k = Ahat_k^{-1} (a_k, r_k[8:])                                     (parallel)
 //   backward: x_{N-1} = e_{N-1},  x_k = e_k - G_k^T x_{k+1}[:8]                      (8-dim recursion)
-// The 8-dim recursions are the only serial part (2 x (N-1) steps of an 8x8 mat-vec).
+// The 8-dim recursions are the only serial part (2 x (N-1) steps of an 8x8 mat-vec); one
+// wavefront of the team (rw) runs each on its 8x8 lane grid with DPP / permlane reductions while
+// the others wait at the barrier -- the parallel phases (rhs gather, S1, S3, S5, update,
+// products) use all 256 lanes.
 //
 // The kernel body is written against a team policy `WV`: lane() in [0, NL), sync() (team barrier
 // with LDS visibility), bcast(v, j) (v of lane j of the CALLER's wavefront), max()/sum() over the
-// team, so the same code runs on the GPU (policy in impc_qp.hip) and, for tests only, in an
-// NL-thread CPU emulation (tests/native/wave_emu.cpp).  The 8-dim recursions are computed
-// redundantly by every wavefront of the team on its own 8x8 lane grid, so no exchange crosses
-// wavefronts inside them.
+// team, so the same code runs on the GPU (policy GpuTeam in impc_qp.hip) and, for tests only, in an
+// NL-thread CPU emulation (tests/native/wave_emu.cpp).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <math.h>
