@@ -58,6 +58,9 @@ constexpr int kTile = 64;   // transpose tile edge
 #ifndef IMPC_VS
 #define IMPC_VS 1
 #endif
+#ifndef IMPC_DUPADD  // strided lane-grid sums: duplicated adds instead of copies before the swaps
+#define IMPC_DUPADD 1
+#endif
 #ifndef IMPC_WAVES_PER_SIMD
 #define IMPC_WAVES_PER_SIMD 2
 #endif
@@ -259,13 +262,45 @@ struct GpuTeam {
             return __hiloint2double(rh[0], rl[0]) + __hiloint2double(rh[1], rl[1]);
         }
     }
+#if IMPC_DUPADD
+    // x + y computed a second time into its own register, out of CSE's sight: the permlane swaps
+    // need their operand in two registers, and a second add issued beside the first is off the
+    // chain where a two-v_mov copy of the result was on it.  (The hazard recognizer pads the
+    // gfx950 "VALU write -> v_permlane read" distance after the asm itself: checked in the .s.)
+    __device__ static double add_dup(double x, double y) {
+        double r;
+        asm("v_add_f64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+        return r;
+    }
+    // pair_sum of a value held (bitwise identically) in two registers a, b; returns the sum and,
+    // when DUP, its second copy
+    template <bool P32, bool DUP>
+    __device__ static double pair_sum2(double a, double b, double *dup) {
+        const int al = __double2loint(a), ah = __double2hiint(a), bl = __double2loint(b), bh = __double2hiint(b);
+        auto rl = P32 ? __builtin_amdgcn_permlane32_swap(al, bl, false, false)
+                      : __builtin_amdgcn_permlane16_swap(al, bl, false, false);
+        auto rh = P32 ? __builtin_amdgcn_permlane32_swap(ah, bh, false, false)
+                      : __builtin_amdgcn_permlane16_swap(ah, bh, false, false);
+        const double x = __hiloint2double(rh[0], rl[0]), y = __hiloint2double(rh[1], rl[1]);
+        if (DUP) *dup = add_dup(x, y);
+        return x + y;
+    }
+#endif
     // sum over lanes {j, j+8, .., j+56}: row_ror 8 (xor 8), then xor 16 and xor 32 pair sums,
     // low + high in both partners: ((v0+v1)+(v2+v3)) + ((v4+v5)+(v6+v7)) over the 8 rows i
     __device__ double sum_stride8(double v) {
+#if IMPC_DUPADD
+        const double d = dpp<0x128>(v);  // row_ror:8
+        const double a = v + d, b = add_dup(v, d);
+        double c2;
+        const double c = pair_sum2<false, true>(a, b, &c2);
+        return pair_sum2<true, false>(c, c2, nullptr);
+#else
         v = v + dpp<0x128>(v);  // row_ror:8
         v = pair_sum<false>(v);
         v = pair_sum<true>(v);
         return v;
+#endif
     }
     __device__ double max(double v) {
         for (int mask = 32; mask >= 1; mask >>= 1) {
