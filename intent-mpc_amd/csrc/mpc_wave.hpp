@@ -99,6 +99,9 @@ namespace impc {
 #else
 #define IMPC_LOADS_FIRST(NR, NV) ((void)0)
 #endif
+#ifndef IMPC_GJ  // stage inverses by Gauss-Jordan (1) or Cholesky + L^-1 + L^-T L^-1 (0)
+#define IMPC_GJ 1
+#endif
 #ifndef IMPC_PCAP_REG  // pair sweeps: keep the stage results in registers until the sweep ends (1)
 #define IMPC_PCAP_REG 0  // or store each one as it is produced (0: measured faster, fewer spills)
 #endif
@@ -652,6 +655,9 @@ struct WaveQP {
                         val += rhog[g] * w[4 * g + e] * w[4 * g + f];
                     }
                     if (!isB && r == cc) val += diagx[13 * k + r];
+#if IMPC_GJ
+                    if (!isB && k > 0 && r < 8 && cc < 8) val -= E[8 * r + cc];  // Schur complement
+#endif
                 }
                 if (isB)
                     Bb[dd] = val;
@@ -660,6 +666,40 @@ struct WaveQP {
             }
             wv.sync();
             IMPC_SEC(kSecFAsm);
+#if IMPC_GJ
+            // Ahat_k^{-1} by Gauss-Jordan elimination: one element per lane, the pivots in order
+            // (SPD, no pivoting needed; a pivot <= 0 flags the factorisation as failed, as a failed
+            // Cholesky did), ping-pong between two LDS buffers so every step is one barrier.  The
+            // last step writes the lower triangle to both halves of Ai (exactly symmetric).
+            {
+                double *src = A, *dst = Li;
+                const int gi = L / 13, gc = L % 13;
+                const bool act = L < 169 && gi < sz && gc < sz;
+                for (int j = 0; j < sz; j++) {
+                    const bool last = j == sz - 1;
+                    if (act) {
+                        const int i = last && gc > gi ? gc : gi, c = last && gc > gi ? gi : gc;
+                        const double p = src[13 * j + j];
+                        if (!(p > 0.0)) bad = 1;
+                        const double r = 1.0 / p;
+                        double v;
+                        if (i == j && c == j)
+                            v = r;
+                        else if (i == j)
+                            v = src[13 * j + c] * r;
+                        else if (c == j)
+                            v = -(src[13 * i + j] * r);
+                        else
+                            v = src[13 * i + c] - (src[13 * i + j] * r) * src[13 * j + c];
+                        (last ? Ai : dst)[13 * gi + gc] = v;
+                    }
+                    wv.sync();
+                    double *t = src;
+                    src = dst;
+                    dst = t;
+                }
+            }
+#else
             if (k > 0) {
                 if (L < 64) {
                     int i = L >> 3, j = L & 7;
@@ -710,6 +750,7 @@ struct WaveQP {
                 Ai[13 * r + cc] = s;
             }
             wv.sync();
+#endif
             _Pragma("unroll") for (int s = 0; s < VS; s++)
                 if (vok[s] && vs_[s] == k)
                     _Pragma("unroll") for (int cc = 0; cc < 13; cc++) ainv[s][cc] = cc < sz ? Ai[13 * vr_[s] + cc] : 0.0;
