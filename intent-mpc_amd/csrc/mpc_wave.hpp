@@ -99,8 +99,8 @@ namespace impc {
 #else
 #define IMPC_LOADS_FIRST(NR, NV) ((void)0)
 #endif
-#ifndef IMPC_GJ  // stage inverses by Gauss-Jordan (1) or Cholesky + L^-1 + L^-T L^-1 (0)
-#define IMPC_GJ 1
+#ifndef IMPC_GJ  // stage inverses by Gauss-Jordan with 2x2 (2) or 1x1 (1) pivots, or Cholesky +
+#define IMPC_GJ 2  // L^-1 + L^-T L^-1 (0)
 #endif
 #ifndef IMPC_PCAP_REG  // pair sweeps: keep the stage results in registers until the sweep ends (1)
 #define IMPC_PCAP_REG 0  // or store each one as it is produced (0: measured faster, fewer spills)
@@ -668,13 +668,66 @@ struct WaveQP {
             IMPC_SEC(kSecFAsm);
 #if IMPC_GJ
             // Ahat_k^{-1} by Gauss-Jordan elimination: one element per lane, the pivots in order
-            // (SPD, no pivoting needed; a pivot <= 0 flags the factorisation as failed, as a failed
-            // Cholesky did), ping-pong between two LDS buffers so every step is one barrier.  The
-            // last step writes the lower triangle to both halves of Ai (exactly symmetric).
+            // (SPD, no pivoting needed; a non-positive-definite pivot flags the factorisation as
+            // failed, as a failed Cholesky did), ping-pong between two LDS buffers so every step
+            // is one barrier.  The last step writes the lower triangle to both halves of Ai
+            // (exactly symmetric).
             {
                 double *src = A, *dst = Li;
                 const int gi = L / 13, gc = L % 13;
                 const bool act = L < 169 && gi < sz && gc < sz;
+#if IMPC_GJ == 2
+                // two pivots per step (2x2 block pivot Q = P^-1, P = S[J][J], J = {j, j+1}):
+                //   D[J][J] = Q, D[J][c] = Q S[J][c], D[i][J] = -S[i][J] Q,
+                //   D[i][c] = S[i][c] - (S[i][J] Q) S[J][c]; a non-PD pivot block flags failure
+                for (int j = 0; j < sz; j += 2) {
+                    const bool two = j + 1 < sz, last = j + (two ? 2 : 1) >= sz;
+                    if (act) {
+                        const int i = last && gc > gi ? gc : gi, c = last && gc > gi ? gi : gc;
+                        double v;
+                        if (two) {
+                            const double p00 = src[13 * j + j], p01 = src[13 * j + j + 1];
+                            const double p10 = src[13 * (j + 1) + j], p11 = src[13 * (j + 1) + j + 1];
+                            const double det = p00 * p11 - p01 * p10;
+                            if (!(p00 > 0.0) || !(det > 0.0)) bad = 1;
+                            const double rd = 1.0 / det;
+                            const double q00 = p11 * rd, q01 = -(p01 * rd), q10 = -(p10 * rd), q11 = p00 * rd;
+                            const int ri = i - j, ci = c - j;
+                            const bool iJ = ri == 0 || ri == 1, cJ = ci == 0 || ci == 1;
+                            if (iJ && cJ) {
+                                v = ri == 0 ? (ci == 0 ? q00 : q01) : (ci == 0 ? q10 : q11);
+                            } else if (iJ) {
+                                const double s0 = src[13 * j + c], s1 = src[13 * (j + 1) + c];
+                                v = ri == 0 ? q00 * s0 + q01 * s1 : q10 * s0 + q11 * s1;
+                            } else {
+                                const double a0 = src[13 * i + j], a1 = src[13 * i + j + 1];
+                                const double u0 = a0 * q00 + a1 * q10, u1 = a0 * q01 + a1 * q11;
+                                if (cJ)
+                                    v = -(ci == 0 ? u0 : u1);
+                                else
+                                    v = src[13 * i + c] - (u0 * src[13 * j + c] + u1 * src[13 * (j + 1) + c]);
+                            }
+                        } else {
+                            const double p = src[13 * j + j];
+                            if (!(p > 0.0)) bad = 1;
+                            const double r = 1.0 / p;
+                            if (i == j && c == j)
+                                v = r;
+                            else if (i == j)
+                                v = src[13 * j + c] * r;
+                            else if (c == j)
+                                v = -(src[13 * i + j] * r);
+                            else
+                                v = src[13 * i + c] - (src[13 * i + j] * r) * src[13 * j + c];
+                        }
+                        (last ? Ai : dst)[13 * gi + gc] = v;
+                    }
+                    wv.sync();
+                    double *t = src;
+                    src = dst;
+                    dst = t;
+                }
+#else
                 for (int j = 0; j < sz; j++) {
                     const bool last = j == sz - 1;
                     if (act) {
@@ -698,6 +751,7 @@ struct WaveQP {
                     src = dst;
                     dst = t;
                 }
+#endif
             }
 #else
             if (k > 0) {
