@@ -12,3 +12,5 @@ cat $O/configs_s3.jsonl | cut -c1-200
 timeout -k 10 300 python -u tools/xref_sweep.py > $O/xref_sweep.jsonl 2> $O/xref.err || { tail -20 $O/xref.err; exit 1; }
 cat $O/xref_sweep.jsonl
 bash tools/profile_r02.sh
+timeout -k 10 600 python3 bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail -20 $O/bench_default.err; exit 1; }
+cut -c1-300 $O/bench_default.json
