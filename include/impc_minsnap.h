@@ -21,8 +21,13 @@
  *                                                      accelerations, zeros for continuity rows
  *   solveX/Y/Z                      :831-868           coefficient d of segment s divided by
  *                                                      (T_{s+1} - T_s)^d
- * m = 2S + (S+1) + (S+1) + (S-1)(continuity_degree - 2).  Corridor constraints (:570-602,
- * :796-817; rows from an unordered_map, whose order is unspecified) are not built.
+ *   setCorridorConstraint /        :960-1012          corridor rows (impc_minsnap_corridor_*): segment
+ *   updateCorridorParam,                               i with size r_i != 0 gets one row per sample t
+ *   constructA corridor rows       :557-579           of for (t = 0; t <= 1; t += 1/numCorridor_i),
+ *   constructBound corridor rows   :815-835           entries pow(t, d), bounds interp(p_i, p_{i+1}, t)
+ *                                                      -+ r_i, in std::unordered_map<double, pose>
+ *                                                      order (libstdc++, as the reference iterates)
+ * m = 2S + (S+1) + (S+1) + (S-1)(continuity_degree - 2) [+ the corridor samples].
  * P is returned as its upper triangle (OsqpEigen keeps triangularView<Upper>, Data.tpp:38).
  */
 #ifndef IMPC_MINSNAP_H
@@ -63,6 +68,27 @@ int impc_minsnap_build_values(const impc_minsnap_params *p, int64_t nb, int32_t 
 int impc_minsnap_build_bounds(const impc_minsnap_params *p, int64_t nb, int32_t num_waypoints, const double *path,
                               const double *init_vel, const double *end_vel, const double *init_acc,
                               const double *end_acc, double *l, double *u);
+
+/* Corridor constraints.  numCorridor_i = ceil((T_{i+1} - T_i) * corridor_res) of every segment
+ * (0 where corridor_size is 0) for nb paths: corridor_size, corridor_num [nb][W-1].  The sample
+ * times, hence the pattern and the A values, depend only on the numCorridor vector, so a batch
+ * holds paths with equal vectors; the *_corridor_values / _bounds calls take that vector and fail
+ * (return 1) for a path whose own vector differs.  corridor_num = NULL is the plain problem. */
+int impc_minsnap_corridor_num(const impc_minsnap_params *p, int64_t nb, int32_t num_waypoints, const double *path,
+                              const double *corridor_size, double corridor_res, int32_t *corridor_num);
+int impc_minsnap_corridor_dims(const impc_minsnap_params *p, int32_t num_waypoints, const int32_t *corridor_num,
+                               impc_qp_dims *out);
+int impc_minsnap_corridor_pattern(const impc_minsnap_params *p, int32_t num_waypoints, const int32_t *corridor_num,
+                                  int64_t *Pp, int64_t *Pi, int64_t *Ap, int64_t *Ai);
+int impc_minsnap_corridor_values(const impc_minsnap_params *p, int64_t nb, int32_t num_waypoints, const double *path,
+                                 const double *init_vel, const double *end_vel, const double *init_acc,
+                                 const double *end_acc, const int32_t *corridor_num, const double *corridor_size,
+                                 double corridor_res, double *Px, double *q, double *Ax, double *l, double *u,
+                                 double *seg_time);
+int impc_minsnap_corridor_bounds(const impc_minsnap_params *p, int64_t nb, int32_t num_waypoints, const double *path,
+                                 const double *init_vel, const double *end_vel, const double *init_acc,
+                                 const double *end_acc, const int32_t *corridor_num, const double *corridor_size,
+                                 double corridor_res, double *l, double *u);
 
 /* solveX/Y/Z's rescaling of the solutions to real time, in place: x [3 nb][n]. */
 int impc_minsnap_unscale(const impc_minsnap_params *p, int64_t nb, int32_t num_waypoints, const double *seg_time,

@@ -158,6 +158,15 @@ _sig("impc_minsnap_build_values", C.c_int, C.POINTER(MinsnapParams), C.c_int64, 
      _dp, _dp, _dp, _dp, _dp, _dp)
 _sig("impc_minsnap_build_bounds", C.c_int, C.POINTER(MinsnapParams), C.c_int64, C.c_int32, _dp, _dp, _dp, _dp, _dp,
      _dp, _dp)
+_i32p = C.POINTER(C.c_int32)
+_sig("impc_minsnap_corridor_num", C.c_int, C.POINTER(MinsnapParams), C.c_int64, C.c_int32, _dp, _dp, C.c_double, _i32p)
+_sig("impc_minsnap_corridor_dims", C.c_int, C.POINTER(MinsnapParams), C.c_int32, _i32p, C.POINTER(Dims))
+_sig("impc_minsnap_corridor_pattern", C.c_int, C.POINTER(MinsnapParams), C.c_int32, _i32p, _i64p, _i64p, _i64p,
+     _i64p)
+_sig("impc_minsnap_corridor_values", C.c_int, C.POINTER(MinsnapParams), C.c_int64, C.c_int32, _dp, _dp, _dp, _dp, _dp,
+     _i32p, _dp, C.c_double, _dp, _dp, _dp, _dp, _dp, _dp)
+_sig("impc_minsnap_corridor_bounds", C.c_int, C.POINTER(MinsnapParams), C.c_int64, C.c_int32, _dp, _dp, _dp, _dp, _dp,
+     _i32p, _dp, C.c_double, _dp, _dp)
 _sig("impc_minsnap_unscale", C.c_int, C.POINTER(MinsnapParams), C.c_int64, C.c_int32, _dp, _dp)
 _sig("impc_mpc_dims", C.c_int, C.POINTER(MpcParams), C.c_int32, C.c_int32, C.POINTER(Dims))
 _sig("impc_mpc_build_pattern", C.c_int, C.POINTER(MpcParams), C.c_int32, C.c_int32, _i64p, _i64p, _i64p, _i64p)
@@ -213,7 +222,9 @@ EXPORTED = [
     "impc_mpc_builder_destroy", "impc_mpc_build_values_device", "impc_intent_fanout", "impc_intent_fanout_device",
     "impc_fanout_candidates_device", "impc_intent_params_from_config", "impc_intent_prob", "impc_intent_prob_device",
     "impc_predict_traj", "impc_predict_traj_device", "impc_minsnap_dims", "impc_minsnap_build_pattern",
-    "impc_minsnap_build_values", "impc_minsnap_build_bounds", "impc_minsnap_unscale",
+    "impc_minsnap_build_values", "impc_minsnap_build_bounds", "impc_minsnap_unscale", "impc_minsnap_corridor_num",
+    "impc_minsnap_corridor_dims", "impc_minsnap_corridor_pattern", "impc_minsnap_corridor_values",
+    "impc_minsnap_corridor_bounds",
     "impc_reference_traj_device", "impc_repeat_rows_device", "impc_comm_unique_id", "impc_comm_create", "impc_comm_destroy", "impc_comm_allgather", "impc_comm_gather_info",
     "impc_comm_max", "impc_ctx_timer_mark", "impc_ctx_timer_read",
 ]
@@ -568,6 +579,13 @@ class DeviceArray:
         _check(lib.impc_copy_to_host(self.ctx.h, out.ctypes.data_as(_P), _P(self.ptr), self.nbytes),
                "impc_copy_to_host")
         return out
+
+    def set(self, arr):
+        host = np.ascontiguousarray(arr, self.dtype)
+        if host.shape != self.shape:
+            raise ValueError(f"DeviceArray.set: shape {host.shape}, expected {self.shape}")
+        _check(lib.impc_copy_to_device(self.ctx.h, _P(self.ptr), host.ctypes.data_as(_P), self.nbytes),
+               "impc_copy_to_device")
 
     def free(self):
         if self.ptr:

@@ -7,14 +7,37 @@ candidate scoring / selection (impc_select_best, :771-887).
 Host work is limited to the per-candidate repetition of the instance inputs (every candidate of
 a replan is linearised at the same previous plan); the candidate table of the selection is built
 on the device (impc_fanout_candidates_device).
+
+The replan's wall-clock budget (mpcPlanner.cpp:609-628): the reference issues candidate i only
+while `time = now - startTime < 0.15 s` and solves it with
+`timeLimit = max(solverTimeLimit_ - time, solverTimeLimit_)` (solver_time_limit, 0.05 s by
+default, :166-167); a candidate enters the selection only when solveTraj succeeded, i.e.
+solveProblem returned NoError (:513-518) -- every status but a non-convex problem.  The batch
+issues all six candidates of every instance at one instant, so the cut-off is one check before
+the grouped solve: past it no candidate is issued and every instance selects nothing
+(best_cand -1, the reference's validTraj = false).
 """
 import ctypes as C
 import time
 
 import numpy as np
 
-from . import (Batch, DeviceArray, MpcBuilder, ReferencePaths, SelectParams, _P, _check, lib, mpc_dims, mpc_pattern,
-               repeat_rows_device, solve_group)
+from . import (NON_CVX, Batch, DeviceArray, MpcBuilder, ReferencePaths, SelectParams, Settings, _P, _check, lib,
+               mpc_dims, mpc_pattern, repeat_rows_device, solve_group)
+
+ISSUE_CUTOFF_S = 0.15  # makePlanWithPred: no candidate is issued 0.15 s after the replan started (:613)
+
+
+def candidate_valid(cand_slot, status_single, status_pair):
+    """valid[i][c] of the selection: candidate c of instance i was solved without an OSQP error
+    (solveTraj's successSolve, mpcPlanner.cpp:513-518 -- every status but OSQP_NON_CVX).  Candidate
+    c sits at row 4i+slot of the single-intent batch (slot < 4) or 2i+slot-4 of the two-intent
+    batch (fanout.hpp k_fanout_candidates)."""
+    slot = np.asarray(cand_slot)
+    ii = np.arange(slot.shape[0])[:, None]
+    ok_s = np.asarray(status_single) != NON_CVX
+    ok_p = np.asarray(status_pair) != NON_CVX
+    return np.where(slot < 4, ok_s[4 * ii + np.minimum(slot, 3)], ok_p[2 * ii + np.clip(slot - 4, 0, 1)]).astype(np.int8)
 
 
 class DeviceReplan:
@@ -25,6 +48,7 @@ class DeviceReplan:
         self.ctx, self.params, self.pd, self.I, self.K, self.L = ctx, params, pd, I, K, L
         self.N = params.horizon
         N = self.N
+        self.settings = settings
         self.fan = dict(ob_idx=DeviceArray(ctx, (I,), np.int32), cand_type=DeviceArray(ctx, (I, 6), np.int32),
                         cand_slot=DeviceArray(ctx, (I, 6), np.int32), closest_prob=DeviceArray(ctx, (I, 4)),
                         single_pos=DeviceArray(ctx, (I, 4, K, L, 3)), single_size=DeviceArray(ctx, (I, 4, K, L, 3)),
@@ -45,14 +69,21 @@ class DeviceReplan:
             self.shapes.append(dict(K=kk, nb=nb, n=n, m=m, batch=b, builder=MpcBuilder(ctx, params, 0, kk, L),
                                     vals=outs))
 
-    def run(self, pos, vel, xref, prev, first_time, prev_count, dyn_cur, pred_pos, pred_size, prob, timings=None):
+    def run(self, pos, vel, xref, prev, first_time, prev_count, dyn_cur, pred_pos, pred_size, prob, timings=None,
+            solver_time_limit=None, t_start=None, issue_cutoff_s=ISSUE_CUTOFF_S):
         """Returns dict(best_cand, cand_type, cand_slot, ob_idx, x_single, x_pair, info_single, info_pair,
-        xref).  xref: the reference of every instance [I][N][8], or an impc.ReferencePaths -- the
-        instances' input paths and reference-tracking state, whose getReferenceTraj / getXRef then
-        runs on the device (mpcPlanner.cpp:968-981, 1199-1231) from `pos`."""
+        xref, issued, time_limit, valid).  xref: the reference of every instance [I][N][8], or an
+        impc.ReferencePaths -- the instances' input paths and reference-tracking state, whose
+        getReferenceTraj / getXRef then runs on the device (mpcPlanner.cpp:968-981, 1199-1231) from
+        `pos`.  Budget (module docstring): t_start is the replan's startTime (perf_counter seconds,
+        default: entry to run); solver_time_limit, when given, is solverTimeLimit_ and sets every
+        candidate's OSQP time_limit to max(limit - elapsed, limit); the settings' own time_limit
+        applies otherwise.  When the cut-off has passed, x_* / info_* are None."""
         I, K, L, N = self.I, self.K, self.L, self.N
         t = {}
         t0 = time.perf_counter()
+        if t_start is None:
+            t_start = t0
         din = [DeviceArray(self.ctx, np.ascontiguousarray(a, dt)) for a, dt in
                ((pos, np.float64), (first_time, np.int8), (prev, np.float64), (prev_count, np.int32),
                 (dyn_cur, np.float64), (pred_pos, np.float64), (pred_size, np.float64), (prob, np.float64))]
@@ -87,8 +118,27 @@ class DeviceReplan:
             sh["builder"].build(sh["nb"], r[0].ptr, r[1].ptr, r[2].ptr, r[3].ptr, None, None, None, f[dp].ptr,
                                 f[ds].ptr, *[v.ptr for v in sh["vals"]])
             sh["batch"].set_values_device(*[sh["vals"][k].ptr for k in (0, 1, 2, 3, 4)])
-        solve_group([sh["batch"] for sh in self.shapes])
         self.ctx.synchronize()
+        elapsed = time.perf_counter() - t_start
+        issued = elapsed < issue_cutoff_s
+        time_limit = self.settings.time_limit
+        if solver_time_limit is not None:
+            time_limit = max(solver_time_limit - elapsed, solver_time_limit)
+        for sh in self.shapes:
+            s = Settings.from_buffer_copy(self.settings)
+            s.time_limit = time_limit
+            sh["batch"].set_settings(s)
+        results = None
+        if issued:
+            solve_group([sh["batch"] for sh in self.shapes])
+            self.ctx.synchronize()
+            results = [sh["batch"].get() for sh in self.shapes]
+        # candidate c of instance i sits at row 4i+slot of the single-intent batch (slot < 4) or
+        # 2i+slot-4 of the two-intent batch (fanout.hpp k_fanout_candidates)
+        slot = f["cand_slot"].get()
+        valid = (candidate_valid(slot, results[0][2]["status_val"], results[1][2]["status_val"]) if issued
+                 else np.zeros((I, 6), np.int8))
+        self.sel["valid"].set(valid)
         t["fanout_build_solve_s"] = time.perf_counter() - t0
         # selection, on the device: the candidate table (solution pointers, obstacle sets in the
         # selection's padded layout) from the fan-out outputs, then scoring + evaluateTraj
@@ -112,17 +162,15 @@ class DeviceReplan:
         self.ctx.synchronize()
         xref_used = xref_d.get()
         din += [xref_d, vel_d]
-        slot = f["cand_slot"].get()
         t["select_s"] = time.perf_counter() - t0
         for d in din + rep[4] + rep[2]:
             d.free()
         if timings is not None:
             timings.update(t)
         out = dict(best_cand=sel["best_cand"].get(), cand_type=f["cand_type"].get(), cand_slot=slot,
-                   ob_idx=f["ob_idx"].get(), xref=xref_used)
-        for sh, nm in zip(self.shapes, ("single", "pair")):
-            x, y, info = sh["batch"].get()
-            out["x_" + nm], out["info_" + nm] = x, info
+                   ob_idx=f["ob_idx"].get(), xref=xref_used, issued=issued, time_limit=time_limit, valid=valid)
+        for k, (sh, nm) in enumerate(zip(self.shapes, ("single", "pair"))):
+            out["x_" + nm], out["info_" + nm] = (results[k][0], results[k][2]) if issued else (None, None)
             out["vals_" + nm] = [v.get() for v in sh["vals"]]
         return out
 

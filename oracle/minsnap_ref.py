@@ -7,8 +7,14 @@ Follows, entry by entry and in the reference's insertion order:
   avgTimeAllocation              :125-138  (getPoseDistance, utils.h:69-72)
   constructP                     :241-307  (only the uncommented loop, :256-270)
   constructQ                     :309-312
-  constructA                     :314-585  (corridor rows :559-585 not restated)
-  constructBound                 :587-847  (corridor rows not restated)
+  constructA                     :314-585  (corridor rows :557-579)
+  constructBound                 :587-847  (corridor rows :815-835)
+  updateCorridorParam            :985-1012 (numCorridor, the accumulated sample times t)
+  interpolatePose                :1014-1023
+The reference emits a segment's corridor rows in the iteration order of the
+std::unordered_map<double, pose> holding its samples (libstdc++'s hashing of the keys); this
+restatement emits them in insertion (increasing t) order and returns each row's (segment, t), so
+a checker matches rows by key -- the row order itself is not restated here.
   solveX/Y/Z                     :870-905  (coefficient rescaling)
 Values use math.pow / math.sqrt (the same libm calls as the reference's pow / sqrt), except pow(x, 2), which
 GCC folds to x * x in the reference build (_sq).
@@ -42,16 +48,39 @@ def constraint_num(S, cont):
     return (2 + S - 1 + S - 1) + (2 + S - 1) + (2 + S - 1) + (S - 1) * (cont - 2)
 
 
+def corridor_samples(duration, size, res):
+    """updateCorridorParam :994-1006 for one segment: (numCorridor, sample times in insertion
+    order); (0, []) when the segment's corridor size is 0."""
+    if size == 0.0:
+        return 0, []
+    num = math.ceil(duration * res)
+    dt = 1.0 / num
+    ts = []
+    t = 0.0
+    while t <= 1.0:
+        ts.append(t)
+        t += dt
+    return num, ts
+
+
 def build(path, deg=7, diff=4, cont=3, desired_vel=1.0, soft=False, sc_dev=(0.0, 0.0, 0.0), init_vel=(0, 0, 0),
-          end_vel=(0, 0, 0), init_acc=(0, 0, 0), end_acc=(0, 0, 0)):
+          end_vel=(0, 0, 0), init_acc=(0, 0, 0), end_acc=(0, 0, 0), corridor_size=None, corridor_res=None):
     """Returns dict(P: {(r,c): v} upper triangle, A: {(r,c): v} in insertion order, l, u [3][m],
-    T, n, m)."""
+    T, n, m, cnum [S], corridor [(segment, t)] of the rows after the plain ones)."""
     cont = max(cont, 2)
     W = len(path)
     S = W - 1
     D = deg + 1
     n, m = D * S, constraint_num(S, cont)
     T = time_allocation(path, desired_vel)
+    cnum, corridor = [], []
+    if corridor_size is not None:
+        for i in range(S):
+            num, ts = corridor_samples(T[i + 1] - T[i], corridor_size[i], corridor_res)
+            cnum.append(num)
+            corridor += [(i, t) for t in ts]
+    m_plain = m
+    m += len(corridor)
     P = {}
     for s in range(S):  # constructP :256-270 (both triangles inserted; OsqpEigen keeps the upper)
         for i in range(diff, deg + 1):
@@ -135,6 +164,12 @@ def build(path, deg=7, diff=4, cont=3, desired_vel=1.0, soft=False, sc_dev=(0.0,
         continuity(3)  # jerk :504-528
     if cont >= 4:
         continuity(4)  # snap :530-555
+    for i, t in corridor:  # corridor :557-579
+        for d in range(D):
+            f = math.pow(t, d)
+            if f != 0:
+                ins(r, D * i + d, f)
+        r += 1
     assert r == m
     l, u = np.zeros((3, m)), np.zeros((3, m))
     for a in range(3):
@@ -146,9 +181,13 @@ def build(path, deg=7, diff=4, cont=3, desired_vel=1.0, soft=False, sc_dev=(0.0,
         rows += [(init_vel[a], init_vel[a]), (end_vel[a], end_vel[a])] + [(0.0, 0.0)] * (S - 1)
         rows += [(init_acc[a], init_acc[a]), (end_acc[a], end_acc[a])] + [(0.0, 0.0)] * (S - 1)
         rows += [(0.0, 0.0)] * ((S - 1) * (cont - 2))
+        for i, t in corridor:  # :815-835, interpolatePose :1014-1023 between waypoints i, i+1
+            ps, pe = path[i][a], path[i + 1][a]
+            mid = ps + (pe - ps) * (t - 0.0) / (1.0 - 0.0)
+            rows.append((mid - corridor_size[i], mid + corridor_size[i]))
         l[a] = [x[0] for x in rows]
         u[a] = [x[1] for x in rows]
-    return dict(P=P, A=A, l=l, u=u, T=T, n=n, m=m)
+    return dict(P=P, A=A, l=l, u=u, T=T, n=n, m=m, m_plain=m_plain, cnum=cnum, corridor=corridor)
 
 
 def to_csc(entries, n):

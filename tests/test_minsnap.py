@@ -113,3 +113,108 @@ def test_device_solve_and_update_match_persistent_oracle(ctx):
                 dt = T[b, sgi + 1] - T[b, sgi]
                 end = np.polyval(coef[sgi][::-1], dt)
                 assert abs(end - path[b, sgi + 1, a]) <= 2 * (1e-3 + 1e-3 * np.abs(path[b, :, a]).max())
+
+
+def _dense(Ap, Ai, Ax, m, n):
+    A = np.zeros((m, n))
+    for c in range(n):
+        for k in range(Ap[c], Ap[c + 1]):
+            A[Ai[k], c] = Ax[k]
+    return A
+
+
+CORRIDOR_CASES = [dict(W=2, res=5.0, size=(0.5,)), dict(W=5, res=5.0, size=(0.5, 0.0, 0.3, 0.4)),
+                  dict(W=4, res=3.3, size=(0.2, 0.2, 0.2)), dict(W=6, res=10.0, size=(0.0, 0.25, 0.0, 0.25, 0.1))]
+
+
+@pytest.mark.parametrize("case", CORRIDOR_CASES, ids=[str(i) for i in range(len(CORRIDOR_CASES))])
+def test_corridor_assembly_matches_restatement(case):
+    """setCorridorConstraint (polyTrajSolver.cpp:960-1012): numCorridor per segment, the corridor
+    rows of A (pow(t, d), :557-579) and their bounds (interpolated waypoints -+ r, :815-835) bit for
+    bit against oracle/minsnap_ref.py, rows matched by (segment, t) -- the product emits them in
+    the std::unordered_map order the reference iterates, the restatement in insertion order."""
+    W, res = case["W"], case["res"]
+    p = minsnap.params(desired_vel=1.5)
+    # one path repeated with sub-ulp-free translations keeps the batch's numCorridor vector equal
+    base = paths(1, W, seed=100 + W)
+    path = np.concatenate([base, base + 1.0, base - 2.0])
+    nb = path.shape[0]
+    size = np.broadcast_to(np.array(case["size"]), (nb, W - 1))
+    cn = minsnap.corridor_num(p, path, size, res)
+    assert (cn == cn[0]).all()
+    cnum = cn[0]
+    pat = minsnap.pattern(p, W, cnum)
+    v = minsnap.values(p, path, cnum=cnum, corridor_size=size, corridor_res=res)
+    l2, u2 = minsnap.bounds(p, path, cnum=cnum, corridor_size=size, corridor_res=res)
+    np.testing.assert_array_equal(l2, v["l"])
+    np.testing.assert_array_equal(u2, v["u"])
+    D = 8
+    for b in range(nb):
+        r = ref.build(path[b].tolist(), desired_vel=1.5, corridor_size=list(size[b]), corridor_res=res)
+        assert list(cn[b]) == r["cnum"]
+        assert (pat["n"], pat["m"]) == (r["n"], r["m"]) and r["m"] > r["m_plain"]
+        Ar = _dense(*ref.to_csc(r["A"], r["n"]), r["m"], r["n"])
+        for a in range(3):
+            A = _dense(pat["Ap"], pat["Ai"], v["Ax"][3 * b + a], pat["m"], pat["n"])
+            mp = r["m_plain"]
+            np.testing.assert_array_equal(A[:mp], Ar[:mp])
+            np.testing.assert_array_equal(v["l"][3 * b + a][:mp], r["l"][a][:mp])
+            key = {rc: mp + k for k, rc in enumerate(r["corridor"])}
+            seen, segs = set(), []
+            for row in range(mp, r["m"]):
+                cols = np.nonzero(A[row])[0]
+                seg = int(cols[0]) // D
+                assert (cols // D == seg).all()
+                t = A[row, D * seg + 1] if len(cols) > 1 else 0.0
+                k = key[(seg, t)]
+                seen.add(k)
+                segs.append(seg)
+                np.testing.assert_array_equal(A[row], Ar[k])
+                assert v["l"][3 * b + a][row] == r["l"][a][k] and v["u"][3 * b + a][row] == r["u"][a][k]
+            assert len(seen) == r["m"] - mp and segs == sorted(segs)
+
+
+def test_corridor_rejects_mismatched_paths():
+    p = minsnap.params()
+    path = paths(2, 4, seed=5)
+    path[1] *= 3.0  # longer segments: more corridor samples
+    size = np.full((2, 3), 0.3)
+    cn = minsnap.corridor_num(p, path, size, 5.0)
+    assert (cn[1] > cn[0]).any()
+    with pytest.raises(impc.ImpcError):
+        minsnap.values(p, path, cnum=cn[0], corridor_size=size, corridor_res=5.0)
+
+
+@pytest.mark.gpu
+def test_corridor_device_solve_matches_persistent_oracle(ctx):
+    """polyTrajOccMap's use (corridor radius, corridor_res 5, polyTrajOccMap.cpp:64-90): the
+    corridor QPs of a batch of translated copies of one path, setUpProblem then updateProblem,
+    against the oracle's persistent workspaces."""
+    W, res = 5, 5.0
+    p = minsnap.params()
+    s = impc.default_settings(verbose=0)
+    base = paths(1, W, seed=77)
+    path = np.concatenate([base + k for k in range(8)])
+    nb = path.shape[0]
+    size = np.full((nb, W - 1), 0.4)
+    cnum = minsnap.corridor_num(p, path, size, res)[0]
+    rng = np.random.default_rng(78)
+    iv2 = rng.normal(scale=0.5, size=(nb, 3))
+    ms = minsnap.MinsnapBatch(ctx, p, nb, W, s, cnum=cnum)
+    try:
+        ms.update_path(path, size, res)
+        c1, x1, i1 = ms.solve()
+        c2, x2, i2 = ms.solve(init_vel=iv2)
+    finally:
+        ms.close()
+    cor = dict(cnum=cnum, corridor_size=size, corridor_res=res)
+    pat = minsnap.pattern(p, W, cnum)
+    v = minsnap.values(p, path, **cor)
+    l2, u2 = minsnap.bounds(p, path, iv2, **cor)
+    os_ = ora.settings_from(s)
+    for qp in range(3 * nb):
+        w = ora.Workspace(pat, v["Px"][qp], v["q"][qp], v["Ax"][qp], v["l"][qp], v["u"][qp], os_)
+        check(x1[qp], i1[qp], w.solve())
+        w.update_bounds(l2[qp], u2[qp])
+        check(x2[qp], i2[qp], w.solve())
+        w.close()
