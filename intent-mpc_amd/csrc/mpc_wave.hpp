@@ -57,6 +57,9 @@ namespace impc {
 #endif
 #define IMPC_REP(X) for (int rep_ = 0; rep_ < (IMPC_DUP == (X) ? 2 : 1); rep_++)
 
+#ifndef IMPC_HWRW  // recursion wave chosen from the waves' SIMD placement (+0.5 % config 3, +0.7 % config 4)
+#define IMPC_HWRW 1
+#endif
 #ifndef IMPC_NOCHUNK
 #define IMPC_NOCHUNK 1
 #endif
@@ -1843,8 +1846,22 @@ struct WaveQP {
         // OSQP 0.6.2 counts setup_time + solve time on a first run (every solveTraj call is one)
         const uint64_t t0 = device_clock_100mhz();
         rw = (int)(b % (NL / 64));  // spread the serial recursions of co-resident QPs over SIMDs
+#if IMPC_HWRW && defined(__HIP_DEVICE_COMPILE__)
+        // recursion wave from the hardware placement (HW_REG_HW_ID: WAVE_ID [3:0], SIMD_ID [5:4]):
+        // the wave on SIMD (wave slot of the team's wave 0) mod 4, so co-resident teams, which sit
+        // in different wave slots, run their recursions on different SIMDs; the QP-index choice
+        // above when no wave of the team is on that SIMD
+        if ((L & 63) == 0) lds[LD::JUNK_OFF + (L >> 6)] = (double)(__builtin_amdgcn_s_getreg((31 << 11) | 4) & 0x3f);
+#endif
         IMPC_SEC_START();
         clear_exchange();
+#if IMPC_HWRW && defined(__HIP_DEVICE_COMPILE__)
+        {
+            const int target = (int)lds[LD::JUNK_OFF] & 3;
+            _Pragma("unroll") for (int w = NL / 64 - 1; w >= 0; w--)
+                if (((int)lds[LD::JUNK_OFF + w] >> 4) == target) rw = w;
+        }
+#endif
         load(b);
         double *ps = io.persist ? io.persist + b * persist_stride(T.n, T.mg) : nullptr;
         {
