@@ -57,8 +57,8 @@ namespace impc {
 #endif
 #define IMPC_REP(X) for (int rep_ = 0; rep_ < (IMPC_DUP == (X) ? 2 : 1); rep_++)
 
-#ifndef IMPC_HWRW  // recursion wave chosen from the waves' SIMD placement (+0.5 % config 3, +0.7 % config 4)
-#define IMPC_HWRW 1
+#ifndef IMPC_HWRW  // recursion wave from the waves' SIMD placement: +0.5 %, off (profiles/r02/exp/README.md)
+#define IMPC_HWRW 0
 #endif
 #ifndef IMPC_NOCHUNK
 #define IMPC_NOCHUNK 1
