@@ -40,14 +40,21 @@ def test_budget_time_limit_and_cutoff(ctx):
     rp = DeviceReplan(ctx, p, pd, I, K, L, impc.default_settings(verbose=0))
     try:
         free = rp.run(*args)
-        # solverTimeLimit_ = 0.05 s (mpcPlanner.cpp:167): no candidate QP comes near it, so the
-        # limited replan is bit-identical to the unlimited one
+        # solverTimeLimit_ = 0.05 s (mpcPlanner.cpp:167), measured on the device clock from each
+        # QP's dequeue: a QP that finishes inside it is bit-identical to the unlimited replan; one
+        # that reaches it (a slow or shared box) stops early with OSQP_TIME_LIMIT_REACHED
         lim = rp.run(*args, solver_time_limit=0.05)
         assert lim["issued"] and lim["time_limit"] == 0.05
+        hit_any = False
         for nm in ("single", "pair"):
-            np.testing.assert_array_equal(lim["x_" + nm], free["x_" + nm])
-            np.testing.assert_array_equal(lim["info_" + nm]["iter"], free["info_" + nm]["iter"])
-        np.testing.assert_array_equal(lim["best_cand"], free["best_cand"])
+            hit = lim["info_" + nm]["status_val"] == impc.TIME_LIMIT_REACHED
+            hit_any |= bool(hit.any())
+            ok = ~hit
+            np.testing.assert_array_equal(lim["x_" + nm][ok], free["x_" + nm][ok])
+            np.testing.assert_array_equal(lim["info_" + nm]["iter"][ok], free["info_" + nm]["iter"][ok])
+            assert (lim["info_" + nm]["iter"][hit] <= free["info_" + nm]["iter"][hit]).all()
+        if not hit_any:
+            np.testing.assert_array_equal(lim["best_cand"], free["best_cand"])
         assert (lim["valid"] == 1).all() and (lim["best_cand"] >= 0).all()
         # a time limit every QP exceeds: OSQP_TIME_LIMIT_REACHED is still a successful solveTraj,
         # so every candidate stays in the selection
