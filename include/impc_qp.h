@@ -84,7 +84,7 @@ typedef struct {
     int64_t scaled_termination;
     int64_t check_termination;
     int64_t warm_start;
-    double time_limit; /* seconds per QP, measured on the device clock from the QP's ADMM start; 0 = off */
+    double time_limit; /* seconds per QP, on the device clock from the start of the QP's setup; 0 = off */
 } impc_settings;
 
 /* Subset of OSQPInfo (types.h:66-89), one per QP. */
@@ -226,9 +226,25 @@ int impc_batch_get_timings(impc_batch b, double *setup_ms, double *solve_ms, dou
 int impc_batch_set_persistent(impc_batch b, int on);
 
 /* Per-QP solve latency (ms) of the last profiled structured-kernel solve: from the moment a
- * workgroup takes the QP off the work queue to its results being written (device wall clock,
- * 100 MHz), for each of the B QPs.  Profiling must be on before the solve. */
+ * workgroup takes the QP off the work queue (the tick its time limit counts from) to its results
+ * being written, on the device's constant-rate clock (rate: impc_ctx_clock_rate), for each of the
+ * B QPs.  Profiling must be on before the solve. */
 int impc_batch_get_qp_latency(impc_batch b, double *ms);
+
+/* Per-QP OSQP time limits (seconds, host array [B]; 0 = none), overriding the settings'
+ * time_limit for the following solves; NULL returns to the settings' value.  The reference sets
+ * each solveTraj call's own limit (mpcPlanner.cpp:442-444: setTimeLimit(timeLimit) only when
+ * not firstTime_, timeLimit = max(solverTimeLimit_ - t, solverTimeLimit_) at :613-615), so one
+ * batch of candidates from several planners carries one limit per QP. */
+int impc_batch_set_time_limits(impc_batch b, const double *time_limit);
+
+/* The device clock the time limits and latencies are measured on: its rate in Hz, from
+ * hipDeviceAttributeWallClockRate (queried once per context). */
+int impc_ctx_clock_rate(impc_ctx ctx, double *hz);
+/* Clock self-check (diagnostics, tests): one kernel spins on the device clock until `seconds`
+ * have passed at the reported rate; *event_seconds = the same launch timed by HIP events on the
+ * context stream.  The two agree when the rate is right. */
+int impc_ctx_clock_check(impc_ctx ctx, double seconds, double *event_seconds);
 
 /* Factor-order permutation chosen by the symbolic analysis (perm[k] = variable at position k). */
 int impc_batch_get_perm(impc_batch b, int64_t *perm);

@@ -34,6 +34,7 @@ constexpr double kMinScaling = 1e-04, kMaxScaling = 1e+04;                      
 
 struct DevSettings {
     double rho, sigma, adaptive_rho_tolerance, eps_abs, eps_rel, eps_prim_inf, eps_dual_inf, alpha, time_limit;
+    double tick_s;  // seconds per device-clock tick (hipDeviceAttributeWallClockRate of the context's device)
     int32_t scaling, adaptive_rho, rho_interval, max_iter, scaled_termination, check_termination, warm_start;
 };
 
@@ -46,8 +47,9 @@ struct DevSym {
 };
 
 // Per-QP scalar slots (interleaved like every other array).
-// SC_T0: device clock at the start of osqp_setup (a first solve's time limit counts setup time)
-enum : int32_t { SC_C = 0, SC_CINV, SC_RHO, SC_SETUP_ERR, SC_T0, SC_NSCAL };
+// SC_TSETUP: device-clock ticks the QP's osqp_setup took (a first solve's time limit counts the
+// setup time, OSQP 0.6.2's setup_time, and nothing that ran between setup and solve)
+enum : int32_t { SC_C = 0, SC_CINV, SC_RHO, SC_SETUP_ERR, SC_TSETUP, SC_NSCAL };
 
 // Batch-interleaved per-QP arrays.
 struct DevWork {
@@ -65,6 +67,7 @@ struct DevWork {
     // outputs (interleaved)
     double *xo, *yo;
     impc_info *info;  // QP-major
+    const double *tlim = nullptr;  // per-QP time limits [B] (impc_batch_set_time_limits), or the settings'
 };
 
 #define IMPC_AT(arr, e) (arr)[(int64_t)(e) * S + lane]
@@ -517,7 +520,9 @@ IMPC_HD int update_rho(const DevSym &sy, const DevWork &wk, const DevSettings &s
     return bad;
 }
 
-IMPC_HD uint64_t device_clock_100mhz() {
+// the device's constant-rate clock (s_memrealtime); its rate comes from
+// hipDeviceAttributeWallClockRate (DevSettings::tick_s), never assumed
+IMPC_HD uint64_t device_clock() {
 #ifdef __HIP_DEVICE_COMPILE__
     return wall_clock64();
 #else
@@ -566,13 +571,14 @@ IMPC_HD void qp_solve(const DevSym &sy, const DevWork &wk, const DevSettings &st
     }
     const double alpha = st.alpha, oma = (double)1.0 - st.alpha, sigma = st.sigma;
     const int32_t chk = st.check_termination;
-    const uint64_t t0 = first_run ? (uint64_t)IMPC_AT(wk.scal, SC_T0) : device_clock_100mhz();
+    const double tl = wk.tlim ? wk.tlim[qp_index] : st.time_limit;
+    const uint64_t t0 = device_clock() - (first_run ? (uint64_t)IMPC_AT(wk.scal, SC_TSETUP) : 0);
     int can_check = 0;
     int64_t iter;
     for (iter = 1; iter <= st.max_iter; iter++) {
         const int need_delta = (chk && iter % chk == 0) || iter == st.max_iter ||
                                (st.adaptive_rho && st.rho_interval && iter % st.rho_interval == 0) ||
-                               st.time_limit > 0;
+                               tl > 0;
         // ---- update_xz_tilde: rhs (factor order) then the LDL^T solve
         for (int32_t p = 0; p < n; p++) {
             int32_t j = sy.perm[p];
@@ -605,8 +611,7 @@ IMPC_HD void qp_solve(const DevSym &sy, const DevWork &wk, const DevSettings &st
         }
         // osqp_solve (PROFILING build): after the ADMM steps, before can_check is recomputed, so
         // can_check keeps the previous iteration's value when the limit fires
-        if (st.time_limit > 0 &&
-            (double)(device_clock_100mhz() - t0) * 1e-8 >= st.time_limit) {
+        if (tl > 0 && (double)(device_clock() - t0) * st.tick_s >= tl) {
             status = IMPC_TIME_LIMIT_REACHED;
             break;
         }

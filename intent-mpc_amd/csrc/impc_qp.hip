@@ -111,8 +111,11 @@ __global__ __launch_bounds__(kBlock) void k_setup(impc::DevSym sy, impc::DevWork
     const int lane = blockIdx.x * kBlock + threadIdx.x;
     if (lane >= B) return;
     const int64_t S = wk.S;
-    IMPC_AT(wk.scal, impc::SC_T0) = (double)impc::device_clock_100mhz();  // setup_time starts here
+    const uint64_t t0 = impc::device_clock();
     impc::qp_setup(sy, wk, st, lane, has_ws);
+    // osqp_setup's own duration (setup_time): a first solve's time limit counts it, not the time
+    // the workspace then waits for the solve
+    IMPC_AT(wk.scal, impc::SC_TSETUP) = (double)(impc::device_clock() - t0);
 }
 
 // first_run: the first solve after k_setup (its time limit counts the setup time, OSQP 0.6.2)
@@ -121,6 +124,12 @@ __global__ __launch_bounds__(kBlock) void k_solve(impc::DevSym sy, impc::DevWork
     const int lane = blockIdx.x * kBlock + threadIdx.x;
     if (lane >= B) return;
     impc::qp_solve(sy, wk, st, lane, lane, 0, first_run);
+}
+
+// impc_ctx_clock_check: spin until the device clock has advanced `ticks` (one wavefront)
+__global__ __launch_bounds__(64) void k_clock_spin(uint64_t ticks) {
+    const uint64_t t0 = impc::device_clock();
+    while (impc::device_clock() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }
 
 // osqp_warm_start (osqp.h:157) on a set-up workspace: scaling, rho and factor stay
@@ -426,6 +435,8 @@ struct impc_ctx_s {
     int device = 0;
     int num_cu = 256;
     hipStream_t stream = nullptr;
+    // the device clock of time limits and latencies: seconds per tick (hipDeviceAttributeWallClockRate)
+    double tick_s = 1e-8;
     // grouped launches: device copy of the entries (grow-only) and its host staging buffer
     GroupEntry *d_group = nullptr;
     int group_cap = 0;
@@ -519,6 +530,8 @@ struct impc_batch_s {
     int64_t device_bytes = 0;
     bool values_set = false, has_ws = false;
     unsigned long long *d_qpt = nullptr;  // profiling: per-QP (start, end) device clock
+    double *d_tlim = nullptr;  // per-QP time limits (impc_batch_set_time_limits), or none
+    bool tlim_on = false;
     // persistent workspace of the structured kernel (impc_batch_set_persistent)
     double *d_persist = nullptr;
     bool persist_on = false, persist_valid = false, q_by_update = false;
@@ -619,6 +632,7 @@ impc::WaveIO wave_io(impc_batch b) {
                     b->in_l,     b->in_u,   b->in_xws, b->in_yws, b->has_ws ? 1 : 0, b->d_xout, b->d_yout,
                     b->d_scal,   b->d_info};
     if (b->profile && b->d_qpt) io.qpt = b->d_qpt;
+    if (b->tlim_on) io.tlim = b->d_tlim;
     if (b->persist_on && b->d_persist) {
         io.persist = b->d_persist;
         io.resume = b->persist_valid ? 1 : 0;
@@ -771,6 +785,7 @@ int generic_solve(impc_batch b, hipStream_t st) {
     }
     const int first_run = b->generic_first_run ? 1 : 0;
     b->generic_first_run = false;
+    b->dwk.tlim = b->tlim_on ? b->d_tlim : nullptr;
     if (b->profile) HIP_OK(hipEventRecord(b->ev[2], st));
     hipLaunchKernelGGL(k_solve, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk, b->dst, b->B,
                        first_run);
@@ -1011,6 +1026,12 @@ int impc_ctx_create(int device, impc_ctx *out) {
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
         c->num_cu = ncu;
+    int khz = 0;  // rate of the constant-rate clock the kernels read (s_memrealtime), kHz
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) {
+        delete c;
+        return fail(IMPC_DEVICE_ERROR, "hipDeviceAttributeWallClockRate unavailable: time limits cannot be measured");
+    }
+    c->tick_s = 1.0 / (1e3 * (double)khz);
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
@@ -1069,6 +1090,7 @@ int impc_batch_create(impc_ctx ctx, int64_t n, int64_t m, const int64_t *Pp, con
     b->S = (batch + kBlock - 1) / kBlock * kBlock;
     impc_default_settings(&b->settings);
     to_dev_settings(&b->settings, &b->dst);
+    b->dst.tick_s = ctx->tick_s;
     const int64_t B = batch;
     const int64_t in_len = b->nnzP + b->n + b->nnzA + 2 * b->m + b->n + b->m;
     const size_t in_bytes = sizeof(double) * (size_t)(in_len * B + 8);
@@ -1111,7 +1133,7 @@ int impc_batch_destroy(impc_batch b) {
         if (e) (void)hipEventDestroy(e);
     void *ptrs[] = {b->d_in,     b->d_xout,  b->d_yout,  b->d_info,  b->d_tables, b->d_scal, b->d_counter,
                     b->d_sym,    b->d_work,  b->d_sec,   b->d_shPx,  b->d_shAx,   b->d_Axv,  b->d_vmap,
-                    b->d_qpt,    b->d_persist};
+                    b->d_qpt,    b->d_persist, b->d_tlim};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete b;
@@ -1130,9 +1152,10 @@ int impc_batch_set_kernel(impc_batch b, int kernel) {
 
 int impc_batch_set_settings(impc_batch b, const impc_settings *s) {
     if (!b || !s) return fail(IMPC_INVALID_ARGUMENT, "null batch or settings");
-    impc::DevSettings d;
+    impc::DevSettings d{};
     int rc = to_dev_settings(s, &d);
     if (rc) return rc;
+    d.tick_s = b->ctx->tick_s;
     if (b->persist_on && s->scaling > impc::kPersistMaxScaling)
         return fail(IMPC_UNSUPPORTED, "persistent workspaces support scaling <= 20 Ruiz passes");
     if (s->rho != b->settings.rho || s->sigma != b->settings.sigma || s->scaling != b->settings.scaling) {
@@ -1548,7 +1571,58 @@ int impc_batch_get_qp_latency(impc_batch b, double *ms) {
     IMPC_TRY(ctx_quiesce(b->ctx));
     std::vector<unsigned long long> t((size_t)b->B * 2);
     HIP_OK(hipMemcpy(t.data(), b->d_qpt, sizeof(unsigned long long) * t.size(), hipMemcpyDeviceToHost));
-    for (int64_t k = 0; k < b->B; k++) ms[k] = (double)(t[2 * k + 1] - t[2 * k]) * 1e-5;  // 100 MHz ticks
+    const double tick_ms = b->ctx->tick_s * 1e3;
+    for (int64_t k = 0; k < b->B; k++) ms[k] = (double)(t[2 * k + 1] - t[2 * k]) * tick_ms;
+    return IMPC_OK;
+}
+
+int impc_batch_set_time_limits(impc_batch b, const double *time_limit) {
+    if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
+    if (!time_limit) {
+        b->tlim_on = false;
+        return IMPC_OK;
+    }
+    for (int64_t k = 0; k < b->B; k++)
+        if (!(time_limit[k] >= 0.0)) return fail(IMPC_SETTINGS_VALIDATION_ERROR, "time limits must be >= 0");
+    HIP_OK(hipSetDevice(b->ctx->device));
+    IMPC_TRY(ctx_quiesce(b->ctx));  // no launch in flight reads the array being replaced
+    if (!b->d_tlim) {
+        HIP_OK(hipMalloc((void **)&b->d_tlim, sizeof(double) * (size_t)b->B));
+        b->device_bytes += (int64_t)sizeof(double) * b->B;
+    }
+    IMPC_TRY(h2d_sync(b->ctx->stream, b->d_tlim, time_limit, sizeof(double) * (size_t)b->B));
+    b->tlim_on = true;
+    return IMPC_OK;
+}
+
+int impc_ctx_clock_rate(impc_ctx ctx, double *hz) {
+    if (!ctx || !hz) return fail(IMPC_INVALID_ARGUMENT, "null context or output");
+    *hz = 1.0 / ctx->tick_s;
+    return IMPC_OK;
+}
+
+int impc_ctx_clock_check(impc_ctx ctx, double seconds, double *event_seconds) {
+    if (!ctx || !event_seconds) return fail(IMPC_INVALID_ARGUMENT, "null context or output");
+    if (!(seconds > 0.0 && seconds <= 10.0)) return fail(IMPC_INVALID_ARGUMENT, "seconds must be in (0, 10]");
+    HIP_OK(hipSetDevice(ctx->device));
+    IMPC_TRY(ctx_quiesce(ctx));
+    hipEvent_t e0, e1;
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    const uint64_t ticks = (uint64_t)(seconds / ctx->tick_s + 0.5);
+    hipError_t err = hipEventRecord(e0, ctx->stream);
+    if (err == hipSuccess) {
+        hipLaunchKernelGGL(k_clock_spin, dim3(1), dim3(64), 0, ctx->stream, ticks);
+        err = hipGetLastError();
+    }
+    if (err == hipSuccess) err = hipEventRecord(e1, ctx->stream);
+    if (err == hipSuccess) err = hipEventSynchronize(e1);
+    float ms = 0.f;
+    if (err == hipSuccess) err = hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (err != hipSuccess) return fail(IMPC_DEVICE_ERROR, std::string("clock check: ") + hipGetErrorString(err));
+    *event_seconds = 1e-3 * (double)ms;
     return IMPC_OK;
 }
 

@@ -140,6 +140,9 @@ struct WaveIO {
     // iterates, and -- when q_updated -- scale q as osqp_update_lin_cost does ((D q) c).
     double *persist = nullptr;
     int32_t resume = 0, q_updated = 0;
+    // per-QP time limits [B] (impc_batch_set_time_limits: each solveTraj call sets its own), or
+    // nullptr for the settings' time_limit
+    const double *tlim = nullptr;
 };
 
 constexpr int kPersistHdr = 24;      // ct[0 .. kPersistMaxScaling), rho at kPersistHdr - 1
@@ -1841,10 +1844,11 @@ struct WaveQP {
     // not occupy registers across the ADMM loop.
     IMPC_WF void solve(int64_t b) {
         const int n = T.n, m = T.m;
-        const uint64_t t_begin = io.qpt ? device_clock_100mhz() : 0;
         // time_limit clock: from the start of the QP's setup (load, scaling, factorisation), as
-        // OSQP 0.6.2 counts setup_time + solve time on a first run (every solveTraj call is one)
-        const uint64_t t0 = device_clock_100mhz();
+        // OSQP 0.6.2 counts setup_time + solve time on a first run (every solveTraj call is one);
+        // the profiling record (qpt) starts at the same tick, so a QP stopped by its limit always
+        // shows a recorded latency of at least that limit
+        const uint64_t t0 = device_clock();
         rw = (int)(b % (NL / 64));  // spread the serial recursions of co-resident QPs over SIMDs
 #if IMPC_HWRW && defined(__HIP_DEVICE_COMPILE__)
         // recursion wave from the hardware placement (HW_REG_HW_ID: WAVE_ID [3:0], SIMD_ID [5:4]):
@@ -1961,7 +1965,9 @@ struct WaveQP {
         // for a grouped launch: read in the loop they cost a scalar-memory round trip each
         // iteration, after every barrier)
         const int32_t max_iter = st.max_iter, rho_int = st.adaptive_rho ? st.rho_interval : 0;
-        const bool tlim = st.time_limit > 0;
+        // team-uniform, in scalar registers (io.tlim: the QP's own limit)
+        const double tl = wv.uniform(io.tlim ? io.tlim[b] : st.time_limit), tick = st.tick_s;
+        const bool tlim = tl > 0;
         int32_t chk_left = chk, rho_left = rho_int;
         for (iter = 1; iter <= max_iter; iter++) {
             const bool chk_now = chk && --chk_left == 0;
@@ -1973,8 +1979,8 @@ struct WaveQP {
             // osqp_solve (PROFILING build): checked after the ADMM steps, before can_check is
             // recomputed (so it keeps the previous iteration's value); one team-wide decision
             if (tlim) {
-                const double el = wv.max((double)(device_clock_100mhz() - t0) * 1e-8);
-                if (el >= st.time_limit) {
+                const double el = wv.max((double)(device_clock() - t0) * tick);
+                if (el >= tl) {
                     status = IMPC_TIME_LIMIT_REACHED;
                     break;
                 }
@@ -2067,8 +2073,8 @@ struct WaveQP {
             io.yo[b * m + T.gen_row[NL * s + L]] = yv;
         }
         if (L == 0 && io.qpt) {
-            io.qpt[2 * b] = t_begin;
-            io.qpt[2 * b + 1] = device_clock_100mhz();
+            io.qpt[2 * b] = t0;
+            io.qpt[2 * b + 1] = device_clock();
         }
         if (L == 0) {
             out->iter = info_iter;

@@ -132,6 +132,9 @@ _sig("impc_comm_allgather", C.c_int, _P, _P, _P, C.c_int64, _P)
 _sig("impc_comm_gather_info", C.c_int, _P, C.POINTER(_P), C.c_int, C.c_int64, _P, _P)
 _sig("impc_comm_max", C.c_int, _P, C.POINTER(C.c_double))
 _sig("impc_ctx_timer_mark", C.c_int, _P, _P)
+_sig("impc_batch_set_time_limits", C.c_int, _P, _dp)
+_sig("impc_ctx_clock_rate", C.c_int, _P, _dp)
+_sig("impc_ctx_clock_check", C.c_int, _P, C.c_double, _dp)
 _sig("impc_ctx_timer_read", C.c_int, _P, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_int64))
 
 
@@ -226,7 +229,8 @@ EXPORTED = [
     "impc_minsnap_corridor_dims", "impc_minsnap_corridor_pattern", "impc_minsnap_corridor_values",
     "impc_minsnap_corridor_bounds",
     "impc_reference_traj_device", "impc_repeat_rows_device", "impc_comm_unique_id", "impc_comm_create", "impc_comm_destroy", "impc_comm_allgather", "impc_comm_gather_info",
-    "impc_comm_max", "impc_ctx_timer_mark", "impc_ctx_timer_read",
+    "impc_comm_max", "impc_ctx_timer_mark", "impc_ctx_timer_read", "impc_batch_set_time_limits",
+    "impc_ctx_clock_rate", "impc_ctx_clock_check",
 ]
 
 
@@ -281,6 +285,18 @@ class Context:
         n = C.c_int64()
         _check(lib.impc_ctx_timer_read(self.h, ms.ctypes.data_as(_dp), max_pairs, C.byref(n)), "impc_ctx_timer_read")
         return ms[: n.value]
+
+    def clock_rate(self):
+        """impc_ctx_clock_rate: Hz of the device clock time limits and latencies are read on."""
+        hz = C.c_double()
+        _check(lib.impc_ctx_clock_rate(self.h, C.byref(hz)), "impc_ctx_clock_rate")
+        return hz.value
+
+    def clock_check(self, seconds):
+        """impc_ctx_clock_check: HIP-event seconds of a kernel that spins `seconds` on the device clock."""
+        ev = C.c_double()
+        _check(lib.impc_ctx_clock_check(self.h, float(seconds), C.byref(ev)), "impc_ctx_clock_check")
+        return ev.value
 
     def close(self):
         if self.h:
@@ -354,6 +370,16 @@ class Batch:
         info = np.empty(self.B, dtype=INFO_DTYPE)
         _check(lib.impc_batch_get(self.h, _d(x), _d(y), info.ctypes.data_as(C.c_void_p)), "impc_batch_get")
         return x.reshape(self.B, self.n), y[: self.B * self.m].reshape(self.B, self.m), info
+
+    def set_time_limits(self, limits):
+        """impc_batch_set_time_limits: per-QP time limits [B] in seconds (0 = none); None clears."""
+        if limits is None:
+            _check(lib.impc_batch_set_time_limits(self.h, None), "impc_batch_set_time_limits")
+            return
+        a = np.ascontiguousarray(limits, dtype=np.float64)
+        if a.size != self.B:
+            raise ValueError(f"set_time_limits: {a.size} values, expected B = {self.B}")
+        _check(lib.impc_batch_set_time_limits(self.h, _d(a)), "impc_batch_set_time_limits")
 
     def set_persistent(self, on=True):
         _check(lib.impc_batch_set_persistent(self.h, int(on)), "impc_batch_set_persistent")

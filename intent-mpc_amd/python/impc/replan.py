@@ -15,14 +15,18 @@ default, :166-167); a candidate enters the selection only when solveTraj succeed
 solveProblem returned NoError (:513-518) -- every status but a non-convex problem.  The batch
 issues all six candidates of every instance at one instant, so the cut-off is one check before
 the grouped solve: past it no candidate is issued and every instance selects nothing
-(best_cand -1, the reference's validTraj = false).
+(best_cand -1, the reference's validTraj = false).  solveTraj sets the time limit only when not
+firstTime_ (:442-444), so the candidates of an instance with first_time set carry none (per-QP
+limits, impc_batch_set_time_limits).  (The reference does not fan out a firstTime_ instance at
+all -- it takes the single-solve branch :645-659; this class is the fan-out branch, and a
+first_time instance's candidates are solved without a limit, as that branch's solve is.)
 """
 import ctypes as C
 import time
 
 import numpy as np
 
-from . import (NON_CVX, Batch, DeviceArray, MpcBuilder, ReferencePaths, SelectParams, Settings, _P, _check, lib,
+from . import (NON_CVX, Batch, DeviceArray, MpcBuilder, ReferencePaths, SelectParams, _P, _check, lib,
                mpc_dims, mpc_pattern, repeat_rows_device, solve_group)
 
 ISSUE_CUTOFF_S = 0.15  # makePlanWithPred: no candidate is issued 0.15 s after the replan started (:613)
@@ -70,15 +74,17 @@ class DeviceReplan:
                                     vals=outs))
 
     def run(self, pos, vel, xref, prev, first_time, prev_count, dyn_cur, pred_pos, pred_size, prob, timings=None,
-            solver_time_limit=None, t_start=None, issue_cutoff_s=ISSUE_CUTOFF_S):
+            solver_time_limit=None, t_start=None, issue_cutoff_s=ISSUE_CUTOFF_S, profile=False):
         """Returns dict(best_cand, cand_type, cand_slot, ob_idx, x_single, x_pair, info_single, info_pair,
         xref, issued, time_limit, valid).  xref: the reference of every instance [I][N][8], or an
         impc.ReferencePaths -- the instances' input paths and reference-tracking state, whose
         getReferenceTraj / getXRef then runs on the device (mpcPlanner.cpp:968-981, 1199-1231) from
         `pos`.  Budget (module docstring): t_start is the replan's startTime (perf_counter seconds,
         default: entry to run); solver_time_limit, when given, is solverTimeLimit_ and sets every
-        candidate's OSQP time_limit to max(limit - elapsed, limit); the settings' own time_limit
-        applies otherwise.  When the cut-off has passed, x_* / info_* are None."""
+        candidate's OSQP time_limit to max(limit - elapsed, limit) -- on instances whose first_time is
+        0 -- and the settings' own time_limit applies otherwise.  When the cut-off has passed, x_* /
+        info_* are None.  profile: also return each candidate QP's device latency (ms, from the
+        tick its time limit counts from) as lat_single / lat_pair."""
         I, K, L, N = self.I, self.K, self.L, self.N
         t = {}
         t0 = time.perf_counter()
@@ -124,15 +130,18 @@ class DeviceReplan:
         time_limit = self.settings.time_limit
         if solver_time_limit is not None:
             time_limit = max(solver_time_limit - elapsed, solver_time_limit)
-        for sh in self.shapes:
-            s = Settings.from_buffer_copy(self.settings)
-            s.time_limit = time_limit
-            sh["batch"].set_settings(s)
-        results = None
+        limited = np.asarray(first_time).reshape(I) == 0  # setTimeLimit only when not firstTime_ (:442-444)
+        for sh, cnt in zip(self.shapes, (4, 2)):
+            sh["batch"].set_settings(self.settings)
+            sh["batch"].set_time_limits(np.repeat(np.where(limited, time_limit, 0.0), cnt))
+            sh["batch"].set_profiling(profile)
+        results = lat = None
         if issued:
             solve_group([sh["batch"] for sh in self.shapes])
             self.ctx.synchronize()
             results = [sh["batch"].get() for sh in self.shapes]
+            if profile:
+                lat = [sh["batch"].qp_latency() for sh in self.shapes]
         # candidate c of instance i sits at row 4i+slot of the single-intent batch (slot < 4) or
         # 2i+slot-4 of the two-intent batch (fanout.hpp k_fanout_candidates)
         slot = f["cand_slot"].get()
@@ -171,6 +180,7 @@ class DeviceReplan:
                    ob_idx=f["ob_idx"].get(), xref=xref_used, issued=issued, time_limit=time_limit, valid=valid)
         for k, (sh, nm) in enumerate(zip(self.shapes, ("single", "pair"))):
             out["x_" + nm], out["info_" + nm] = (results[k][0], results[k][2]) if issued else (None, None)
+            out["lat_" + nm] = lat[k] if lat is not None else None
             out["vals_" + nm] = [v.get() for v in sh["vals"]]
         return out
 

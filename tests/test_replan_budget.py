@@ -1,7 +1,9 @@
 """The replan's wall-clock budget (makePlanWithPred, mpcPlanner.cpp:609-628): the 0.15 s candidate
-issue cut-off, timeLimit = max(solverTimeLimit_ - time, solverTimeLimit_) on every candidate, and
+issue cut-off, timeLimit = max(solverTimeLimit_ - time, solverTimeLimit_) on every candidate of an
+instance that is not on its first plan (solveTraj sets it only when not firstTime_, :442-444), and
 the selection over the candidates whose solveTraj succeeded (every OSQP status but NON_CVX,
-:513-518)."""
+:513-518).  The limit is measured on the device's constant-rate clock, whose rate is read from
+the device (hipDeviceAttributeWallClockRate) and checked against HIP events here."""
 import time
 
 import numpy as np
@@ -23,15 +25,53 @@ def test_candidate_valid_maps_slots_to_batch_rows():
     assert ISSUE_CUTOFF_S == 0.15
 
 
-def _scenario(I=16, K=3, N=20, seed=811):
+def _scenario(I=16, K=3, N=20, seed=811, first_time=None):
     buckets = scenarios.intent_config(N=N, K=K, instances=I, hyps=6, seed=seed)
     inst = next(iter(buckets.values()))["instances"]
     p, pd = impc.mpc_params(horizon=N)
     L = inst["pred"].shape[3]
     pred_size = np.broadcast_to(inst["size"], inst["pred"].shape).copy()
-    args = (inst["pos"], inst["vel"], inst["xref"], inst["prev"], np.ones(I, np.int8), np.full(I, N, np.int32),
+    ft = np.zeros(I, np.int8) if first_time is None else np.asarray(first_time, np.int8)
+    args = (inst["pos"], inst["vel"], inst["xref"], inst["prev"], ft, np.full(I, N, np.int32),
             inst["obp"], inst["pred"], pred_size, inst["prob_all"])
     return p, pd, I, K, L, args
+
+
+def _describe(lim, free, nm, rows):
+    st, it = lim["info_" + nm]["status_val"], lim["info_" + nm]["iter"]
+    lat = lim["lat_" + nm]
+    return "; ".join(f"{nm}[{r}] status {st[r]} iter {it[r]} (free {free['info_' + nm]['iter'][r]}) "
+                     f"latency {lat[r]:.3f} ms" for r in rows[:12])
+
+
+@pytest.mark.gpu
+def test_device_clock_rate_matches_hip_events(ctx):
+    hz = ctx.clock_rate()
+    assert 1e6 <= hz <= 1e10, hz
+    for s in (0.02, 0.1):
+        ev = ctx.clock_check(s)
+        # one launch of one wavefront: launch overhead is microseconds
+        assert abs(ev - s) <= 0.02 * s + 2e-4, (s, ev, hz)
+
+
+@pytest.mark.gpu
+def test_budget_nonbinding_limit_is_bit_identical(ctx):
+    """A limit no QP comes near (100 s) takes the grouped kernel's time-limited loop (deltas every
+    iteration, a team clock reduction per iteration) and must change nothing."""
+    p, pd, I, K, L, args = _scenario()
+    rp = DeviceReplan(ctx, p, pd, I, K, L, impc.default_settings(verbose=0))
+    try:
+        free = rp.run(*args)
+        lim = rp.run(*args, solver_time_limit=100.0, profile=True)
+        assert lim["issued"] and lim["time_limit"] == 100.0
+        for nm in ("single", "pair"):
+            np.testing.assert_array_equal(lim["info_" + nm]["status_val"], free["info_" + nm]["status_val"])
+            np.testing.assert_array_equal(lim["info_" + nm]["iter"], free["info_" + nm]["iter"])
+            np.testing.assert_array_equal(lim["x_" + nm], free["x_" + nm])
+            assert (lim["lat_" + nm] > 0).all() and (lim["lat_" + nm] < 1e5).all()
+        np.testing.assert_array_equal(lim["best_cand"], free["best_cand"])
+    finally:
+        rp.close()
 
 
 @pytest.mark.gpu
@@ -40,18 +80,23 @@ def test_budget_time_limit_and_cutoff(ctx):
     rp = DeviceReplan(ctx, p, pd, I, K, L, impc.default_settings(verbose=0))
     try:
         free = rp.run(*args)
-        # solverTimeLimit_ = 0.05 s (mpcPlanner.cpp:167), measured on the device clock from each
-        # QP's dequeue: a QP that finishes inside it is bit-identical to the unlimited replan; one
-        # that reaches it (a slow or shared box) stops early with OSQP_TIME_LIMIT_REACHED
-        lim = rp.run(*args, solver_time_limit=0.05)
+        # solverTimeLimit_ = 0.05 s (mpcPlanner.cpp:167), counted on the device clock from the tick
+        # the QP's setup starts.  Strict: a QP that reports OSQP_TIME_LIMIT_REACHED must have run at
+        # least that long by the same clock (its recorded latency), and every other QP is bit-identical
+        # to the unlimited replan
+        lim = rp.run(*args, solver_time_limit=0.05, profile=True)
         assert lim["issued"] and lim["time_limit"] == 0.05
         hit_any = False
         for nm in ("single", "pair"):
-            hit = lim["info_" + nm]["status_val"] == impc.TIME_LIMIT_REACHED
+            st = lim["info_" + nm]["status_val"]
+            hit = st == impc.TIME_LIMIT_REACHED
             hit_any |= bool(hit.any())
+            early = np.flatnonzero(hit & (lim["lat_" + nm] < 50.0))
+            assert early.size == 0, "time limit fired early: " + _describe(lim, free, nm, early)
             ok = ~hit
-            np.testing.assert_array_equal(lim["x_" + nm][ok], free["x_" + nm][ok])
-            np.testing.assert_array_equal(lim["info_" + nm]["iter"][ok], free["info_" + nm]["iter"][ok])
+            diff = np.flatnonzero(ok & ((lim["x_" + nm] != free["x_" + nm]).any(axis=1) |
+                                        (lim["info_" + nm]["iter"] != free["info_" + nm]["iter"])))
+            assert diff.size == 0, "QPs inside the limit differ: " + _describe(lim, free, nm, diff)
             assert (lim["info_" + nm]["iter"][hit] <= free["info_" + nm]["iter"][hit]).all()
         if not hit_any:
             np.testing.assert_array_equal(lim["best_cand"], free["best_cand"])
@@ -72,3 +117,64 @@ def test_budget_time_limit_and_cutoff(ctx):
         assert (late["valid"] == 0).all() and (late["best_cand"] == -1).all()
     finally:
         rp.close()
+
+
+@pytest.mark.gpu
+def test_budget_no_time_limit_on_first_plan(ctx):
+    """setTimeLimit only when not firstTime_ (mpcPlanner.cpp:442-444): with instances alternating
+    first_time, a limit every QP would exceed stops only the candidates of the others."""
+    I = 16
+    ft = (np.arange(I) % 2).astype(np.int8)
+    p, pd, I, K, L, args = _scenario(I=I, first_time=ft)
+    rp = DeviceReplan(ctx, p, pd, I, K, L, impc.default_settings(verbose=0))
+    try:
+        free = rp.run(*args)
+        tiny = rp.run(*args, solver_time_limit=1e-9)
+        for nm, cnt in (("single", 4), ("pair", 2)):
+            first = np.repeat(ft == 1, cnt)
+            st = tiny["info_" + nm]["status_val"]
+            assert (st[first] != impc.TIME_LIMIT_REACHED).all()
+            np.testing.assert_array_equal(tiny["x_" + nm][first], free["x_" + nm][first])
+            np.testing.assert_array_equal(tiny["info_" + nm]["iter"][first], free["info_" + nm]["iter"][first])
+            assert (st[~first] == impc.TIME_LIMIT_REACHED).mean() >= 0.5
+    finally:
+        rp.close()
+
+
+@pytest.mark.gpu
+def test_per_qp_time_limits_generic_and_structured(ctx):
+    """impc_batch_set_time_limits on both kernels: QPs with limit 0 run to completion bit-identically,
+    QPs with a limit below their solve time stop with OSQP_TIME_LIMIT_REACHED; clearing restores
+    the settings' limit."""
+    buckets = scenarios.intent_config(N=20, K=8, instances=4, hyps=8, seed=5)
+    bk = buckets[min(buckets)]
+    pat, v = bk["pattern"], bk["values"]
+    B = v["q"].shape[0]
+    for kernel in (impc.KERNEL_STRUCTURED, impc.KERNEL_GENERIC):
+        b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], B).set_kernel(kernel)
+        try:
+            b.set_settings(impc.default_settings(verbose=0))
+            b.set_values(v["Px"], v["q"], v["Ax"], v["l"], v["u"])
+            b.warm_start(bk["x_ws"], None)
+            b.solve()
+            x0, _, i0 = b.get()
+            tl = np.where(np.arange(B) % 2 == 0, 0.0, 1e-9)
+            b.set_time_limits(tl)
+            b.set_values(v["Px"], v["q"], v["Ax"], v["l"], v["u"])
+            b.warm_start(bk["x_ws"], None)
+            b.solve()
+            x1, _, i1 = b.get()
+            free = tl == 0
+            np.testing.assert_array_equal(x1[free], x0[free])
+            np.testing.assert_array_equal(i1["iter"][free], i0["iter"][free])
+            assert (i1["status_val"][~free] == impc.TIME_LIMIT_REACHED).mean() >= 0.5
+            b.set_time_limits(None)
+            b.set_values(v["Px"], v["q"], v["Ax"], v["l"], v["u"])
+            b.warm_start(bk["x_ws"], None)
+            b.solve()
+            x2, _, i2 = b.get()
+            np.testing.assert_array_equal(x2, x0)
+            with pytest.raises(impc.ImpcError):
+                b.set_time_limits(np.full(B, -1.0))
+        finally:
+            b.close()
