@@ -5,6 +5,11 @@
 //                   stage-structured mpcPlanner QP (impc_mpc_build_*) through the shim's
 //                   solve -> updateGradient -> solve -> updateBounds -> solve sequence against
 //                   a direct persistent batch of the C-ABI (exit 0 = pass)
+//   shim_test replay <in> <out> : the solveTraj call sequence (new Solver per QP, settings,
+//                   set*, initSolver, setWarmStart(x, y = 0), solveProblem, get*) over the QPs of
+//                   <in>, optionally followed by updateGradient -> solveProblem -> updateBounds ->
+//                   solveProblem; results to <out> for tests/test_shim.py to check against the
+//                   oracle (not against the C-ABI)
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -126,7 +131,80 @@ static void structured_case() {
     impc_ctx_destroy(ctx);
 }
 
+// Replay file layout (little-endian): int64 header {n, m, nnzP, nnzA, nqp, flags} (flags bit 0:
+// warm start x per QP, bit 1: update sequence q2 / l3 / u3 per QP), int64 Pp[n+1] Pi Ap[n+1] Ai,
+// then per QP double Px q Ax l u [x_ws] [q2 l3 u3].  Output per QP and step: double status, iter,
+// obj, x[n], y[m].  P is inserted with both triangles (as an Eigen user holding the full symmetric
+// matrix does); the shim keeps the upper one (OsqpEigen Data.tpp:38-39).
+static int replay(const char *in, const char *out) {
+    FILE *f = std::fopen(in, "rb");
+    if (!f) return 2;
+    int64_t h[6];
+    if (std::fread(h, sizeof h, 1, f) != 1) return 2;
+    const int64_t n = h[0], m = h[1], nnzP = h[2], nnzA = h[3], nqp = h[4], flags = h[5];
+    auto rd = [&](auto &v, size_t k) { v.resize(k); return std::fread(v.data(), sizeof(v[0]), k, f) == k; };
+    std::vector<int64_t> Pp, Pi, Ap, Ai;
+    if (!rd(Pp, n + 1) || !rd(Pi, nnzP) || !rd(Ap, n + 1) || !rd(Ai, nnzA)) return 2;
+    FILE *o = std::fopen(out, "wb");
+    if (!o) return 2;
+    auto vec = [](const std::vector<double> &v) {
+        Eigen::VectorXd e((Eigen::Index)v.size());
+        for (size_t k = 0; k < v.size(); k++) e((Eigen::Index)k) = v[k];
+        return e;
+    };
+    for (int64_t qp = 0; qp < nqp; qp++) {
+        std::vector<double> Px, q, Ax, l, u, xw, q2, l3, u3;
+        if (!rd(Px, nnzP) || !rd(q, n) || !rd(Ax, nnzA) || !rd(l, m) || !rd(u, m)) return 2;
+        if ((flags & 1) && !rd(xw, n)) return 2;
+        if ((flags & 2) && (!rd(q2, n) || !rd(l3, m) || !rd(u3, m))) return 2;
+        Eigen::SparseMatrix<double> P((Eigen::Index)n, (Eigen::Index)n), A((Eigen::Index)m, (Eigen::Index)n);
+        for (int64_t j = 0; j < n; j++) {
+            for (int64_t k = Pp[j]; k < Pp[j + 1]; k++) {
+                P.insert(Pi[k], j) = Px[k];
+                if (Pi[k] != j) P.insert(j, Pi[k]) = Px[k];
+            }
+            for (int64_t k = Ap[j]; k < Ap[j + 1]; k++) A.insert(Ai[k], j) = Ax[k];
+        }
+        OsqpEigen::Solver solver;  // mpcPlanner.cpp:436-527
+        solver.settings()->setVerbosity(false);
+        solver.settings()->setWarmStart(true);
+        solver.data()->setNumberOfVariables((int)n);
+        solver.data()->setNumberOfConstraints((int)m);
+        Eigen::VectorXd qv = vec(q), lv = vec(l), uv = vec(u);
+        CHECK(solver.data()->setHessianMatrix(P));
+        CHECK(solver.data()->setGradient(qv));
+        CHECK(solver.data()->setLinearConstraintsMatrix(A));
+        CHECK(solver.data()->setLowerBound(lv));
+        CHECK(solver.data()->setUpperBound(uv));
+        CHECK(solver.initSolver());
+        if (flags & 1) {
+            Eigen::VectorXd x0 = vec(xw), y0;
+            y0.setZero((Eigen::Index)m);
+            CHECK(solver.setWarmStart(x0, y0));
+        }
+        const int steps = (flags & 2) ? 3 : 1;
+        for (int step = 0; step < steps; step++) {
+            if (step == 1) CHECK(solver.updateGradient(vec(q2)));
+            if (step == 2) CHECK(solver.updateBounds(vec(l3), vec(u3)));
+            CHECK(solver.solveProblem() == OsqpEigen::ErrorExitFlag::NoError);
+            double hdr[3] = {(double)solver.getStatus(), (double)solver.getIterations(), solver.getObjValue()};
+            std::fwrite(hdr, sizeof(double), 3, o);
+            const Eigen::VectorXd &x = solver.getSolution();
+            const Eigen::VectorXd &y = solver.getDualSolution();
+            CHECK(x.size() == n && y.size() == m);
+            std::fwrite(x.data(), sizeof(double), (size_t)n, o);
+            std::fwrite(y.data(), sizeof(double), (size_t)m, o);
+        }
+        solver.clearSolver();
+    }
+    std::fclose(f);
+    std::fclose(o);
+    std::printf("replay: %lld QP(s), %d failure(s)\n", (long long)nqp, fails);
+    return fails ? 1 : 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc > 3 && std::strcmp(argv[1], "replay") == 0) return replay(argv[2], argv[3]);
     const bool gpu = argc > 1 && std::strcmp(argv[1], "gpu") == 0;
     // OSQP demo problem: P = [[4,1],[1,2]] (both triangles inserted, as Eigen users do),
     // q = (1,1), A = [[1,1],[1,0],[0,1]], l = (1,0,0), u = (1,0.7,0.7); x* = (0.3,0.7), y* = (-2.9,0,0.2)

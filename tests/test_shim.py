@@ -4,6 +4,7 @@ mpcPlanner::solveTraj call sequence (reference mpcPlanner.cpp:436-527) by tests/
 import os
 import subprocess
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -28,3 +29,105 @@ def test_shim_conversion_and_no_device_behaviour():
 def test_shim_solves_on_gpu():
     rc, out = run("gpu")
     assert rc == 0, out
+
+
+def _replay(tmp_path, cfg, updates=None):
+    """Run the QPs of cfg through the shim's solveTraj call sequence (shim_test replay) and read
+    back status / iterations / objective / x / y per solve step."""
+    pat, v = cfg["pattern"], cfg["values"]
+    n, m = int(pat["n"]), int(pat["m"])
+    B = v["q"].shape[0]
+    xw = cfg.get("x_ws")
+    flags = (1 if xw is not None else 0) | (2 if updates is not None else 0)
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
+    with open(fin, "wb") as f:
+        np.array([n, m, len(pat["Pi"]), len(pat["Ai"]), B, flags], np.int64).tofile(f)
+        for k in ("Pp", "Pi", "Ap", "Ai"):
+            np.ascontiguousarray(pat[k], np.int64).tofile(f)
+        for i in range(B):
+            for k in ("Px", "q", "Ax", "l", "u"):
+                np.ascontiguousarray(v[k][i], float).tofile(f)
+            if xw is not None:
+                np.ascontiguousarray(xw[i], float).tofile(f)
+            if updates is not None:
+                for a in updates:
+                    np.ascontiguousarray(a[i], float).tofile(f)
+    p = subprocess.run([EXE, "replay", str(fin), str(fout)], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    steps = 3 if updates is not None else 1
+    raw = np.fromfile(fout, float).reshape(B, steps, 3 + n + m)
+    return [(raw[:, s, 3:3 + n], raw[:, s, 3 + n:], raw[:, s, 0].astype(int), raw[:, s, 1].astype(int),
+             raw[:, s, 2]) for s in range(steps)]
+
+
+def _check(step, ref, rtol=1e-5):
+    """BASELINE.json's parity bar against the oracle: identical status and iteration count, primal,
+    duals and objective within 1e-5 relative where a solution exists."""
+    x, y, st, it, obj = step
+    xo, yo, so, io_, oo = ref
+    assert np.array_equal(st, so), (st, so)
+    assert np.array_equal(it, io_), (it, io_)
+    has = np.isin(so, (1, 2, -2, -6))
+    assert has.any()
+    rel = lambda a, b: np.abs(a - b).max(axis=1) / np.maximum(np.abs(b).max(axis=1), 1e-12)  # noqa: E731
+    assert rel(x[has], xo[has]).max() <= rtol
+    assert rel(y[has], yo[has]).max() <= rtol
+    assert (np.abs(obj[has] - oo[has]) / np.maximum(np.abs(oo[has]), 1e-12)).max() <= rtol
+
+
+@pytest.mark.gpu
+def test_shim_solvetraj_sequence_vs_oracle(tmp_path):
+    """Row a8: config-1 (first call, cold) and config-3 (intent hypotheses, warm start from the
+    previous plan, y = 0) QPs through OsqpEigen::Solver as solveTraj drives it
+    (mpcPlanner.cpp:436-527), checked against the oracle's osqp_setup + osqp_warm_start +
+    osqp_solve -- the shim's Eigen -> upper-triangle CSC conversion (explicit zeros kept) and
+    its setWarmStart included."""
+    import impc
+    from impc import scenarios
+    from oracle import osqp_oracle as ora
+    os_ = ora.settings_from(impc.default_settings(verbose=0, warm_start=1))
+    cfgs = [scenarios.first_call_config(batch=6, seed=811)]
+    cfgs += list(scenarios.intent_config(instances=2, hyps=8, seed=812).values())
+    for cfg in cfgs:
+        (res,) = _replay(tmp_path, cfg)
+        v = cfg["values"]
+        B = v["q"].shape[0]
+        xw = cfg.get("x_ws")
+        yw = None if xw is None else np.zeros((B, int(cfg["pattern"]["m"])))
+        xo, yo, io = ora.solve_batch(cfg["pattern"], v["Px"], v["q"], v["Ax"], v["l"], v["u"], os_, x_ws=xw,
+                                     y_ws=yw, threads=4)
+        _check(res, (xo, yo, io["status_val"], io["iter"], io["obj_val"]))
+
+
+@pytest.mark.gpu
+def test_shim_update_sequence_vs_persistent_oracle(tmp_path):
+    """Row a8, persistent use: solve -> updateGradient -> solve -> updateBounds -> solve through the
+    shim (Solver.hpp updateGradient / updateBounds -> osqp_update_lin_cost / osqp_update_bounds)
+    against the oracle's persistent workspace over the same sequence."""
+    import impc
+    from impc import scenarios
+    from oracle import osqp_oracle as ora
+    os_ = ora.settings_from(impc.default_settings(verbose=0, warm_start=1))
+    bk = scenarios.intent_config(instances=1, hyps=8, seed=813)[8]
+    v = bk["values"]
+    B, m = v["q"].shape[0], int(bk["pattern"]["m"])
+    rng = np.random.default_rng(814)
+    q2 = v["q"] * (1 + 0.05 * rng.standard_normal(v["q"].shape))
+    l3, u3 = v["l"].copy(), v["u"].copy()
+    fin = np.isfinite(l3) & np.isfinite(u3) & (u3 - l3 > 0.1)
+    l3[fin] += 0.01
+    u3[fin] -= 0.01
+    steps = _replay(tmp_path, bk, updates=(q2, l3, u3))
+    for i in range(B):
+        w = ora.Workspace(bk["pattern"], v["Px"][i], v["q"][i], v["Ax"][i], v["l"][i], v["u"][i], os_)
+        w.warm_start(bk["x_ws"][i], np.zeros(m))
+        refs = [w.solve()]
+        w.update_lin_cost(q2[i])
+        refs.append(w.solve())
+        w.update_bounds(l3[i], u3[i])
+        refs.append(w.solve())
+        w.close()
+        for s, (xo, yo, io) in enumerate(refs):
+            got = tuple(a[i:i + 1] for a in steps[s])
+            _check(got, (xo[None], yo[None], np.array([io["status_val"]]), np.array([io["iter"]]),
+                         np.array([io["obj_val"]])))
