@@ -8,11 +8,13 @@ i.e. everything mpcPlanner::solveTraj asks OsqpEigen for (mpcPlanner.cpp:475-526
 (P, q, A, l, u and the warm start) are resident in HBM before the timed region.
 
 Workloads (--workload):
-  config3 (default; BASELINE.json configs[2], the metric's batch=65536): per GPU 8192 planning
-      instances x 8 intent hypotheses, N=20, 8 predicted dynamic obstacles (hypotheses
-      LEFT+FORWARD / RIGHT+FORWARD carry a 9th), bucketed by obstacle count.  Weak scaling: every
-      rank solves its own 65,536 QPs; an all_gather of the per-QP records returns the hypothesis
-      costs to every rank after the timed region.
+  config3 (default; BASELINE.json configs[2], the metric's batch=65536): 8192 planning instances
+      x 8 intent hypotheses, N=20, 8 predicted dynamic obstacles (hypotheses LEFT+FORWARD /
+      RIGHT+FORWARD carry a 9th), bucketed by obstacle count.  Strong scaling (default): the fixed
+      65,536-QP batch is split across the ranks by planning instance (equal ranges: every instance
+      has the same 8 QPs), and each timed step ends with one RCCL all_gather of every QP's cost
+      record (N > 1).  --scaling weak: every rank solves its own 65,536 QPs and the records are
+      gathered after the timed region.
   config4 (BASELINE.json configs[3]): 262,144 QPs in total (32,768 instances x 8 hypotheses,
       K ~ U{0..20} obstacles), instances sharded across the ranks in contiguous ranges balanced by
       Sigma m (impc.distributed.shard_plan).  Strong scaling: the job is fixed, each rank runs one
@@ -94,7 +96,7 @@ def cpu_info():
     return model
 
 
-def make_batch(impc, ctx, bk, settings, full_values, profile):
+def make_batch(impc, ctx, bk, settings, full_values, profile, queue_weight=None):
     pat, vals = bk["pattern"], bk["values"]
     B = vals["q"].shape[0]
     b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], B)
@@ -107,10 +109,50 @@ def make_batch(impc, ctx, bk, settings, full_values, profile):
         Px0, Ax0, var, Axv = split
         b.set_values_shared(Px0, Ax0, var, Axv, vals["q"], vals["l"], vals["u"])
         nvar = int(var.size)
-    if bk.get("x_ws") is not None:
-        b.warm_start(bk["x_ws"], np.zeros((B, pat["m"])))
+    if bk.get("x_ws") is not None:  # solveTraj: x = previous plan, y = 0 (mpcPlanner.cpp:480-497)
+        b.warm_start(bk["x_ws"], None)
+    if queue_weight is not None:
+        b.set_queue_order(impc.QUEUE_LONGEST_FIRST, queue_weight)
     b.set_profiling(profile)
     return b, nvar
+
+
+def end_to_end(impc, ctx, batches, args, grouped):
+    """PCIe-inclusive steps (SURVEY.md 8d latency definition, end to end): the QP inputs from host
+    arrays (impc_batch_set_values_shared / set_values + the warm start), the solve, and x, y and the
+    info records back into host arrays (impc_batch_get), host wall clock per step.  Outside the
+    headline value, which is measured with the inputs resident in HBM."""
+    # which A entries vary per QP is pattern-level knowledge of the caller (the device builder's
+    # templates), not per-step work: split once, ship the per-QP arrays every step
+    splits = [None if args.full_values else impc.shared_split(bk["values"]["Px"], bk["values"]["Ax"])
+              for bk, _ in batches]
+    times = []
+    for _ in range(args.e2e_steps):
+        ctx.synchronize()
+        t = time.perf_counter()
+        for (bk, b), split in zip(batches, splits):
+            vals = bk["values"]
+            if split is None:
+                b.set_values(vals["Px"], vals["q"], vals["Ax"], vals["l"], vals["u"])
+            else:
+                Px0, Ax0, var, Axv = split
+                b.set_values_shared(Px0, Ax0, var, Axv, vals["q"], vals["l"], vals["u"])
+            if bk.get("x_ws") is not None:
+                b.warm_start(bk["x_ws"], None)
+        if grouped:
+            impc.solve_group([b for _, b in batches])
+        else:
+            for _, b in batches:
+                b.setup()
+                b.solve()
+        for _, b in batches:
+            b.get()
+        times.append(time.perf_counter() - t)
+    qps = sum(b.B for _, b in batches)
+    ms = 1000.0 * float(np.mean(times))
+    return {"qps_per_s": qps / (ms * 1e-3), "ms_per_step": ms, "steps": len(times), "qps": qps,
+            "what": "host wall clock per step, rank-local: host arrays -> impc_batch_set_values_shared + "
+                    "impc_batch_warm_start (H2D, pageable) -> solve -> impc_batch_get (x, y, info D2H)"}
 
 
 def main():
@@ -124,6 +166,16 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=8192, help="QPs solved by the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="CPU baseline threads (the GPU box's CPU share per GPU is 16)")
+    ap.add_argument("--cpu-all-cores", type=int, default=1,
+                    help="also time the CPU baseline with one thread per CPU of the process's affinity set")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="config3: split the fixed 65,536-QP batch across ranks (strong) or 65,536 per rank (weak)")
+    ap.add_argument("--queue", choices=("longest", "fifo"), default="longest",
+                    help="work-queue order of the persistent launches (impc_batch_set_queue_order)")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="single-GPU study: run only rank 0's shard of a W-way strong split (not a headline line)")
+    ap.add_argument("--e2e-steps", type=int, default=2,
+                    help="end-to-end steps after the timed region: host arrays in -> solve -> results on the host")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--full-values", action="store_true",
                     help="ship every QP's full CSC values (default: shared P / dynamics / box values, "
@@ -136,6 +188,8 @@ def main():
     rank, local_rank, world = D.env()
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.shard_of and world != 1:
+        sys.exit("bench.py: --shard-of is a single-GPU study of one rank's shard")
 
     import impc
     from impc import scenarios
@@ -145,23 +199,28 @@ def main():
     dist = D.init("gloo", local_rank) if world > 1 else None
 
     settings = impc.default_settings(verbose=0)
+    strong = args.workload == "config4" or args.scaling == "strong"
     t_gen = time.time()
     if args.workload == "config3":
         buckets = scenarios.intent_config(N=20, K=8, instances=args.instances, hyps=8,
-                                          seed=D.rank_seed(3000, rank))
+                                          seed=3000 if strong else D.rank_seed(3000, rank))
+        if strong:  # equal instance ranges (every instance carries the same 8 hypotheses)
+            bounds = D.equal_instance_bounds(args.instances, args.shard_of or world)
+            buckets = scenarios.slice_instances(buckets, int(bounds[rank]), int(bounds[rank + 1]))
         bks = [bk for _, bk in sorted(buckets.items())]
     else:
         Kinst, w = scenarios.config4_plan(total_qps=args.total_qps)
-        bounds = D.shard_plan(w, world)
+        bounds = D.shard_plan(w, args.shard_of or world)
         lo, hi = int(bounds[rank]), int(bounds[rank + 1])
         bks = scenarios.config4_rank(lo, hi, Kinst)
-        share = [float(w[bounds[r]:bounds[r + 1]].sum()) for r in range(world)]
+        share = [float(w[bounds[r]:bounds[r + 1]].sum()) for r in range(args.shard_of or world)]
     t_gen = time.time() - t_gen
 
     ctx = impc.Context(local_rank)
     batches, nvar = [], []
+    qw = scenarios.queue_weight(bks[0]["params"], bks[0]["N"]) if args.queue == "longest" else None
     for bk in bks:
-        b, nv = make_batch(impc, ctx, bk, settings, args.full_values, profile=True)
+        b, nv = make_batch(impc, ctx, bk, settings, args.full_values, profile=True, queue_weight=qw)
         batches.append((bk, b))
         if nv is not None:
             nvar.append(nv)
@@ -179,7 +238,8 @@ def main():
     comm = D.make_comm(dist, ctx) if (world > 1 or args.workload == "config4") else None
     max_qps = max(counts)
     recv = impc.DeviceArray(ctx, (world * max_qps,), impc.INFO_DTYPE) if comm is not None else None
-    gather_in_step = args.workload == "config4" and not args.no_allgather
+    # strong scaling: the cost records of the step's QPs reach every rank inside the step
+    gather_in_step = (args.workload == "config4" or (strong and world > 1)) and not args.no_allgather
 
     def launch():
         if grouped:  # one persistent launch over all pattern buckets (impc_batch_solve_group)
@@ -233,7 +293,7 @@ def main():
         iters_all.append(info["iter"])
         status_all.append(info["status_val"])
         rho_all.append(info["rho_updates"])
-        recs.append(D.make_records(rank, bk["inst"], bk["hyp"], info))
+        recs.append(D.make_records(rank, bk.get("inst_global", bk["inst"]), bk["hyp"], info))
         alg_bytes += b.B * algorithmic_bytes(pat["n"], pat["m"], bk["K"], bk["N"])
         alg_flops += algorithmic_flops(pat["n"], pat["m"], int(pat["Ap"][-1]), bk["N"], info["iter"])
     iters_all = np.concatenate(iters_all)
@@ -245,7 +305,7 @@ def main():
         # mpcPlanner.cpp:771-887), on the solutions still in HBM; timed on its own
         sel = select_candidates(impc, scenarios, ctx, buckets, dict((bk["K"], b) for bk, b in batches),
                                 pd_params=bks[0]["params"])
-        if comm is not None and not args.no_allgather:  # hypothesis costs to every rank
+        if comm is not None and not args.no_allgather and not gather_in_step:  # costs to every rank
             comm.gather_info([b for _, b in batches], max_qps, recv.ptr)
     gathered = None
     if recv is not None and not args.no_allgather:
@@ -277,14 +337,23 @@ def main():
         except Exception:
             traffic = None
 
+    e2e = end_to_end(impc, ctx, batches, args, grouped) if args.e2e_steps > 0 else None
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         cpu = cpu_baseline(bks, settings, args.cpu_sample, args.cpu_threads)
+        if args.cpu_all_cores:
+            cores = len(os.sched_getaffinity(0))
+            allc = cpu_baseline(bks, settings, min(total_qps, args.cpu_sample * max(1, cores // args.cpu_threads)),
+                                cores)
+            cpu["all_cores"] = {k: allc[k] for k in ("value", "unit", "cores", "sample")}
 
     if args.workload == "config3":
         config = {
-            "workload": "configs[2]: 8192 instances x 8 intent hypotheses per GPU, N=20, 8(+1) dynamic obstacles",
-            "global_batch": global_batch, "batch_per_gpu": total_qps,
+            "workload": ("configs[2]: 65536 QPs = 8192 instances x 8 intent hypotheses, split by instance over the "
+                         "ranks, N=20, 8(+1) dynamic obstacles, per-step RCCL all-gather of the cost records (N>1)")
+            if strong else "configs[2]: 8192 instances x 8 intent hypotheses per GPU, N=20, 8(+1) dynamic obstacles",
+            "global_batch": global_batch, "batch_per_gpu": total_qps, "shard_qps": counts,
             "buckets": {str(bk["K"]): int(b.B) for bk, b in batches},
         }
     else:
@@ -298,6 +367,8 @@ def main():
         "horizon": 20,
         "settings": "OSQP 0.6.2 defaults, adaptive_rho_interval auto->25, warm-started from previous plan",
         "parallelism": f"independent QPs, {world} rank(s)",
+        "queue": ("longest-first (device-estimated key: warm-start violation + q_weight*||q||_inf, "
+                  "impc_batch_set_queue_order)") if args.queue == "longest" else "fifo",
         "values": values_mode + (f" (P and dynamics/box A entries once per bucket, per-QP A entries {nvar_desc})"
                                  if values_mode == "shared" else " (every QP's full CSC values)"),
     })
@@ -312,11 +383,13 @@ def main():
         "p50_latency_ms": qp_lat["p50"] if qp_lat else None,
         "step_latency_ms": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak" if args.workload == "config3" else "strong",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded intent-hypothesis scenarios, SURVEY.md 8d)",
         "config": config,
+        "shard_study": (f"rank 0's shard of a {args.shard_of}-way strong split, alone on one GPU"
+                        if args.shard_of else None),
         "qp_latency_ms": qp_lat,
         "iters": {"mean": float(iters_all.mean()), "p50": float(np.median(iters_all)), "max": int(iters_all.max()),
                   "rho_updates_mean": float(np.concatenate(rho_all).mean())},
@@ -337,6 +410,7 @@ def main():
                     "algorithmic_bytes_per_launch": alg_bytes, "traffic_bytes_per_launch": traffic},
         },
         "cpu_baseline": cpu,
+        "e2e": e2e,
         "selection": sel,
         "cost_allgather": gathered,
         "gen_seconds": t_gen,

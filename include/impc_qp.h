@@ -145,7 +145,8 @@ int impc_batch_set_values_shared(impc_batch b, const double *Px, const double *A
                                  const int64_t *var_pos, const double *Ax_var, const double *q, const double *l,
                                  const double *u);
 
-/* osqp_warm_start(x, y) for every QP (host, QP-major; y may be NULL = zero duals).  As in OSQP
+/* osqp_warm_start(x, y) for every QP (host, QP-major; y may be NULL = zero duals, the solveTraj
+ * warm start: then no duals are uploaded or read by the solve).  As in OSQP
  * it turns the warm_start setting on.  On a set-up workspace (generic kernel after a solve,
  * structured kernel with a persistent workspace) it replaces the iterates and keeps scaling, rho
  * and factor.  Pass x = NULL to clear a pending warm start (the next setup cold-starts). */
@@ -237,6 +238,21 @@ int impc_batch_get_qp_latency(impc_batch b, double *ms);
  * not firstTime_, timeLimit = max(solverTimeLimit_ - t, solverTimeLimit_) at :613-615), so one
  * batch of candidates from several planners carries one limit per QP. */
 int impc_batch_set_time_limits(impc_batch b, const double *time_limit);
+
+/* Work-queue order of the structured kernel's persistent launches (no reference counterpart: the
+ * reference solves each candidate in its own loop iteration, mpcPlanner.cpp:609-628).
+ *   IMPC_QUEUE_FIFO (default): QPs are dequeued in batch order (a grouped launch: batch by batch).
+ *   IMPC_QUEUE_LONGEST_FIRST: before each launch the device estimates every QP's difficulty from its
+ *     own inputs, key = ||A x_ws - proj_[l,u](A x_ws)||_inf + q_weight * ||q||_inf (the warm start's
+ *     constraint violation plus a scale of the linear cost), and the launch dequeues its QPs in
+ *     descending key order across all its batches, so the QPs that run longest start first and the
+ *     launch tail shrinks (a launch is ordered when any of its batches asks for it; each batch's
+ *     keys use its own q_weight).
+ * The order changes no result: each QP is solved alone from its own inputs.  The generic kernel
+ * (one QP per lane, no queue) ignores it. */
+#define IMPC_QUEUE_FIFO 0
+#define IMPC_QUEUE_LONGEST_FIRST 1
+int impc_batch_set_queue_order(impc_batch b, int mode, double q_weight);
 
 /* The device clock the time limits and latencies are measured on: its rate in Hz, from
  * hipDeviceAttributeWallClockRate (queried once per context). */

@@ -11,6 +11,7 @@
 // Inputs are kept QP-major on the device (the layout the C-ABI receives them in); the generic
 // path interleaves them (LDS-tiled transpose) at setup.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -29,6 +30,7 @@
 #include "admm_core.hpp"
 #include "mpc_structure.hpp"
 #include "mpc_wave.hpp"
+#include "queue.hpp"
 #include "symbolic.hpp"
 
 #define IMPC_VERSION "impc_qp 0.2.0 (OSQP 0.6.2 semantics, gfx950)"
@@ -375,7 +377,7 @@ struct GpuTeam {
 
 template <int NL, int VS, int GS, int WPS, int WF>
 __global__ __launch_bounds__(NL, WPS) void k_mpc_wave(impc::WaveTables T, impc::WaveIO io, impc::DevSettings st,
-                                                      unsigned *counter) {
+                                                      unsigned *counter, const uint32_t *__restrict__ ord) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     using LD = impc::WaveLds<NL, VS, GS>;
     GpuTeam<NL> wv{smem + LD::RED_OFF};
@@ -384,9 +386,10 @@ __global__ __launch_bounds__(NL, WPS) void k_mpc_wave(impc::WaveTables T, impc::
     for (;;) {
         if (threadIdx.x == 0) next = atomicAdd(counter, 1u);
         __syncthreads();
-        const unsigned b = next;
+        const unsigned pos = next;
         __syncthreads();
-        if ((int64_t)b >= io.B) break;
+        if ((int64_t)pos >= io.B) break;
+        const unsigned b = ord ? ord[pos] : pos;  // queue order (impc_batch_set_queue_order)
         impc::WaveQP<GpuTeam<NL>, NL, VS, GS, WF> qp(wv, T, io, st, smem);
         qp.solve((int64_t)b);
     }
@@ -406,7 +409,8 @@ struct GroupEntry {
 // CUs idle between launches.  A workgroup reloads the pattern tables when it crosses batches.
 template <int NL, int VS, int GS, int WPS, int WF, bool TIER>
 __global__ __launch_bounds__(NL, WPS) void k_mpc_wave_group(const GroupEntry *__restrict__ g, int count,
-                                                            int64_t total, unsigned *counter) {
+                                                            int64_t total, unsigned *counter,
+                                                            const uint32_t *__restrict__ ord) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     using LD = impc::WaveLds<NL, VS, GS>;
     GpuTeam<NL> wv{smem + LD::RED_OFF};
@@ -415,9 +419,11 @@ __global__ __launch_bounds__(NL, WPS) void k_mpc_wave_group(const GroupEntry *__
     for (;;) {
         if (threadIdx.x == 0) next = atomicAdd(counter, 1u);
         __syncthreads();
-        const unsigned b = next;
+        const unsigned pos = next;
         __syncthreads();
-        if ((int64_t)b >= total) break;
+        if ((int64_t)pos >= total) break;
+        // queue order (impc_batch_set_queue_order): a permutation of the launch's QPs
+        const unsigned b = ord ? ord[pos] : pos;
         int e = 0;
         while (e + 1 < count && (int64_t)b >= g[e + 1].first) e++;
         if (e != cur) {
@@ -529,6 +535,7 @@ struct impc_batch_s {
     impc_info *d_info = nullptr;
     int64_t device_bytes = 0;
     bool values_set = false, has_ws = false;
+    bool ws_y = false;  // the warm start carries duals (else y = 0: nothing uploaded or read)
     unsigned long long *d_qpt = nullptr;  // profiling: per-QP (start, end) device clock
     double *d_tlim = nullptr;  // per-QP time limits (impc_batch_set_time_limits), or none
     bool tlim_on = false;
@@ -559,6 +566,14 @@ struct impc_batch_s {
     impc::DevSym dsym{};
     impc::DevWork dwk{};
     bool generic_dirty = true, generic_setup_done = false, generic_first_run = false;
+    // work-queue order of the structured kernel's persistent launches (impc_batch_set_queue_order)
+    int queue_mode = IMPC_QUEUE_FIFO;
+    double queue_qw = 0.0;
+    int32_t *d_csr = nullptr;  // CSR of A's pattern: row_ptr [m + 1], column [nnzA], CSC entry [nnzA]
+    // order scratch of the launches this batch heads: keys, sorted keys, indices, order, sort temp
+    void *d_qscr = nullptr;
+    int64_t qscr_cap = 0;
+    size_t qtmp_bytes = 0;
     // profiling
     bool profile = false;
     hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -629,7 +644,7 @@ int deinterleave(impc_batch b, const double *src, double *dst_dev, int64_t len, 
 // The structured kernel's view of a batch's inputs / outputs.
 impc::WaveIO wave_io(impc_batch b) {
     impc::WaveIO io{b->B,        b->shared ? b->d_shPx : b->in_Px, b->in_q, b->shared ? b->d_shAx : b->in_Ax,
-                    b->in_l,     b->in_u,   b->in_xws, b->in_yws, b->has_ws ? 1 : 0, b->d_xout, b->d_yout,
+                    b->in_l,     b->in_u,   b->in_xws, b->in_yws, b->has_ws ? (b->ws_y ? 1 : 2) : 0, b->d_xout, b->d_yout,
                     b->d_scal,   b->d_info};
     if (b->profile && b->d_qpt) io.qpt = b->d_qpt;
     if (b->tlim_on) io.tlim = b->d_tlim;
@@ -761,6 +776,7 @@ int generic_setup(impc_batch b, hipStream_t st) {
     if ((rc = interleave(b, b->in_u, const_cast<double *>(w.u), b->m, st))) return rc;
     if (b->has_ws) {
         if ((rc = interleave(b, b->in_xws, const_cast<double *>(w.xws), b->n, st))) return rc;
+        if (!b->ws_y && b->m) HIP_OK(hipMemsetAsync(b->in_yws, 0, sizeof(double) * b->m * b->B, st));
         if ((rc = interleave(b, b->in_yws, const_cast<double *>(w.yws), b->m, st))) return rc;
     }
     if (b->profile) HIP_OK(hipEventRecord(b->ev[0], st));
@@ -823,21 +839,95 @@ int64_t resident_groups(int num_cu, size_t lds, int64_t work) {
 
 // ---- structured path
 template <int VS, int GS, int WF>
-int launch_wave_w(impc_batch b, hipStream_t st, const impc::WaveIO &io) {
+int launch_wave_w(impc_batch b, hipStream_t st, const impc::WaveIO &io, const uint32_t *ord) {
     constexpr int WPS = VS == kWaveVS ? IMPC_WAVES_PER_SIMD : 1;
     using LD = impc::WaveLds<kTeam, VS, GS>;
     const size_t lds = sizeof(double) * (size_t)LD::size(b->wt);  // products sized by the pattern
     if (int rc = ensure_lds_attr(k_mpc_wave<kTeam, VS, GS, WPS, WF>, lds)) return rc;
     const int64_t groups = resident_groups<VS>(b->ctx->num_cu, lds, b->B);
     hipLaunchKernelGGL((k_mpc_wave<kTeam, VS, GS, WPS, WF>), dim3((unsigned)groups), dim3(kTeam), lds, st, b->wt, io,
-                       b->dst, b->d_counter);
+                       b->dst, b->d_counter, ord);
     HIP_OK(hipGetLastError());
     return IMPC_OK;
 }
 template <int VS, int GS>
-int launch_wave(impc_batch b, hipStream_t st, const impc::WaveIO &io) {
+int launch_wave(impc_batch b, hipStream_t st, const impc::WaveIO &io, const uint32_t *ord) {
     constexpr int WS = impc::WaveLds<kTeam, VS, GS>::WSPEC;
-    return b->ms->W == WS ? launch_wave_w<VS, GS, WS>(b, st, io) : launch_wave_w<VS, GS, 0>(b, st, io);
+    return b->ms->W == WS ? launch_wave_w<VS, GS, WS>(b, st, io, ord) : launch_wave_w<VS, GS, 0>(b, st, io, ord);
+}
+
+// ---- work-queue order (impc_batch_set_queue_order, csrc/queue.hpp)
+// CSR of A's pattern with each entry's CSC index, built once per batch on the host
+int build_queue_csr(impc_batch b) {
+    if (b->d_csr) return IMPC_OK;
+    const int64_t m = b->m, nnz = b->nnzA;
+    std::vector<int32_t> h((size_t)(m + 1 + 2 * nnz), 0);
+    int32_t *rp = h.data(), *col = rp + m + 1, *ent = col + nnz;
+    for (int64_t k = 0; k < nnz; k++) rp[b->Ai[(size_t)k] + 1]++;
+    for (int64_t r = 0; r < m; r++) rp[r + 1] += rp[r];
+    std::vector<int32_t> fill(rp, rp + m);
+    for (int64_t j = 0; j < b->n; j++)
+        for (int64_t k = b->Ap[(size_t)j]; k < b->Ap[(size_t)j + 1]; k++) {
+            const int32_t at = fill[(size_t)b->Ai[(size_t)k]]++;
+            col[at] = (int32_t)j;
+            ent[at] = (int32_t)k;
+        }
+    HIP_OK(hipMalloc((void **)&b->d_csr, sizeof(int32_t) * h.size()));
+    b->device_bytes += (int64_t)(sizeof(int32_t) * h.size());
+    return h2d_sync(b->ctx->stream, b->d_csr, h.data(), sizeof(int32_t) * h.size());
+}
+
+// The queue order of one persistent launch over bs[0 .. count) (bs[k]'s QPs at launch-wide queue
+// indices firsts[k] ..): when any of them asks for IMPC_QUEUE_LONGEST_FIRST, every QP's key on the
+// device (each batch with its own q_weight), sorted descending (stable: ties in queue order).
+// *ord = the permutation (scratch of bs[0]), or nullptr for the plain FIFO queue.
+int queue_order(impc_batch *bs, const int64_t *firsts, int count, int64_t total, hipStream_t st,
+                const uint32_t **ord) {
+    *ord = nullptr;
+    bool any = false;
+    for (int k = 0; k < count; k++) any = any || bs[k]->queue_mode == IMPC_QUEUE_LONGEST_FIRST;
+    if (!any || total < 2) return IMPC_OK;
+    if (total > (int64_t)UINT32_MAX) return fail(IMPC_UNSUPPORTED, "queue order: too many QPs in one launch");
+    impc_batch h = bs[0];
+    size_t tmp = 0;
+    HIP_OK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, (const double *)nullptr, (double *)nullptr,
+                                                        (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)total,
+                                                        0, 64, st));
+    auto bytes_for = [](int64_t cap, size_t t) { return (size_t)cap * (2 * sizeof(double) + 2 * sizeof(uint32_t)) + t; };
+    if (total > h->qscr_cap || tmp > h->qtmp_bytes) {
+        IMPC_TRY(ctx_quiesce(h->ctx));  // no launch in flight reads the order being replaced
+        if (h->d_qscr) {
+            HIP_OK(hipFree(h->d_qscr));
+            h->device_bytes -= (int64_t)bytes_for(h->qscr_cap, h->qtmp_bytes);
+        }
+        h->d_qscr = nullptr;
+        h->qscr_cap = std::max(total, h->qscr_cap);
+        h->qtmp_bytes = std::max(tmp, h->qtmp_bytes);
+        HIP_OK(hipMalloc(&h->d_qscr, bytes_for(h->qscr_cap, h->qtmp_bytes)));
+        h->device_bytes += (int64_t)bytes_for(h->qscr_cap, h->qtmp_bytes);
+    }
+    double *key = (double *)h->d_qscr, *key2 = key + h->qscr_cap;
+    uint32_t *idx = (uint32_t *)(key2 + h->qscr_cap), *out = idx + h->qscr_cap;
+    void *t = (void *)(out + h->qscr_cap);
+    for (int k = 0; k < count; k++) {
+        impc_batch b = bs[k];
+        if (b->B == 0) continue;
+        IMPC_TRY(build_queue_csr(b));
+        impc::QueueKeyArgs a{};
+        a.B = b->B, a.n = b->n, a.m = b->m, a.first = firsts[k];
+        a.row_ptr = b->d_csr, a.row_col = b->d_csr + b->m + 1, a.row_ent = b->d_csr + b->m + 1 + b->nnzA;
+        a.shared = b->shared ? 1 : 0;
+        a.Ax = b->shared ? b->d_shAx : b->in_Ax;
+        a.nvar = b->nvar, a.vmap = b->d_vmap, a.Ax_var = b->d_Axv;
+        a.q = b->in_q, a.l = b->in_l, a.u = b->in_u, a.xws = b->in_xws, a.has_ws = b->has_ws ? 1 : 0;
+        a.q_weight = b->queue_qw;
+        const unsigned grid = (unsigned)std::min<int64_t>(b->B, 4096);
+        hipLaunchKernelGGL(impc::k_queue_key, dim3(grid), dim3(256), 0, st, a, key, idx);
+        HIP_OK(hipGetLastError());
+    }
+    HIP_OK(hipcub::DeviceRadixSort::SortPairsDescending(t, tmp, key, key2, idx, out, (int)total, 0, 64, st));
+    *ord = out;
+    return IMPC_OK;
 }
 
 // After a structured solve of a persistent batch: its workspace holds the scaled iterates, and an
@@ -860,14 +950,17 @@ int structured_solve(impc_batch b, hipStream_t st) {
     io.sec = b->d_sec;
 #endif
     if (b->profile) HIP_OK(hipEventRecord(b->ev[2], st));
+    const uint32_t *ord = nullptr;
+    const int64_t first0 = 0;
+    IMPC_TRY(queue_order(&b, &first0, 1, b->B, st, &ord));
     int rc;
     switch (b->vs * 8 + b->gs) {
-        case kWaveVS * 8 + 2: rc = launch_wave<kWaveVS, 2>(b, st, io); break;
-        case kWaveVS * 8 + 3: rc = launch_wave<kWaveVS, 3>(b, st, io); break;
-        case kWaveVS * 8 + 4: rc = launch_wave<kWaveVS, 4>(b, st, io); break;
-        case kWaveVSLong * 8 + 2: rc = launch_wave<kWaveVSLong, 2>(b, st, io); break;
-        case kWaveVSLong * 8 + 3: rc = launch_wave<kWaveVSLong, 3>(b, st, io); break;
-        case kWaveVSLong * 8 + 4: rc = launch_wave<kWaveVSLong, 4>(b, st, io); break;
+        case kWaveVS * 8 + 2: rc = launch_wave<kWaveVS, 2>(b, st, io, ord); break;
+        case kWaveVS * 8 + 3: rc = launch_wave<kWaveVS, 3>(b, st, io, ord); break;
+        case kWaveVS * 8 + 4: rc = launch_wave<kWaveVS, 4>(b, st, io, ord); break;
+        case kWaveVSLong * 8 + 2: rc = launch_wave<kWaveVSLong, 2>(b, st, io, ord); break;
+        case kWaveVSLong * 8 + 3: rc = launch_wave<kWaveVSLong, 3>(b, st, io, ord); break;
+        case kWaveVSLong * 8 + 4: rc = launch_wave<kWaveVSLong, 4>(b, st, io, ord); break;
         default: return fail(IMPC_UNSUPPORTED, "no structured kernel for this size");
     }
     if (rc) return rc;
@@ -883,22 +976,22 @@ int structured_solve(impc_batch b, hipStream_t st) {
 
 template <int VS, int GS, int WF, bool TIER>
 int launch_group_w(impc_ctx ctx, hipStream_t st, const GroupEntry *entries, int count, int64_t total, size_t lds,
-                   unsigned *counter) {
+                   unsigned *counter, const uint32_t *ord) {
     constexpr int WPS = VS == kWaveVS ? IMPC_WAVES_PER_SIMD : 1;
     if (int rc = ensure_lds_attr(k_mpc_wave_group<kTeam, VS, GS, WPS, WF, TIER>, lds)) return rc;
     const int64_t groups = resident_groups<VS>(ctx->num_cu, lds, total);
     hipLaunchKernelGGL((k_mpc_wave_group<kTeam, VS, GS, WPS, WF, TIER>), dim3((unsigned)groups), dim3(kTeam), lds, st,
-                       entries, count, total, counter);
+                       entries, count, total, counter, ord);
     HIP_OK(hipGetLastError());
     return IMPC_OK;
 }
 // spec: every batch of the group has the shape's default horizon
 template <int VS, int GS, bool TIER = false>
 int launch_group(impc_ctx ctx, hipStream_t st, const GroupEntry *entries, int count, int64_t total, size_t lds,
-                 unsigned *counter, bool spec) {
+                 unsigned *counter, bool spec, const uint32_t *ord) {
     constexpr int WS = impc::WaveLds<kTeam, VS, GS>::WSPEC;
-    return spec ? launch_group_w<VS, GS, WS, TIER>(ctx, st, entries, count, total, lds, counter)
-                : launch_group_w<VS, GS, 0, TIER>(ctx, st, entries, count, total, lds, counter);
+    return spec ? launch_group_w<VS, GS, WS, TIER>(ctx, st, entries, count, total, lds, counter, ord)
+                : launch_group_w<VS, GS, 0, TIER>(ctx, st, entries, count, total, lds, counter, ord);
 }
 
 // dynamic LDS bytes of the structured kernel for a shape (team VS, GS) and pattern (CG, n)
@@ -1133,7 +1226,7 @@ int impc_batch_destroy(impc_batch b) {
         if (e) (void)hipEventDestroy(e);
     void *ptrs[] = {b->d_in,     b->d_xout,  b->d_yout,  b->d_info,  b->d_tables, b->d_scal, b->d_counter,
                     b->d_sym,    b->d_work,  b->d_sec,   b->d_shPx,  b->d_shAx,   b->d_Axv,  b->d_vmap,
-                    b->d_qpt,    b->d_persist, b->d_tlim};
+                    b->d_qpt,    b->d_persist, b->d_tlim, b->d_csr, b->d_qscr};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete b;
@@ -1283,12 +1376,10 @@ int impc_batch_warm_start(impc_batch b, const double *x, const double *y) {
     }
     const size_t B = (size_t)b->B;
     IMPC_TRY(h2d_sync(b->ctx->stream, b->in_xws, x, sizeof(double) * b->n * B));
-    if (b->m) {
-        if (y)
-            IMPC_TRY(h2d_sync(b->ctx->stream, b->in_yws, y, sizeof(double) * b->m * B));
-        else
-            IMPC_TRY(fill0_sync(b->ctx->stream, b->in_yws, sizeof(double) * b->m * B));
-    }
+    // y = 0 (the solveTraj warm start, mpcPlanner.cpp:480-497): nothing is uploaded, the structured
+    // kernel reads no duals (WaveIO::has_ws == 2) and the generic path zero-fills its copy
+    if (b->m && y) IMPC_TRY(h2d_sync(b->ctx->stream, b->in_yws, y, sizeof(double) * b->m * B));
+    b->ws_y = y != nullptr;
     // osqp_warm_start turns the warm_start setting on (osqp.c, oracle ora_warm_start)
     b->settings.warm_start = 1;
     b->dst.warm_start = 1;
@@ -1296,6 +1387,7 @@ int impc_batch_warm_start(impc_batch b, const double *x, const double *y) {
         // a set-up generic workspace takes the warm start in place, keeping scaling, rho and factor
         hipStream_t st = b->ctx->stream;
         int rc = interleave(b, b->in_xws, const_cast<double *>(b->dwk.xws), b->n, st);
+        if (!rc && !b->ws_y && b->m) rc = fill0_sync(st, b->in_yws, sizeof(double) * b->m * b->B);
         if (!rc) rc = interleave(b, b->in_yws, const_cast<double *>(b->dwk.yws), b->m, st);
         if (rc) return rc;
         hipLaunchKernelGGL(k_warm_start, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk,
@@ -1406,16 +1498,24 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
         if (L.total == 0) continue;
         HIP_OK(hipMemsetAsync(L.counter, 0, 256, st));
         const GroupEntry *E = ctx->d_group + L.first;
+        std::vector<impc_batch> lb((size_t)L.count);
+        std::vector<int64_t> lf((size_t)L.count);
+        for (int k = 0; k < L.count; k++) {
+            lb[(size_t)k] = bs[order[(size_t)(L.first + k)]];
+            lf[(size_t)k] = entries[(size_t)(L.first + k)].first;
+        }
+        const uint32_t *ord = nullptr;
+        IMPC_TRY(queue_order(lb.data(), lf.data(), L.count, L.total, st, &ord));
         int rc;
         switch (b0->vs * 8 + L.gs + (L.tier ? 64 : 0)) {
-            case 64 + kWaveVS * 8 + 2: rc = launch_group<kWaveVS, 2, true>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec); break;
-            case 64 + kWaveVS * 8 + 3: rc = launch_group<kWaveVS, 3, true>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec); break;
-            case kWaveVS * 8 + 2: rc = launch_group<kWaveVS, 2>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec); break;
-            case kWaveVS * 8 + 3: rc = launch_group<kWaveVS, 3>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec); break;
-            case kWaveVS * 8 + 4: rc = launch_group<kWaveVS, 4>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec); break;
-            case kWaveVSLong * 8 + 2: rc = launch_group<kWaveVSLong, 2>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec); break;
-            case kWaveVSLong * 8 + 3: rc = launch_group<kWaveVSLong, 3>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec); break;
-            case kWaveVSLong * 8 + 4: rc = launch_group<kWaveVSLong, 4>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec); break;
+            case 64 + kWaveVS * 8 + 2: rc = launch_group<kWaveVS, 2, true>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord); break;
+            case 64 + kWaveVS * 8 + 3: rc = launch_group<kWaveVS, 3, true>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord); break;
+            case kWaveVS * 8 + 2: rc = launch_group<kWaveVS, 2>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord); break;
+            case kWaveVS * 8 + 3: rc = launch_group<kWaveVS, 3>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord); break;
+            case kWaveVS * 8 + 4: rc = launch_group<kWaveVS, 4>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord); break;
+            case kWaveVSLong * 8 + 2: rc = launch_group<kWaveVSLong, 2>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord); break;
+            case kWaveVSLong * 8 + 3: rc = launch_group<kWaveVSLong, 3>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord); break;
+            case kWaveVSLong * 8 + 4: rc = launch_group<kWaveVSLong, 4>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord); break;
             default: return fail(IMPC_UNSUPPORTED, "no structured kernel for this size");
         }
         if (rc) return rc;
@@ -1592,6 +1692,18 @@ int impc_batch_set_time_limits(impc_batch b, const double *time_limit) {
     }
     IMPC_TRY(h2d_sync(b->ctx->stream, b->d_tlim, time_limit, sizeof(double) * (size_t)b->B));
     b->tlim_on = true;
+    return IMPC_OK;
+}
+
+int impc_batch_set_queue_order(impc_batch b, int mode, double q_weight) {
+    if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
+    if (mode != IMPC_QUEUE_FIFO && mode != IMPC_QUEUE_LONGEST_FIRST)
+        return fail(IMPC_INVALID_ARGUMENT, "unknown queue order");
+    if (!(q_weight >= 0.0 && q_weight < 1e300)) return fail(IMPC_INVALID_ARGUMENT, "q_weight must be finite, >= 0");
+    HIP_OK(hipSetDevice(b->ctx->device));
+    if (mode == IMPC_QUEUE_LONGEST_FIRST) IMPC_TRY(build_queue_csr(b));
+    b->queue_mode = mode;
+    b->queue_qw = q_weight;
     return IMPC_OK;
 }
 

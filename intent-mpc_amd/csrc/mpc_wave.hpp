@@ -121,7 +121,7 @@ struct WaveTables {
 struct WaveIO {
     int64_t B;
     const double *Px, *q, *Ax, *l, *u, *xws, *yws;  // QP-major inputs
-    int32_t has_ws;
+    int32_t has_ws;    // 0: none, 1: x and y, 2: x with y = 0 (yws not read)
     double *xo, *yo;   // QP-major outputs (unscaled)
     double *scal;      // per-QP scratch [B][n + n + mg]: D, E(box), E(general)
     impc_info *info;
@@ -1925,7 +1925,7 @@ struct WaveQP {
                 int ov = T.var_orig[NL * s + L];
                 double xv = io.xws[b * n + ov];
                 x[s] = st.scaling > 0 ? (1. / D[s]) * xv : xv;
-                double yv = io.yws[b * m + T.var_boxrow[NL * s + L]];
+                double yv = io.has_ws == 1 ? io.yws[b * m + T.var_boxrow[NL * s + L]] : 0.0;
                 if (st.scaling > 0) {
                     yv = (1. / Eb[s]) * yv;
                     yv *= c;
@@ -1937,7 +1937,7 @@ struct WaveQP {
             wv.sync();
             _Pragma("unroll") for (int s = 0; s < GS; s++) {
                 if (!gok[s]) continue;
-                double yv = io.yws[b * m + T.gen_row[NL * s + L]];
+                double yv = io.has_ws == 1 ? io.yws[b * m + T.gen_row[NL * s + L]] : 0.0;
                 if (st.scaling > 0) {
                     yv = (1. / Eg[s]) * yv;
                     yv *= c;

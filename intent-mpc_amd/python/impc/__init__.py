@@ -133,6 +133,7 @@ _sig("impc_comm_gather_info", C.c_int, _P, C.POINTER(_P), C.c_int, C.c_int64, _P
 _sig("impc_comm_max", C.c_int, _P, C.POINTER(C.c_double))
 _sig("impc_ctx_timer_mark", C.c_int, _P, _P)
 _sig("impc_batch_set_time_limits", C.c_int, _P, _dp)
+_sig("impc_batch_set_queue_order", C.c_int, _P, C.c_int, C.c_double)
 _sig("impc_ctx_clock_rate", C.c_int, _P, _dp)
 _sig("impc_ctx_clock_check", C.c_int, _P, C.c_double, _dp)
 _sig("impc_ctx_timer_read", C.c_int, _P, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_int64))
@@ -212,6 +213,7 @@ _sig("impc_fanout_candidates_device", C.c_int, _P, C.c_int64, C.c_int32, C.c_int
 
 # every symbol declared in include/*.h (checked by tests/test_abi.py)
 KERNEL_AUTO, KERNEL_GENERIC, KERNEL_STRUCTURED = 0, 1, 2
+QUEUE_FIFO, QUEUE_LONGEST_FIRST = 0, 1
 
 EXPORTED = [
     "impc_default_settings", "impc_last_error", "impc_version", "impc_ctx_create", "impc_ctx_destroy",
@@ -230,7 +232,7 @@ EXPORTED = [
     "impc_minsnap_corridor_bounds",
     "impc_reference_traj_device", "impc_repeat_rows_device", "impc_comm_unique_id", "impc_comm_create", "impc_comm_destroy", "impc_comm_allgather", "impc_comm_gather_info",
     "impc_comm_max", "impc_ctx_timer_mark", "impc_ctx_timer_read", "impc_batch_set_time_limits",
-    "impc_ctx_clock_rate", "impc_ctx_clock_check",
+    "impc_ctx_clock_rate", "impc_ctx_clock_check", "impc_batch_set_queue_order",
 ]
 
 
@@ -380,6 +382,11 @@ class Batch:
         if a.size != self.B:
             raise ValueError(f"set_time_limits: {a.size} values, expected B = {self.B}")
         _check(lib.impc_batch_set_time_limits(self.h, _d(a)), "impc_batch_set_time_limits")
+
+    def set_queue_order(self, mode, q_weight=0.0):
+        """impc_batch_set_queue_order: QUEUE_FIFO or QUEUE_LONGEST_FIRST (device-estimated difficulty
+        key = warm-start violation + q_weight * ||q||_inf, descending)."""
+        _check(lib.impc_batch_set_queue_order(self.h, int(mode), float(q_weight)), "impc_batch_set_queue_order")
 
     def set_persistent(self, on=True):
         _check(lib.impc_batch_set_persistent(self.h, int(on)), "impc_batch_set_persistent")

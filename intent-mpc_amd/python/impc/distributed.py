@@ -104,6 +104,13 @@ def shard_plan(weights, world):
     return np.array(bounds, dtype=np.int64)
 
 
+def equal_instance_bounds(instances, world):
+    """Config 3 strong scaling: the fixed batch's planning instances in `world` contiguous ranges
+    of equal size (+-1); every instance carries the same 8 hypothesis QPs, so equal instance counts
+    are equal QP counts and equal constraint sums.  Returns bounds [world + 1]."""
+    return np.linspace(0, int(instances), int(world) + 1).astype(np.int64)
+
+
 def unpad(flat, counts):
     """Rank-ordered records from an all-gather of zero-padded blocks: flat [world * max, ...]
     (rank r's block at rows [r * max, (r + 1) * max)), rank r's first counts[r] rows kept."""

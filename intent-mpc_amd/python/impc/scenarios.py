@@ -185,6 +185,36 @@ def intent_config(N=20, K=8, instances=8192, hyps=8, seed=3000, params=None, ste
     return out
 
 
+def slice_instances(buckets, lo, hi):
+    """Planning instances [lo, hi) of intent_config buckets (one rank's share of config 3 split by
+    instance, strong scaling): each bucket keeps the QPs of those instances, with instance indices
+    local to the slice (``inst``) and global (``inst_global``), and the per-instance arrays sliced
+    the same way.  Buckets left empty are dropped."""
+    out = {}
+    for kk, bk in buckets.items():
+        sel = (bk["inst"] >= lo) & (bk["inst"] < hi)
+        if not sel.any():
+            continue
+        nb = dict(bk)
+        nb["values"] = {k: v[sel] for k, v in bk["values"].items()}
+        for k in ("x_ws", "hyp", "dyn_pos", "dyn_size"):
+            nb[k] = bk[k][sel]
+        nb["inst_global"] = bk["inst"][sel]
+        nb["inst"] = bk["inst"][sel] - lo
+        nb["instances"] = {k: (v if k == "size" else v[lo:hi]) for k, v in bk["instances"].items()}
+        out[kk] = nb
+    return out
+
+
+def queue_weight(pd, N):
+    """q_weight of the longest-first work queue (impc_batch_set_queue_order) for mpcPlanner QPs:
+    with q = -Q xRef (castMPCToQPGradient, mpcPlanner.cpp:952-966), ||q||_inf / (position weight
+    x (N - 1)) is the reference's mean advance per step (m); the key weighs it 1:10 against the
+    warm start's constraint violation (m), the measured ranking of the ADMM iteration count on
+    config 3's QPs (tools/queue_order_study.py)."""
+    return 1.0 / (10.0 * (N - 1) * pd["position_weight"])
+
+
 def first_call_config(N=20, batch=1, seed=1000, params=None, step_range=STEP_RANGE):
     """Config 1: the first makePlan() QP -- no obstacles, cold start (mpcPlanner.cpp:543-569)."""
     p, pd = params if params is not None else mpc_params(horizon=N)

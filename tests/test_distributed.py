@@ -167,3 +167,76 @@ def test_two_rank_config4_shard_and_gather():
         k = Kinst[i]
         assert set(rows[:, 6]) <= ({0} if k == 0 else {k, k + 1})
     assert (all0[:, 4] != 0).all()                                   # every QP solved (a status set)
+
+
+def _config3_strong_worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(WORLD))
+    try:
+        import sys
+        here = os.path.dirname(os.path.abspath(__file__))
+        sys.path[:0] = [here, os.path.dirname(here)]
+        from helpers import oracle
+        import impc
+        from impc import scenarios
+        r, lr, w = D.env()
+        dist = D.init("gloo", lr)
+        # bench.py --workload config3 --scaling strong's rank path at a small batch: one fixed
+        # scenario (same seed on every rank) split by instance, per-rank solve, padded cost gather
+        I = 5
+        full = scenarios.intent_config(instances=I, seed=3000)
+        bounds = D.equal_instance_bounds(I, w)
+        mine = scenarios.slice_instances(full, int(bounds[r]), int(bounds[r + 1]))
+        counts = [8 * int(bounds[k + 1] - bounds[k]) for k in range(w)]
+        s = impc.default_settings(verbose=0, adaptive_rho_interval=25)
+        recs = []
+        for K, bk in sorted(mine.items()):
+            _, _, info = oracle(bk, s)
+            rec = D.make_records(r, bk["inst_global"], bk["hyp"], info)
+            recs.append(np.concatenate([rec, np.full((rec.shape[0], 1), K)], axis=1))
+            # the slice's own instance indices address its sliced per-instance arrays
+            assert (bk["instances"]["xref"][bk["inst"]] == full[K]["instances"]["xref"][bk["inst_global"]]).all()
+        allrec = D.gather_costs(dist, np.concatenate(recs), counts)
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((r, np.concatenate(recs), allrec, counts))
+    except Exception:  # surface the failure in the parent
+        import traceback
+        q.put((rank, traceback.format_exc(), None, None))
+
+
+def test_two_rank_config3_strong_split_matches_whole_batch():
+    """Strong scaling of config 3: two ranks split one fixed batch by instance; the gathered
+    records are exactly those of solving the whole batch in one process (same QPs, same costs),
+    each instance's 8 hypotheses on one rank."""
+    import impc
+    from helpers import oracle
+    from impc import scenarios
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_config3_strong_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(WORLD):
+        r, rec, allrec, counts = q.get(timeout=300)
+        assert allrec is not None, rec
+        out[r] = (rec, allrec, counts)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    all0, all1 = out[0][1], out[1][1]
+    np.testing.assert_array_equal(all0, all1)
+    assert all0.shape[0] == sum(out[0][2]) == 5 * 8
+    assert out[0][2] == [16, 24]
+    s = impc.default_settings(verbose=0, adaptive_rho_interval=25)
+    whole = {}
+    for K, bk in sorted(scenarios.intent_config(instances=5, seed=3000).items()):
+        _, _, info = oracle(bk, s)
+        for i, h, o, it in zip(bk["inst"], bk["hyp"], info["obj_val"], info["iter"]):
+            whole[(int(i), int(h))] = (o, it, K)
+    for row in all0:
+        o, it, K = whole[(int(row[1]), int(row[2]))]
+        assert row[3] == o and row[5] == it and row[6] == K
+        assert row[0] == (0 if row[1] < 2 else 1)
