@@ -83,6 +83,16 @@ def relaunch(args_n, argv):
     return subprocess.call(cmd, env=env)
 
 
+def cpu_quota():
+    """CPUs the process may use per the cgroup v2 quota (cpu.max "quota period"), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_info():
     model = None
     try:
@@ -347,6 +357,9 @@ def main():
             allc = cpu_baseline(bks, settings, min(total_qps, args.cpu_sample * max(1, cores // args.cpu_threads)),
                                 cores)
             cpu["all_cores"] = {k: allc[k] for k in ("value", "unit", "cores", "sample")}
+            cpu["all_cores"]["cgroup_cpu_quota"] = cpu_quota()
+            cpu["all_cores"]["what"] = ("one oracle thread per CPU of os.sched_getaffinity(0); the box's cgroup "
+                                        "quota (cgroup_cpu_quota CPUs) bounds what they get")
 
     if args.workload == "config3":
         config = {

@@ -89,7 +89,9 @@ int impc_comm_gather_info(impc_comm c, impc_batch *bs, int count, int64_t max_qp
         HIP_OK(hipMalloc(&c->stage, bytes));
         c->stage_bytes = bytes;
     }
-    IMPC_TRY(ctx_order_launch(c->ctx, st));
+    // the solves that wrote d_info, and an earlier gather still reading the staging block, may
+    // have run on other streams: wait for all of them
+    IMPC_TRY(ctx_order_after_all(c->ctx, st));
     char *dst = (char *)c->stage;
     for (int k = 0; k < count; k++) {
         const size_t nb = sizeof(impc_info) * (size_t)bs[k]->B;

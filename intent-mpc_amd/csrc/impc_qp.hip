@@ -488,6 +488,14 @@ static int ctx_order_launch(impc_ctx ctx, hipStream_t st) {
     HIP_OK(hipStreamWaitEvent(st, ctx->ev_order, 0));
     return IMPC_OK;
 }
+// st waits for every launch noted on any caller stream (ctx_note_launch) as well as for the
+// context stream: for consumers of results that may have been produced on another stream (the
+// cost gather) and of scratch an earlier call on another stream may still be reading
+static int ctx_order_after_all(impc_ctx ctx, hipStream_t st) {
+    if (st != ctx->stream) IMPC_TRY(ctx_order_launch(ctx, st));
+    for (hipEvent_t e : ctx->ev_pending) HIP_OK(hipStreamWaitEvent(st, e, 0));
+    return IMPC_OK;
+}
 static int ctx_note_launch(impc_ctx ctx, hipStream_t st) {
     if (st == ctx->stream) return IMPC_OK;
     // recycle the events of launches that have completed (keeps the pending list short)
@@ -1064,7 +1072,7 @@ int prepare_structured(impc_batch b) {
     // per-QP HBM scratch for the scaling vectors: long-horizon shape only (the default shape keeps
     // them in LDS, mpc_wave.hpp WaveLds::ONCHIP)
     const size_t scal_bytes =
-        b->vs == kWaveVS ? 0 : sizeof(double) * (size_t)b->B * (size_t)(2 * s.n + s.mg);
+        b->vs == kWaveVS && !IMPC_OFFCHIP_SCL ? 0 : sizeof(double) * (size_t)b->B * (size_t)(2 * s.n + s.mg);
     if (scal_bytes) HIP_OK(hipMalloc((void **)&b->d_scal, scal_bytes));
     HIP_OK(hipMalloc((void **)&b->d_counter, 256));
     b->device_bytes += (int64_t)(scal_bytes + h.size() * 4 + 256);

@@ -203,7 +203,10 @@ struct WaveLds {
     // One-variable-per-lane shape: the Ruiz scaling vectors D, E and the ADMM deltas of the
     // termination checks live here (the long-horizon shape keeps them in HBM / registers: its LDS
     // is full).  Layout of each: [var slots NMAX][box rows NMAX][general slots NL GS].
-    static constexpr bool ONCHIP = VS == 1;
+#ifndef IMPC_OFFCHIP_SCL  // experiment: D, E in the per-QP HBM scratch and the deltas in registers also
+#define IMPC_OFFCHIP_SCL 0  // for the one-variable-per-lane shape (frees 2 x VEC_N doubles of LDS)
+#endif
+    static constexpr bool ONCHIP = VS == 1 && !IMPC_OFFCHIP_SCL;
     static constexpr int VEC_N = 2 * NMAX + NL * GS;
     // Pair-blocked stage recursions (default horizon of the one-variable-per-lane shape): the
     // 8-dim recursions step over two stages at a time along the even stages, with the products

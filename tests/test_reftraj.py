@@ -1,6 +1,6 @@
 """getReferenceTraj / getXRef (mpcPlanner.cpp:968-981, 1199-1231) on the device
 (impc_reference_traj_device) against the restatement oracle/reftraj_ref.py: bit-exact references
-and identical lastRefStartIdx_ over a sequence of replans, ragged and empty paths, the 29-point
+and identical lastRefStartIdx_ over a sequence of replans, ragged and empty paths, the 30-point
 search window ((int)(3.0 / ts)), padding with the last point, and the per-candidate repeat layout."""
 import numpy as np
 import pytest

@@ -34,10 +34,14 @@ if hasattr(ctx, "clock_rate"):
 rp = DeviceReplan(ctx, p, pd, I, K, L, impc.default_settings(verbose=0))
 free = rp.run(*args)
 for rep in range(3):
+    prof = "profile" in DeviceReplan.run.__code__.co_varnames  # this tree: per-QP device latency
     t = time.perf_counter()
-    lim = rp.run(*args, solver_time_limit=0.05)
+    lim = rp.run(*args, solver_time_limit=0.05, **(dict(profile=True) if prof else {}))
     host = time.perf_counter() - t
     r = dict(rep=rep, host_replan_s=round(host, 4), time_limit=lim["time_limit"])
+    if prof:
+        lat = np.concatenate([lim["lat_single"], lim["lat_pair"]])
+        r["device_qp_latency_ms"] = dict(p50=round(float(np.median(lat)), 3), max=round(float(lat.max()), 3))
     for nm in ("single", "pair"):
         st, it = lim["info_" + nm]["status_val"], lim["info_" + nm]["iter"]
         fit = free["info_" + nm]["iter"]
