@@ -479,7 +479,25 @@ def cpu_baseline(bks, settings, sample, threads):
                         x_ws=None if bk.get("x_ws") is None else bk["x_ws"][:k], threads=threads)
         t_all += time.perf_counter() - t
         n_all += k
-    return {"value": n_all / t_all, "unit": "QP-solves/s", "cores": threads, "kind": "port",
+    # per-QP latency on one thread, the reference's own measures: solveProblem only
+    # (mpcPlanner.cpp:512-520) and setup + warm start + solve
+    lat_s, lat_all = [], []
+    bk = max(bks, key=lambda x: x["values"]["q"].shape[0])
+    v = bk["values"]
+    for i in range(min(128, v["q"].shape[0])):
+        t = time.perf_counter()
+        w = ora.Workspace(bk["pattern"], v["Px"][i], v["q"][i], v["Ax"][i], v["l"][i], v["u"][i], s)
+        if bk.get("x_ws") is not None:
+            w.warm_start(bk["x_ws"][i], np.zeros(int(bk["pattern"]["m"])))
+        t1 = time.perf_counter()
+        w.solve()
+        t2 = time.perf_counter()
+        w.close()
+        lat_s.append(t2 - t1)
+        lat_all.append(t2 - t)
+    single = {"solve_p50_ms": 1e3 * float(np.median(lat_s)), "setup_solve_p50_ms": 1e3 * float(np.median(lat_all)),
+              "sample": f"first {len(lat_s)} QPs of the K={bk['K']} bucket, one thread"}
+    return {"value": n_all / t_all, "unit": "QP-solves/s", "cores": threads, "kind": "port", "single_qp": single,
             "host_cpus": os.cpu_count(), "cpu_model": cpu_info(),
             "sample": f"{n_all} QPs of the same workload (first of each bucket), one setup+warm-start+solve "
                       f"per QP, {threads} threads ({t_all:.1f} s wall)"}
