@@ -858,10 +858,18 @@ int launch_wave_w(impc_batch b, hipStream_t st, const impc::WaveIO &io, const ui
     HIP_OK(hipGetLastError());
     return IMPC_OK;
 }
+// the default-horizon instance (compile-time W) takes the batch: its W is the shape's WSPEC and,
+// for the one-variable-per-lane shape with the twisted elimination, the pattern qualifies for it
+// (MpcStructure::twist_ok)
+bool spec_ok(impc_batch b) {
+    const int ws = b->vs == kWaveVS ? impc::WaveLds<kTeam, kWaveVS, 2>::WSPEC : impc::WaveLds<kTeam, kWaveVSLong, 2>::WSPEC;
+    const bool tw = b->vs == kWaveVS && impc::WaveLds<kTeam, kWaveVS, 2>::TW;
+    return b->ms->W == ws && (!tw || b->ms->twist_ok);
+}
 template <int VS, int GS>
 int launch_wave(impc_batch b, hipStream_t st, const impc::WaveIO &io, const uint32_t *ord) {
     constexpr int WS = impc::WaveLds<kTeam, VS, GS>::WSPEC;
-    return b->ms->W == WS ? launch_wave_w<VS, GS, WS>(b, st, io, ord) : launch_wave_w<VS, GS, 0>(b, st, io, ord);
+    return spec_ok(b) ? launch_wave_w<VS, GS, WS>(b, st, io, ord) : launch_wave_w<VS, GS, 0>(b, st, io, ord);
 }
 
 // ---- work-queue order (impc_batch_set_queue_order, csrc/queue.hpp)
@@ -1471,8 +1479,7 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
         Launch &L = launches.back();
         L.count++;
         L.lds = std::max(L.lds, wave_lds_bytes(b->vs, b->gs, b->wt));
-        L.spec = L.spec && b->ms->W == (b->vs == kWaveVS ? impc::WaveLds<kTeam, kWaveVS, 2>::WSPEC
-                                                         : impc::WaveLds<kTeam, kWaveVSLong, 2>::WSPEC);
+        L.spec = L.spec && spec_ok(b);
         GroupEntry &e = entries[(size_t)p];
         e.T = b->wt;
         e.io = wave_io(b);

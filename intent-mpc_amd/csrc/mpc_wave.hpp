@@ -57,8 +57,8 @@ namespace impc {
 #endif
 #define IMPC_REP(X) for (int rep_ = 0; rep_ < (IMPC_DUP == (X) ? 2 : 1); rep_++)
 
-#ifndef IMPC_HWRW  // recursion wave from the waves' SIMD placement: +0.5 %, off (profiles/r02/exp/README.md)
-#define IMPC_HWRW 0
+#ifndef IMPC_HWRW  // recursion wave from the waves' SIMD placement: +0.5-1 % (profiles/r02/exp/README.md,
+#define IMPC_HWRW 1  // profiles/r03/exp/README.md); re-validated on the GPU suite in round 3, on
 #endif
 #ifndef IMPC_NOCHUNK
 #define IMPC_NOCHUNK 1
@@ -82,6 +82,12 @@ namespace impc {
 #endif
 #ifndef IMPC_PSTRIDE_PAD
 #define IMPC_PSTRIDE_PAD 1
+#endif
+#ifndef IMPC_TWIST  // twisted (two-ended) block elimination on the default horizon (WaveQP::TWIST):
+#define IMPC_TWIST 0  // built, parity green, measured slower (profiles/r03/exp/README.md), off
+#endif
+#ifndef IMPC_TWOPQ  // twisted chains: one address register per prefetch (no ds_read2 merging)
+#define IMPC_TWOPQ 0
 #endif
 #ifndef IMPC_PAIR  // pair-blocked stage recursions on the default horizon (WaveLds::PAIR): built,
 #define IMPC_PAIR 0  // measured slower (profiles/r02/exp/README.md), off
@@ -219,7 +225,14 @@ struct WaveLds {
     static constexpr int M_OFF = H_OFF + (PAIR ? 64 * NH : 0);  // [NH][40] M_k, row-major 8 x 5
     static constexpr int SCL_OFF = M_OFF + (PAIR ? 40 * NH : 0);  // D, E (scaling)
     static constexpr int DLT_OFF = SCL_OFF + (ONCHIP ? VEC_N : 0);  // dx, dy (check iterations)
-    static constexpr int P_OFF = DLT_OFF + (ONCHIP ? VEC_N : 0);    // products, column-slot layout (size below)
+    // Twisted (two-ended) elimination of the default horizon (IMPC_TWIST, WaveQP::TWIST): the middle
+    // stage's state lanes' G_{KM-1}[:, 8:] rows ([8][5]; their cp registers hold Abar^-1 Bbar' rows)
+    static constexpr bool TW = VS == 1 && NL == 256 && IMPC_TWIST && !CHUNK && !PAIR;
+    static constexpr int MID_OFF = DLT_OFF + (ONCHIP ? VEC_N : 0);
+    // ... and the coupling-row table (int32 per general-row slot: (upper entry << 16) | upper
+    // column for rows coupling stages k, k + 1 > KM, else -1), set per batch by load_tables
+    static constexpr int CPL_OFF = MID_OFF + (TW ? 40 : 0);
+    static constexpr int P_OFF = CPL_OFF + (TW ? NL * GS / 2 : 0);  // products, column-slot layout (size below)
     // chunk-boundary exchange of the recursions (inside the team reduction scratch, past red[0..3])
     static constexpr int XF_OFF = RED_OFF + 8;              // forward: a^_{S(c+1)-1}, c = 0..2
     static constexpr int XB_OFF = RED_OFF + 32;             // backward: x^_{S(c)}, c = 1..3
@@ -250,8 +263,10 @@ struct WaveLds {
     // factorisation aliases (inside R..X region and the products buffer)
     static constexpr int FA = R_OFF, FL = FA + 169, FI = FL + 169, FB = FI + 169, FG = FB + 104, FE = FG + 104,
                          DIAGX = FE + 64;
+    // twisted elimination: Acheck_{k+1}^{-1}[:8, :8] of the stage eliminated last from the bottom
+    static constexpr int FEB = DIAGX + NMAX;
     // general rows' rho during the factorisation: products region + 4 mg
-    static_assert(DIAGX + NMAX <= RED_OFF, "factorisation scratch does not fit");
+    static_assert(FEB + 64 <= RED_OFF, "factorisation scratch does not fit");
 };
 
 struct WaveRho {
@@ -320,6 +335,17 @@ struct WaveQP {
     WaveRho R;
     double c = 1.0, cinv = 1.0;
     int rw = 0;  // the wavefront that runs the stage recursions for this QP
+    // Twisted (two-ended) block elimination, default horizon of the one-variable-per-lane shape:
+    // stages 0 .. KM-1 are eliminated top-down (the Schur complements Ahat_k, F_k as in the
+    // one-ended scheme), stages W .. KM+1 bottom-up (Acheck_k = M_kk - Bbar_k' Acheck_{k+1}^-1[:8,:8]
+    // Bbar_k, H_k = (Acheck_k^-1 Bbar_k')[:8, :]), and the middle stage KM takes both
+    // (Abar = M - E_{KM-1} - Bbar_KM' Acheck_{KM+1}^-1[:8,:8] Bbar_KM).  Each solve then runs its
+    // 8-dim recursions as two concurrent chains of (W - 1) / 2 steps on two wavefronts -- top-down
+    // and bottom-up, then outward from the middle -- instead of one chain of W steps.
+    static constexpr bool TWIST = LD::TW && WF == LD::WSPEC;
+    static constexpr int KM = (LD::WSPEC - 1) / 2;
+    // (the coupling-row table lives in LDS, WaveLds::CPL_OFF: kept in registers it was spilled and
+    // reloaded from scratch every iteration)
     // settings / pattern scalars the ADMM iteration reads, held in registers (a grouped launch's
     // tables and settings live in global memory: read in the loop, each is a scalar-memory round
     // trip after every barrier)
@@ -460,6 +486,22 @@ struct WaveQP {
         double *pb = lds + LD::P_OFF;
         for (int e = w.lane(); e < pz + 8; e += NL) pb[e] = 0.0;
         w.sync();
+        if constexpr (TWIST) {
+            // coupling rows: entries in stages k and k + 1 > KM, one of them in stage k + 1
+            // (MpcStructure::twist_ok, checked on the host) -- the upper entry, last in column order
+            int32_t *cpl = (int32_t *)(lds + LD::CPL_OFF);
+            for (int g = w.lane(); g < NL * GS; g += NL) {
+                int hi = -1, lo = 1 << 30, eu = 0, cu = 0;
+                for (int e = 0; e < 4 && g < T.mg; e++) {
+                    const int c = T.gen_col[4 * g + e];
+                    if (c < 0) continue;
+                    const int st_ = c / 13;
+                    if (st_ > hi) hi = st_, eu = e, cu = c;
+                    lo = st_ < lo ? st_ : lo;
+                }
+                cpl[g] = g < T.mg && hi == lo + 1 && hi > KM ? (eu << 16) | cu : -1;
+            }
+        }
         for (int e = w.lane(); e < T.n * T.CG; e += NL) {
             const int v = e / T.CG, t = e % T.CG, id = T.colg[e];
             if (id >= 0)
@@ -626,6 +668,7 @@ struct WaveQP {
     // ------------------------------------------------------------ block factorisation
     // Returns 1 if a pivot is not positive (OSQP_NONCVX_ERROR).
     IMPC_WF int factorize() {
+        if constexpr (TWIST) return factorize_tw();
         const int n = T.n, W = Wst(), N = W + 1;
         double *w = pbuf(), *rhog = pbuf() + 4 * T.mg, *diagx = lds + LD::DIAGX;
         const bool pair = LD::PAIR && W == LD::WSPEC;
@@ -1414,10 +1457,14 @@ struct WaveQP {
 
     // --------------------------------------------------------------- one ADMM iteration
     IMPC_WF void iterate(bool need_delta) {
+        if constexpr (TWIST) {
+            iterate_tw(need_delta);
+            return;
+        }
         const int W = Wst();
         const bool pair = LD::PAIR && W == LD::WSPEC;
         double *rb = rbuf(), *tb = tbuf(), *eb = ebuf(), *xb = xbuf();
-        const double sigma = sig_, alpha = alp_, oma = (double)1.0 - alp_;
+        const double sigma = sig_;
         IMPC_REP(kSecRhs) {
             // rhs = sigma x - q + A' v   (stage order)
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
@@ -1564,7 +1611,14 @@ struct WaveQP {
             wv.lsync();
         }
         IMPC_SEC(kSecS5);
-        // update_x and the box rows (update_z / project / update_y)
+        update_and_products(need_delta);
+    }
+
+    // update_x and the box rows (update_z / project / update_y), the general rows, and the
+    // products of the next rhs (the end of every ADMM iteration)
+    IMPC_WF void update_and_products(bool need_delta) {
+        double *xb = xbuf();
+        const double alpha = alp_, oma = (double)1.0 - alp_;
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (!vok[s]) continue;
             double xt = xb[NL * s + L];
@@ -1601,6 +1655,403 @@ struct WaveQP {
         IMPC_SEC(kSecUpdate);
         IMPC_REP(kSecProducts) write_v_products();
         IMPC_SEC(kSecProducts);
+    }
+
+    // ------------------------------------------------------ twisted elimination (TWIST)
+    // One 8-dim chain of S steps on the recursion grid (lane l = 8i + j of the calling wavefront):
+    //   v <- c - B v  (TR: c - B' v),  B = the stored block of stage k(m) = K0 + D m.
+    // F slot k holds its block with the column index on i for even k (factorize), so a plain
+    // product of an even stage reduces over i (input at i, output at j) and a transposed one over j,
+    // odd stages the other way round: consecutive steps alternate without moving data.  c of step m
+    // is read at cb + 13 (k + CO) + (output index); the result goes to ob + 13 (k + OO) + (output
+    // index), captured in registers during the sweep (each lane keeps at most one even and one odd
+    // step) and stored after it.  v: the input of step 0, at its index.
+    static IMPC_WF constexpr bool strd(int k, bool tr) { return ((k & 1) == 0) != tr; }
+    template <int S, int K0, int D, bool TR, int CO, int OO>
+    IMPC_WF void chain(const double *cb, double *ob, double v) {
+        static_assert(S >= 1 && S <= 16, "captures hold one even and one odd step per lane");
+        const double *Fm = lds + LD::F_OFF;
+        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;
+        double fq[2], cq[2], cap0 = 0.0, cap1 = 0.0;
+        // each prefetch from its own (opaque) address register: merged into one ds_read2 with the
+        // next prefetch of the same parity, a load would issue two steps late and its wait would
+        // sit on the chain (IMPC_TWOPQ)
+        auto ldF = [&](int k) {
+            int o = 64 * k + l;
+            if (IMPC_TWOPQ) opaque(o);
+            return Fm[o];
+        };
+        auto ldC = [&](int k) {
+            int o = 13 * (k + CO) + (strd(k, TR) ? j : i);
+            if (IMPC_TWOPQ) opaque(o);
+            return cb[o];
+        };
+        _Pragma("unroll") for (int m = 0; m < 2 && m < S; m++) {
+            const int k = K0 + D * m;
+            fq[m] = ldF(k);
+            cq[m] = ldC(k);
+        }
+        _Pragma("unroll") for (int m = 0; m < S; m++) {
+            const int k = K0 + D * m;
+            const double f0 = fq[m & 1], c0 = cq[m & 1];
+            if (m + 2 < S) {  // the next step of this parity, two steps ahead
+                fq[m & 1] = ldF(k + 2 * D);
+                cq[m & 1] = ldC(k + 2 * D);
+            }
+            if (strd(k, TR)) {
+                v = rstep<true>(f0, c0, v);
+                if (((m >> 1) & 7) == i) (m & 1 ? cap1 : cap0) = v;
+            } else {
+                v = rstep<false>(f0, c0, v);
+                if (((m >> 1) & 7) == j) (m & 1 ? cap1 : cap0) = v;
+            }
+        }
+        // even steps: output index (strd(K0) ? j : i), kept by the lane whose other index is m / 2
+        const bool se = strd(K0, TR), so = strd(K0 + D, TR);
+        const int me = 2 * (se ? i : j), mo = 2 * (so ? i : j) + 1;
+        if (me < S) ob[13 * (K0 + D * me + OO) + (se ? j : i)] = cap0;
+        if (mo < S) ob[13 * (K0 + D * mo + OO) + (so ? j : i)] = cap1;
+    }
+
+    // One ADMM iteration with the twisted solve.  Exchange vectors per stage k (13 slots each):
+    //   rb: r (rhs); a_k in [:8] for top stages 1..KM; u_{k-1} = Bbar_{k-1} x_{k-1} in [:8] for
+    //       bottom stages (written after r is consumed)
+    //   tb: t_k (top, k <= KM) / s_k = Acheck_k^-1[:8,:] r_k (bottom) in [:8]; then c_{k-1} =
+    //       Bbar_{k-1} zhat_{k-1} (bottom, k - 1 > KM) in [:8]
+    //   eb: e_k = Ahat_k^-1 (a_k, r_k[8:]) (top) / zhat_k = Acheck_k^-1 (r_k - Bbar_k' w_{k+1}) (bottom)
+    //   xb: w_k = (zhat_k)[:8] (bottom, chain A), then the solution x
+    IMPC_WF void iterate_tw(bool need_delta) {
+        constexpr int W = WF;
+        double *rb = rbuf(), *tb = tbuf(), *eb = ebuf(), *xb = xbuf();
+        const double sigma = sig_;
+        const int wave = L >> 6, rw2 = (rw + 2) & 3;
+        // rhs = sigma x - q + A' v   (stage order)
+        IMPC_REP(kSecRhs) {
+            _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                if (!vok[s]) continue;
+                const int v = NL * s + L;
+                const double vb = rhob(s) * zb[s] - yb[s];
+                double r = sigma * x[s] - q[s];
+                r += ab[s] * vb;
+                r += col_gather(v, hid_[s]);
+                rb[v] = r;
+            }
+            wv.lsync();
+        }
+        IMPC_SEC(kSecRhs);
+        IMPC_REP(kSecS1) {
+            // P1: t_k = r_k[:8] - G_{k-1}[:, 8:] r_{k-1}[8:] (top and middle), s_k = Acheck_k^-1[:8,:] r_k (bottom)
+            _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                if (!vok[s] || vr_[s] >= 8) continue;
+                const int v = NL * s + L, k = vs_[s];
+                double t;
+                if (k <= KM) {
+                    t = rb[v];
+                    if (k > 0) {
+                        const double *rp = rb + 13 * (k - 1) + 8, *mc = lds + LD::MID_OFF + 5 * vr_[s];
+                        double rv[5];
+                        _Pragma("unroll") for (int cc = 0; cc < 5; cc++) rv[cc] = rp[cc];
+                        // the middle stage's lanes hold Abar^-1 Bbar' rows in cp: their G_{KM-1}[:, 8:]
+                        // rows live in LDS
+                        _Pragma("unroll") for (int cc = 0; cc < 5; cc++) t -= (k == KM ? mc[cc] : cp[s][cc]) * rv[cc];
+                    }
+                } else {
+                    const double *rk = rb + 13 * k;
+                    double rv[13];
+                    _Pragma("unroll") for (int cc = 0; cc < 13; cc++) rv[cc] = rk[cc];
+                    t = 0.0;
+                    _Pragma("unroll") for (int cc = 0; cc < 13; cc++) t += ainv[s][cc] * rv[cc];
+                }
+                tb[v] = t;
+            }
+            wv.lsync();
+        }
+        IMPC_SEC(kSecS1);
+        IMPC_REP(kSecFwd) {
+            // chains A: a_{k+1} = t_{k+1} - F_k a_k (k = 0..KM-1) and w_k = s_k - H_k w_{k+1}
+            // (k = W-1..KM+1, w_W = s_W), on two wavefronts at once
+            if (L < 8) rb[L] = tb[L];                      // a_0 = t_0
+            if (L >= 64 && L < 72) xb[13 * W + L - 64] = tb[13 * W + L - 64];  // w_W = s_W
+            if (wave == rw) {
+                const int l = lane_o() & 63;
+                chain<KM, 0, 1, false, 1, 1>(tb, rb, tb[strd(0, false) ? (l >> 3) : (l & 7)]);
+            } else if (wave == rw2) {
+                const int l = lane_o() & 63;
+                chain<W - 1 - KM, W - 1, -1, false, 0, 0>(tb, xb,
+                                                           tb[13 * W + (strd(W - 1, false) ? (l >> 3) : (l & 7))]);
+            }
+            wv.lsync();
+        }
+        IMPC_SEC(kSecFwd);
+        IMPC_REP(kSecS3) {
+            // P3: e_k (top), x_KM = Abar^-1 ((a_KM, r_KM[8:]) - Bbar_KM' w_{KM+1}) (middle),
+            // zhat_k = Acheck_k^-1 r_k - (Acheck_k^-1 Bbar_k') w_{k+1} (bottom)
+            _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                if (!vok[s]) continue;
+                const int v = NL * s + L, k = vs_[s];
+                // the coupling term first, kept apart from the 13-term product by a scheduling
+                // barrier, so the two operand sets are not live at once
+                double g = 0.0;
+                if (k >= KM && k < W) {
+                    const double *w1 = xb + 13 * (k + 1);
+                    double wv_[8];
+                    _Pragma("unroll") for (int p = 0; p < 8; p++) wv_[p] = w1[p];
+                    _Pragma("unroll") for (int p = 0; p < 8; p++) g += cp[s][p] * wv_[p];
+                }
+#if defined(__HIP_DEVICE_COMPILE__)
+                __builtin_amdgcn_sched_barrier(0);
+#endif
+                const double *rk = rb + 13 * k;
+                double rv[13];
+                _Pragma("unroll") for (int cc = 0; cc < 13; cc++) rv[cc] = rk[cc];
+                IMPC_LOADS_FIRST(7, 20);
+                double e = 0.0;
+                _Pragma("unroll") for (int cc = 0; cc < 13; cc++) e += ainv[s][cc] * rv[cc];
+                e -= g;
+                (k == KM ? xb : eb)[v] = e;
+            }
+            wv.lsync();
+        }
+        IMPC_SEC(kSecS3);
+        IMPC_REP(kSecFAsm) {
+            // P3b: u_KM = Bbar_KM x_KM and c_k = Bbar_k zhat_k (k > KM), one coupling row per state:
+            // Bbar_k row i = rho a_up a_(k, .) of the row whose stage-(k+1) entry is state i
+            _Pragma("unroll") for (int s = 0; s < GS; s++) {
+                const int cp_ = ((const int32_t *)(lds + LD::CPL_OFF))[NL * s + L];
+                if (cp_ < 0) continue;
+                const int cu = cp_ & 0xFFFF, eu = cp_ >> 16;
+                const bool m0 = cu / 13 == KM + 1;
+                const double *src = m0 ? xb : eb;
+                double acc = 0.0, au = 0.0;
+                _Pragma("unroll") for (int e = 0; e < 4; e++) {
+                    const bool up = e == eu;
+                    au = up ? a[s][e] : au;
+                    acc += up ? 0.0 : a[s][e] * src[gcol(s, e)];
+                }
+                (m0 ? rb : tb)[cu] = (rhog_(s) * au) * acc;
+            }
+            wv.lsync();
+        }
+        IMPC_REP(kSecBwd) {
+            // chains B: x_k[:8] = e_k[:8] - F_k' x_{k+1}[:8] (k = KM-1..0) and
+            // u_k = c_k - H_k' u_{k-1} (k = KM+1..W-1)
+            if (wave == rw) {
+                const int l = lane_o() & 63;
+                chain<KM, KM - 1, -1, true, 0, 0>(eb, xb, xb[13 * KM + (strd(KM - 1, true) ? (l >> 3) : (l & 7))]);
+            } else if (wave == rw2) {
+                const int l = lane_o() & 63;
+                chain<W - 1 - KM, KM + 1, 1, true, 1, 1>(tb, rb,
+                                                          rb[13 * (KM + 1) + (strd(KM + 1, true) ? (l >> 3) : (l & 7))]);
+            }
+            wv.lsync();
+        }
+        IMPC_SEC(kSecBwd);
+        IMPC_REP(kSecS5) {
+            // P5: controls of the top stages (S5), all of a bottom stage: x_k = zhat_k - Acheck_k^-1[:, :8] u_{k-1}
+            _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                if (!vok[s]) continue;
+                const int v = NL * s + L, k = vs_[s];
+                if (k < KM && vr_[s] >= 8) {
+                    const double *xn = xb + 13 * (k + 1);
+                    double t = eb[v], xv[8];
+                    _Pragma("unroll") for (int jj = 0; jj < 8; jj++) xv[jj] = xn[jj];
+                    _Pragma("unroll") for (int jj = 0; jj < 8; jj++) t -= cp[s][jj] * xv[jj];
+                    xb[v] = t;
+                } else if (k > KM) {
+                    const double *uu = rb + 13 * k;
+                    double t = eb[v], uv[8];
+                    _Pragma("unroll") for (int jj = 0; jj < 8; jj++) uv[jj] = uu[jj];
+                    _Pragma("unroll") for (int jj = 0; jj < 8; jj++) t -= ainv[s][jj] * uv[jj];
+                    xb[v] = t;
+                }
+            }
+            wv.lsync();
+        }
+        IMPC_SEC(kSecS5);
+        update_and_products(need_delta);
+    }
+
+    // The twisted factorisation (TWIST): top stages 0..KM-1 as the one-ended scheme, bottom stages
+    // W..KM+1 from the bottom up, then the middle stage with both Schur complements.
+    IMPC_WF int factorize_tw() {
+        constexpr int W = WF, N = W + 1;
+        double *w = pbuf(), *rhog = pbuf() + 4 * T.mg, *diagx = lds + LD::DIAGX;
+        double *A = lds + LD::FA, *Li = lds + LD::FL, *Ai = lds + LD::FI, *Bb = lds + LD::FB, *G = lds + LD::FG,
+               *E = lds + LD::FE, *EB = lds + LD::FEB, *Fm = F();
+        _Pragma("unroll") for (int s = 0; s < GS; s++) {
+            const int g = NL * s + L;
+            if (gok[s]) {
+                _Pragma("unroll") for (int e = 0; e < 4; e++) w[4 * g + e] = a[s][e];
+                rhog[g] = rhog_(s);
+            }
+        }
+        _Pragma("unroll") for (int s = 0; s < VS; s++) {
+            if (vok[s]) {
+                const double rb = rhob(s);
+                diagx[NL * s + L] = (pd[s] + st.sigma) + rb * ab[s] * ab[s];
+            }
+        }
+        wv.sync();
+        int bad = 0;
+        for (int it = 0; it < N; it++) {
+            const int k = it < KM ? it : it < N - 1 ? W - (it - KM) : KM;
+            const int sz = k < W ? 13 : 8;
+            const bool top = k < KM, mid = k == KM;
+            // assemble M_kk (the top Schur complement E_{k-1} folded in for k <= KM) and Bbar_k
+            for (int d = L; d < kStageDests; d += NL) {
+                const bool isB = d >= 169;
+                if (isB && k == W) continue;
+                const int dd = isB ? d - 169 : d;
+                const int r = dd / 13, cc = dd % 13;
+                double val = 0.0;
+                if (isB || (r < sz && cc < sz)) {
+                    const int32_t t0 = T.term_ptr[(int64_t)k * kStageDests + d];
+                    const int32_t t1 = T.term_ptr[(int64_t)k * kStageDests + d + 1];
+                    for (int32_t t = t0; t < t1; t++) {
+                        const int32_t code = T.term[t];
+                        const int32_t g = code >> 4, e = (code >> 2) & 3, f = code & 3;
+                        val += rhog[g] * w[4 * g + e] * w[4 * g + f];
+                    }
+                    if (!isB && r == cc) val += diagx[13 * k + r];
+                    if (!isB && k > 0 && k <= KM && r < 8 && cc < 8) val -= E[8 * r + cc];
+                }
+                if (isB)
+                    Bb[dd] = val;
+                else
+                    A[dd] = val;
+            }
+            wv.sync();
+            IMPC_SEC(kSecFAsm);
+            if (!top && k < W) {
+                // bottom Schur complement: A -= Bbar_k' (Acheck_{k+1}^-1[:8,:8]) Bbar_k (T = EB Bbar_k in Li)
+                for (int p = L; p < 104; p += NL) {
+                    const int ii = p / 13, cc = p % 13;
+                    double sacc = 0.0;
+                    for (int qq = 0; qq < 8; qq++) sacc += EB[8 * ii + qq] * Bb[13 * qq + cc];
+                    Li[p] = sacc;
+                }
+                wv.sync();
+                for (int d = L; d < 169; d += NL) {
+                    const int r = d / 13, cc = d % 13;
+                    double sacc = 0.0;
+                    for (int p = 0; p < 8; p++) sacc += Bb[13 * p + r] * Li[13 * p + cc];
+                    A[d] -= sacc;
+                }
+                wv.sync();
+            }
+            // A^-1 by Gauss-Jordan with 2x2 pivot blocks (as factorize)
+            {
+                double *src = A, *dst = Li;
+                const int gi = L / 13, gc = L % 13;
+                const bool act = L < 169 && gi < sz && gc < sz;
+                for (int j = 0; j < sz; j += 2) {
+                    const bool two = j + 1 < sz, last = j + (two ? 2 : 1) >= sz;
+                    if (act) {
+                        const int i = last && gc > gi ? gc : gi, c = last && gc > gi ? gi : gc;
+                        double v;
+                        if (two) {
+                            const double p00 = src[13 * j + j], p01 = src[13 * j + j + 1];
+                            const double p10 = src[13 * (j + 1) + j], p11 = src[13 * (j + 1) + j + 1];
+                            const double det = p00 * p11 - p01 * p10;
+                            if (!(p00 > 0.0) || !(det > 0.0)) bad = 1;
+                            const double rd = 1.0 / det;
+                            const double q00 = p11 * rd, q01 = -(p01 * rd), q10 = -(p10 * rd), q11 = p00 * rd;
+                            const int ri = i - j, ci = c - j;
+                            const bool iJ = ri == 0 || ri == 1, cJ = ci == 0 || ci == 1;
+                            if (iJ && cJ) {
+                                v = ri == 0 ? (ci == 0 ? q00 : q01) : (ci == 0 ? q10 : q11);
+                            } else if (iJ) {
+                                const double s0 = src[13 * j + c], s1 = src[13 * (j + 1) + c];
+                                v = ri == 0 ? q00 * s0 + q01 * s1 : q10 * s0 + q11 * s1;
+                            } else {
+                                const double a0 = src[13 * i + j], a1 = src[13 * i + j + 1];
+                                const double u0 = a0 * q00 + a1 * q10, u1 = a0 * q01 + a1 * q11;
+                                if (cJ)
+                                    v = -(ci == 0 ? u0 : u1);
+                                else
+                                    v = src[13 * i + c] - (u0 * src[13 * j + c] + u1 * src[13 * (j + 1) + c]);
+                            }
+                        } else {
+                            const double p = src[13 * j + j];
+                            if (!(p > 0.0)) bad = 1;
+                            const double r = 1.0 / p;
+                            if (i == j && c == j)
+                                v = r;
+                            else if (i == j)
+                                v = src[13 * j + c] * r;
+                            else if (c == j)
+                                v = -(src[13 * i + j] * r);
+                            else
+                                v = src[13 * i + c] - (src[13 * i + j] * r) * src[13 * j + c];
+                        }
+                        (last ? Ai : dst)[13 * gi + gc] = v;
+                    }
+                    wv.sync();
+                    double *t = src;
+                    src = dst;
+                    dst = t;
+                }
+            }
+            _Pragma("unroll") for (int s = 0; s < VS; s++)
+                if (vok[s] && vs_[s] == k)
+                    _Pragma("unroll") for (int cc = 0; cc < 13; cc++) ainv[s][cc] = cc < sz ? Ai[13 * vr_[s] + cc] : 0.0;
+            if (top) {
+                // G_k = Bbar_k Ahat_k^-1, E_k = G_k Bbar_k', F_k (recursion layout), cp rows (S5 / S1)
+                for (int p = L; p < 104; p += NL) {
+                    const int ii = p / 13, cc = p % 13;
+                    double sacc = 0.0;
+                    for (int t = 0; t < 13; t++) sacc += Bb[13 * ii + t] * Ai[13 * t + cc];
+                    G[p] = sacc;
+                }
+                wv.sync();
+                if (L < 64) {
+                    const int ii = L >> 3, jj = L & 7;
+                    double sacc = 0.0;
+                    for (int t = 0; t < 13; t++) sacc += G[13 * ii + t] * Bb[13 * jj + t];
+                    E[8 * ii + jj] = sacc;
+                    Fm[64 * k + 8 * ii + jj] = !(k & 1) ? G[13 * jj + ii] : G[13 * ii + jj];
+                }
+                _Pragma("unroll") for (int s = 0; s < VS; s++) {
+                    if (!vok[s]) continue;
+                    if (vs_[s] == k && vr_[s] >= 8)
+                        _Pragma("unroll") for (int jj = 0; jj < 8; jj++) cp[s][jj] = G[13 * jj + vr_[s]];
+                    if (vs_[s] == k + 1 && vr_[s] < 8 && k + 1 < KM)
+                        _Pragma("unroll") for (int jj = 0; jj < 8; jj++) cp[s][jj] = jj < 5 ? G[13 * vr_[s] + 8 + jj] : 0.0;
+                }
+                if (k + 1 == KM && L < 40) lds[LD::MID_OFF + L] = G[13 * (L / 5) + 8 + L % 5];  // [8][5]
+                wv.sync();
+            } else if (k < W) {
+                // G'_k = A^-1 Bbar_k' (13 x 8, row-major at G[8 r + p]); bottom: H_k = G'_k[:8, :] in F
+                // slot k (recursion layout) and the stage's cp rows; middle: G'_KM to LDS
+                for (int p = L; p < 104; p += NL) {
+                    const int r = p >> 3, qq = p & 7;
+                    double sacc = 0.0;
+                    for (int cc = 0; cc < 13; cc++) sacc += Ai[13 * r + cc] * Bb[13 * qq + cc];
+                    G[p] = sacc;
+                }
+                wv.sync();
+                if (!mid && L < 64) {
+                    const int ii = L >> 3, jj = L & 7;
+                    Fm[64 * k + 8 * ii + jj] = !(k & 1) ? G[8 * jj + ii] : G[8 * ii + jj];
+                }
+                _Pragma("unroll") for (int s = 0; s < VS; s++)
+                    if (vok[s] && vs_[s] == k)
+                        _Pragma("unroll") for (int jj = 0; jj < 8; jj++) cp[s][jj] = G[8 * vr_[s] + jj];
+            }
+            if (!top && !mid) {
+                // Acheck_k^-1[:8, :8] for the next stage up
+                if (L < 64) EB[L] = Ai[13 * (L >> 3) + (L & 7)];
+            }
+            wv.sync();
+            IMPC_SEC(kSecFDense);
+        }
+        _Pragma("unroll") for (int s = 0; s < VS; s++)
+            if (vok[s] && vs_[s] == 0 && vr_[s] < 8)
+                _Pragma("unroll") for (int jj = 0; jj < 8; jj++) cp[s][jj] = 0.0;
+        bad = (int)wv.max((double)bad);
+        clear_exchange();
+        zero_products();
+        return bad;
     }
 
     // ------------------------------------------------------------ update_info + checks
@@ -1972,7 +2423,20 @@ struct WaveQP {
         const double tl = wv.uniform(io.tlim ? io.tlim[b] : st.time_limit), tick = st.tick_s;
         const bool tlim = tl > 0;
         int32_t chk_left = chk, rho_left = rho_int;
-        for (iter = 1; iter <= max_iter; iter++) {
+        // The refactorisation after an adaptive-rho update runs between two passes of the inner
+        // iteration loop rather than inside it: the register allocator then places the spills the
+        // factorisation's temporaries force around that (rare) call, outside the hot loop.  The
+        // order of operations is the one of a single loop.
+        bool refac = false;
+        iter = 1;
+        for (;;) {
+        if (refac) {
+            refac = false;
+            factorize();
+            write_v_products();
+            IMPC_SEC(kSecFactor);
+        }
+        for (; iter <= max_iter; iter++) {
             const bool chk_now = chk && --chk_left == 0;
             if (chk_now) chk_left = chk;
             const bool rho_now = rho_int && --rho_left == 0;
@@ -2013,12 +2477,14 @@ struct WaveQP {
                 if ((rn > R.rho * st.adaptive_rho_tolerance) || (rn < R.rho / st.adaptive_rho_tolerance)) {
                     IMPC_SEC(kSecChecks);
                     set_rho(dmin(dmax(rn, kRhoMin), kRhoMax));
-                    factorize();
-                    write_v_products();
-                    IMPC_SEC(kSecFactor);
                     rho_updates += 1;
+                    refac = true;
+                    iter++;  // this iteration is complete; the next pass starts at the next one
+                    break;
                 }
             }
+        }
+        if (!refac) break;
         }
         IMPC_SEC_START();
         double D[VS], Eb[VS], Eg[GS];

@@ -10,6 +10,7 @@ from oracle import osqp_oracle as ora
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HARNESS_PATH = os.path.join(ROOT, "tests", "native", "build", "libimpc_core_cpu.so")
 EMU_PATH = os.path.join(ROOT, "tests", "native", "build", "libwave_emu.so")
+EMU_TW_PATH = os.path.join(ROOT, "tests", "native", "build", "libwave_emu_tw.so")
 
 # BASELINE.json north_star: primal within 1e-5 relative of the reference solver.
 PRIMAL_RTOL = 1e-5
@@ -72,15 +73,17 @@ def harness(cfg, settings):
     return xo, yo, info
 
 
-_E = None
+_E = {}
 
 
-def emulate(cfg, settings):
-    """Test-only CPU emulation of the structured wave kernel (mpc_wave.hpp, 128 lanes as threads)."""
-    global _E
-    if _E is None:
-        _E = C.CDLL(EMU_PATH)
-        _E.emu_wave_solve_batch.restype = C.c_int
+def emulate(cfg, settings, twist=False):
+    """Test-only CPU emulation of the structured wave kernel (mpc_wave.hpp, 256 lanes as threads);
+    twist: the build with the twisted elimination of the default horizon (IMPC_TWIST=1)."""
+    path = EMU_TW_PATH if twist else EMU_PATH
+    if path not in _E:
+        _E[path] = C.CDLL(path)
+        _E[path].emu_wave_solve_batch.restype = C.c_int
+    E = _E[path]
     pat, v = cfg["pattern"], cfg["values"]
     B = v["q"].shape[0]
     n, m = pat["n"], pat["m"]
@@ -91,7 +94,7 @@ def emulate(cfg, settings):
     xo, yo = np.empty((B, n)), np.empty((B, m))
     info = np.empty(B, dtype=impc.INFO_DTYPE)
     p = lambda a: None if a is None else a.ctypes.data_as(C.c_void_p)  # noqa: E731
-    rc = _E.emu_wave_solve_batch(C.c_int64(n), C.c_int64(m), *[p(a) for a in pats], C.c_int64(B),
+    rc = E.emu_wave_solve_batch(C.c_int64(n), C.c_int64(m), *[p(a) for a in pats], C.c_int64(B),
                                  *[p(a) for a in keep], C.byref(settings), p(xw), p(yw), p(xo), p(yo),
                                  info.ctypes.data_as(C.c_void_p))
     assert rc == 0, rc

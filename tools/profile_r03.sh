@@ -5,12 +5,16 @@
 # Every step has its own time limit; the script stops at the first failure.
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; cd "$R" || exit 1; export TMPDIR=/tmp
-O="$R/gpurun_out/r03f"; mkdir -p "$O"
+O="$R/gpurun_out/${TAG:-r03f}"; mkdir -p "$O"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
 tail -n 1 $O/pytest_gpu.log
 timeout -k 10 120 python -u tools/tlim_diag.py . r03 > $O/tlim_r03.jsonl 2> $O/tlim.err || { tail -20 $O/tlim.err; exit 1; }
 head -1 $O/tlim_r03.jsonl | cut -c1-200
-IMPC_LIB_VARIANT=prof timeout -k 10 300 python -u tools/section_profile.py > $O/section_profile.txt 2> $O/sec.err || { tail -20 $O/sec.err; exit 1; }
+if [ -f intent-mpc_amd/lib/libimpc_qp_prof.so ]; then
+  IMPC_LIB_VARIANT=prof timeout -k 10 300 python -u tools/section_profile.py > $O/section_profile.txt 2> $O/sec.err || { tail -20 $O/sec.err; exit 1; }
+fi
+timeout -k 10 400 python3 -u bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail -20 $O/bench_default.err; exit 1; }
+cut -c1-300 $O/bench_default.json
 cd /tmp || exit 1
 B="$R/bench.py"
 ARGS0="--cpu-sample 0 --e2e-steps 0"
