@@ -2425,34 +2425,41 @@ struct WaveQP {
         int32_t chk_left = chk, rho_left = rho_int;
         // The refactorisation after an adaptive-rho update runs between two passes of the inner
         // iteration loop rather than inside it: the register allocator then places the spills the
-        // factorisation's temporaries force around that (rare) call, outside the hot loop.  The
-        // order of operations is the one of a single loop.
+        // factorisation's temporaries force around that (rare) call, outside the hot loop.
         bool refac = false;
         iter = 1;
         for (;;) {
-        if (refac) {
-            refac = false;
-            factorize();
-            write_v_products();
-            IMPC_SEC(kSecFactor);
-        }
-        for (; iter <= max_iter; iter++) {
-            const bool chk_now = chk && --chk_left == 0;
-            if (chk_now) chk_left = chk;
-            const bool rho_now = rho_int && --rho_left == 0;
-            if (rho_now) rho_left = rho_int;
-            const bool need_delta = chk_now || iter == max_iter || tlim;
-            iterate(need_delta);
-            // osqp_solve (PROFILING build): checked after the ADMM steps, before can_check is
-            // recomputed (so it keeps the previous iteration's value); one team-wide decision
-            if (tlim) {
-                const double el = wv.max((double)(device_clock() - t0) * tick);
-                if (el >= tl) {
-                    status = IMPC_TIME_LIMIT_REACHED;
-                    break;
-                }
+            if (refac) {
+                refac = false;
+                factorize();
+                write_v_products();
+                IMPC_SEC(kSecFactor);
             }
-            can_check = chk_now;
+            // the hot loop: ADMM steps up to the next termination check / rho update (or the end);
+            // the check and the update run between two passes of it, so their code and registers
+            // sit outside it (the operations are those of one loop, in the same order)
+            bool chk_now = false, rho_now = false, stop = false;
+            for (; iter <= max_iter; iter++) {
+                chk_now = chk && --chk_left == 0;
+                if (chk_now) chk_left = chk;
+                rho_now = rho_int && --rho_left == 0;
+                if (rho_now) rho_left = rho_int;
+                const bool need_delta = chk_now || iter == max_iter || tlim;
+                iterate(need_delta);
+                // osqp_solve (PROFILING build): checked after the ADMM steps, before can_check is
+                // recomputed (so it keeps the previous iteration's value); one team-wide decision
+                if (tlim) {
+                    const double el = wv.max((double)(device_clock() - t0) * tick);
+                    if (el >= tl) {
+                        status = IMPC_TIME_LIMIT_REACHED;
+                        stop = true;
+                        break;
+                    }
+                }
+                can_check = chk_now;
+                if (chk_now || rho_now) break;
+            }
+            if (stop || iter > max_iter) break;
             if (can_check) {
                 IMPC_SEC_START();
                 double D[VS], Eb[VS], Eg[GS];
@@ -2479,12 +2486,9 @@ struct WaveQP {
                     set_rho(dmin(dmax(rn, kRhoMin), kRhoMax));
                     rho_updates += 1;
                     refac = true;
-                    iter++;  // this iteration is complete; the next pass starts at the next one
-                    break;
                 }
             }
-        }
-        if (!refac) break;
+            iter++;  // this iteration is complete; the next pass starts at the next one
         }
         IMPC_SEC_START();
         double D[VS], Eb[VS], Eg[GS];
