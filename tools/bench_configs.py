@@ -27,6 +27,9 @@ import impc  # noqa: E402
 from impc import scenarios  # noqa: E402
 
 
+QUEUE = "longest"  # work-queue order of the launches (impc_batch_set_queue_order), --queue
+
+
 def run(ctx, name, cfgs, steps, settings):
     batches = []
     for cfg in cfgs:
@@ -37,6 +40,8 @@ def run(ctx, name, cfgs, steps, settings):
         b.set_values(v["Px"], v["q"], v["Ax"], v["l"], v["u"])
         if cfg.get("x_ws") is not None:
             b.warm_start(cfg["x_ws"], None)
+        if QUEUE == "longest":
+            b.set_queue_order(impc.QUEUE_LONGEST_FIRST, scenarios.queue_weight(cfg["params"], cfg["N"]))
         batches.append(b)
     total = sum(b.B for b in batches)
 
@@ -64,13 +69,16 @@ def run(ctx, name, cfgs, steps, settings):
         b.close()
     return {"config": name, "qps": total, "steps": steps, "ms_per_step": 1000 * el / steps,
             "qp_solves_per_s": total * steps / el, "mean_iter": float(iters.mean()), "kernels": kernels,
-            "launch": "grouped" if grouped else "per batch"}
+            "launch": "grouped" if grouped else "per batch", "queue": QUEUE}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--queue", choices=("longest", "fifo"), default="longest")
     args = ap.parse_args()
+    global QUEUE
+    QUEUE = args.queue
     ctx = impc.Context(0)
     s = impc.default_settings(verbose=0)
     print(json.dumps(run(ctx, "1: single N=20 K=0 QP (cold)", [scenarios.first_call_config(batch=1, seed=1)],
@@ -106,6 +114,8 @@ def receding(ctx, bks, steps, settings):
         b.set_values(v["Px"], v["q"], v["Ax"], v["l"], v["u"])
         b.warm_start(bk["x_ws"], None)
         b.set_persistent(True)
+        if QUEUE == "longest":
+            b.set_queue_order(impc.QUEUE_LONGEST_FIRST, scenarios.queue_weight(bk["params"], bk["N"]))
         batches.append(b)
     total = sum(b.B for b in batches)
     impc.solve_group(batches)  # setup + first solve (t = 0)
@@ -131,7 +141,7 @@ def receding(ctx, bks, steps, settings):
     return {"config": "5: 8192 of 65536 N=40 K=10(+1) receding window, persistent workspaces (update q, l, u; "
                       "scaling replayed from the kept factors, rho and iterates kept)", "qps": total, "steps": steps, "ms_per_step": 1000 * el / steps,
             "qp_solves_per_s": total * steps / el, "mean_iter": float(iters.mean()),
-            "mean_iter_first_solve": float(it0.mean()), "kernels": ["structured"], "launch": "grouped"}
+            "mean_iter_first_solve": float(it0.mean()), "kernels": ["structured"], "launch": "grouped", "queue": QUEUE}
 
 
 if __name__ == "__main__":
