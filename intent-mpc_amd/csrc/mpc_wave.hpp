@@ -114,6 +114,35 @@ namespace impc {
 #ifndef IMPC_PCAP_REG  // pair sweeps: keep the stage results in registers until the sweep ends (1)
 #define IMPC_PCAP_REG 0  // or store each one as it is produced (0: measured faster, fewer spills)
 #endif
+// Round-3 iteration-latency experiments (tools/exp.sh, profiles/r03/exp/README.md "Branch-free
+// general rows and the other phase / sweep variants"): only IMPC_GFREE paid (-1.9..-2.2 % kernel
+// time, identical iterations) and is on; the rest were measured slower alone or beside it, off.
+#ifndef IMPC_GFREE  // general-row update / products without per-slot branches (the GS slots'
+#define IMPC_GFREE 1  // chains interleave; an empty slot computes zeros into the discard slot)
+#endif
+#ifndef IMPC_GUNROLL  // rhs column gather: the groups of a compile-time group count issued at once
+#define IMPC_GUNROLL 0  // (dispatch on CG4) instead of one LDS round trip per group of four
+#endif
+#ifndef IMPC_TREE  // S1 / S3 / S5 / general-row dot products as two to four partial chains
+#define IMPC_TREE 0
+#endif
+#ifndef IMPC_NDT  // the check-iteration deltas: update phase instantiated with and without them
+#define IMPC_NDT 0
+#endif
+#ifndef IMPC_HCAP  // default-horizon sweeps: every step's output kept in its own register (no
+#define IMPC_HCAP 0  // per-step capture select), stored by one lane row / column after the sweep
+#endif
+#ifndef IMPC_SSTORE  // default-horizon sweeps: every stage result stored as produced by all lanes
+#define IMPC_SSTORE 0  // (same value, same address per output index) instead of register captures
+#endif
+#ifndef IMPC_SFOLD  // stage recursions carry (c, S) with a = c - S: the next product is
+#define IMPC_SFOLD 0  // fma(-f, S, f c), one dependent operation per step fewer
+#endif
+
+template <bool B>
+struct BoolC {
+    static constexpr bool value = B;
+};
 
 struct WaveTables {
     int32_t n, m, mg, N, W, CG, nnzP, nnzA;
@@ -522,6 +551,16 @@ struct WaveQP {
     IMPC_WF int gcol(int s, int e) const { return gc[s][e] & 0xFFFF; }
     IMPC_WF int gdst(int s, int e) const { return gc[s][e] >> 16; }
 
+    // col_gather's loop for C4 = 4 NG: s = 0 + group 0 + group 1 + ..., each group (p0+p1)+(p2+p3)
+    template <int NG>
+    IMPC_WF static double gather_n(const double *pb, int sd) {
+        double p[4 * NG];
+        _Pragma("unroll") for (int t = 0; t < 4 * NG; t++) p[t] = pb[t * sd];
+        double s = 0.0;
+        _Pragma("unroll") for (int g = 0; g < NG; g++) s += (p[4 * g] + p[4 * g + 1]) + (p[4 * g + 2] + p[4 * g + 3]);
+        return s;
+    }
+
     // gather sum over the general entries of column v (column-slot layout, independent reads;
     // the sums add groups of four in entry order).  TIER: the first T1 rows, then -- for a heavy
     // column, h = its second-tier index (hid_, -1 for a light column) -- the second tier
@@ -531,6 +570,17 @@ struct WaveQP {
         double s = 0.0;
         if constexpr (!TIER) {
             (void)h;
+#if IMPC_GUNROLL
+            // the same sum, every read of the column issued before the first add (C4 is uniform)
+            switch (C4) {
+                case 4: return gather_n<1>(pb, sd);
+                case 8: return gather_n<2>(pb, sd);
+                case 12: return gather_n<3>(pb, sd);
+                case 16: return gather_n<4>(pb, sd);
+                case 20: return gather_n<5>(pb, sd);
+                default: break;
+            }
+#endif
             for (int t = 0; t < C4; t += 4) {
                 const double p0 = pb[t * sd], p1 = pb[(t + 1) * sd], p2 = pb[(t + 2) * sd], p3 = pb[(t + 3) * sd];
                 s += (p0 + p1) + (p2 + p3);
@@ -1321,6 +1371,15 @@ struct WaveQP {
 #endif
     }
 
+    // IMPC_SFOLD: a step's state is (c, S) with v = c - S (c the step's t / e value, S its 8-lane
+    // sum); the next step's product f v is formed as fma(-f, S, f c), with f c off the chain, so
+    // the subtraction leaves the dependent chain (v itself is formed only for the stores)
+    template <bool STRIDE>
+    IMPC_WF double fstep(double f, double c, double S) {
+        const double p = __builtin_fma(-f, S, prod_nc(f, c));
+        return STRIDE ? wv.sum_stride8(p) : wv.sum_contig8(p);
+    }
+
     // Sweeps with a compile-time step count WC (= WSPEC) are fully unrolled: every LDS wait is
     // exact and the step results stay in registers until the sweep ends, instead of an LDS store
     // per step whose completion the next step's wait would include (measured 195 -> 157 cycles
@@ -1353,24 +1412,63 @@ struct WaveQP {
         // (F, t) of the next even / odd step, loaded two steps ahead (reads past the last stage
         // stay inside the LDS buffers and are never used)
         double fe = Fm[l], te = tb[13 + j], fo = Fm[64 + l], to = tb[26 + i];
+#if IMPC_SFOLD
+        double S = 0.0;  // a_0 = t_0 - 0
+#endif
+        // one step: a <- t - R(f a); SFOLD: (a, S) <- (t, R(fma(-f, S, f a))), the value t - S
+        auto step = [&](auto stride, double f, double t) -> double {
+#if IMPC_SFOLD
+            S = fstep<decltype(stride)::value>(f, a, S);
+            a = t;
+            return t - S;
+#else
+            a = rstep<decltype(stride)::value>(f, t, a);
+            return a;
+#endif
+        };
+        using ST = BoolC<true>;
+        using SC = BoolC<false>;
         if constexpr (WC > 0) {
             double c0[CQ], c1[CQ];
             _Pragma("unroll") for (int q = 0; q < CQ; q++) c0[q] = c1[q] = 0.0;
+#if IMPC_SSTORE
+            // each stage stored as produced by all 64 lanes: the 8 lanes of an output index hold
+            // bitwise the same value and write it to the same address (no lane mask, no capture)
+            double *rj = rb + j, *ri = rb + i;
+#elif IMPC_HCAP
+            double hist[WC];  // every step's output in registers (constant indices), stored after
+#endif
             _Pragma("unroll") for (int k = 0; k < WC; k += 2) {
                 const double f0 = fe, t0 = te;
                 fe = Fm[64 * (k + 2) + l];
                 te = tb[13 * (k + 3) + j];
-                a = rstep<true>(f0, t0, a);
-                cap(c0, a, k, i);
+#if IMPC_SSTORE
+                rj[13 * (k + 1)] = step(ST{}, f0, t0);
+#elif IMPC_HCAP
+                hist[k] = step(ST{}, f0, t0);
+#else
+                cap(c0, step(ST{}, f0, t0), k, i);
+#endif
                 if (k + 1 < WC) {
                     const double f1 = fo, t1 = to;
                     fo = Fm[64 * (k + 3) + l];
                     to = tb[13 * (k + 4) + i];
-                    a = rstep<false>(f1, t1, a);
-                    cap(c1, a, k + 1, j);
+#if IMPC_SSTORE
+                    ri[13 * (k + 2)] = step(SC{}, f1, t1);
+#elif IMPC_HCAP
+                    hist[k + 1] = step(SC{}, f1, t1);
+#else
+                    cap(c1, step(SC{}, f1, t1), k + 1, j);
+#endif
                 }
             }
+#if IMPC_HCAP
+            // even steps' outputs (index j) from the lanes i == 0, odd steps' (index i) from j == 0
+            if (i == 0) _Pragma("unroll") for (int k = 0; k < WC; k += 2) rb[13 * (k + 1) + j] = hist[k];
+            if (j == 0) _Pragma("unroll") for (int k = 1; k < WC; k += 2) rb[13 * (k + 1) + i] = hist[k];
+#elif !IMPC_SSTORE
             cap_store<true>(c0, c1, rb, WC, true, i, j);
+#endif
         } else {
             // one lane per element writes, the rest write to discard slots (no divergent branch)
             double *junk = lds + LD::JUNK_OFF + lo;
@@ -1379,14 +1477,12 @@ struct WaveQP {
                 const double f0 = fe, t0 = te;
                 fe = Fm[64 * (k + 2) + l];
                 te = tb[13 * (k + 3) + j];
-                a = rstep<true>(f0, t0, a);
-                *(wrj ? rb + 13 * (k + 1) + j : junk) = a;
+                *(wrj ? rb + 13 * (k + 1) + j : junk) = step(ST{}, f0, t0);
                 if (k + 1 >= W) break;
                 const double f1 = fo, t1 = to;
                 fo = Fm[64 * (k + 3) + l];
                 to = tb[13 * (k + 4) + i];
-                a = rstep<false>(f1, t1, a);
-                *(wri ? rb + 13 * (k + 2) + i : junk) = a;
+                *(wri ? rb + 13 * (k + 2) + i : junk) = step(SC{}, f1, t1);
             }
         }
     }
@@ -1403,26 +1499,64 @@ struct WaveQP {
         const int k1 = W - 2 > 0 ? W - 2 : 0;
         double fa = Fm[64 * (W - 1) + l], ea = eb[13 * (W - 1) + (ODD ? j : i)];
         double fb = Fm[64 * k1 + l], ebv = eb[13 * k1 + (ODD ? i : j)];
+#if IMPC_SFOLD
+        double S = 0.0;  // x_W = e_W - 0
+#endif
+        auto step = [&](auto stride, double f, double e) -> double {
+#if IMPC_SFOLD
+            S = fstep<decltype(stride)::value>(f, x, S);
+            x = e;
+            return e - S;
+#else
+            x = rstep<decltype(stride)::value>(f, e, x);
+            return x;
+#endif
+        };
+        using SA = BoolC<ODD>;
+        using SB = BoolC<!ODD>;
         if constexpr (WC > 0) {
             double c0[CQ], c1[CQ];
             _Pragma("unroll") for (int q = 0; q < CQ; q++) c0[q] = c1[q] = 0.0;
+#if IMPC_SSTORE
+            double *xe = xb + (ODD ? j : i), *xo = xb + (ODD ? i : j);  // even / odd steps' outputs
+#elif IMPC_HCAP
+            double hist[WC];
+#endif
             _Pragma("unroll") for (int m = 0; m < WC; m += 2) {
                 const int k = WC - 1 - m;
                 const int k2 = k - 2 > 0 ? k - 2 : 0, k3 = k - 3 > 0 ? k - 3 : 0;
                 const double f0 = fa, e0 = ea;
                 fa = Fm[64 * k2 + l];
                 ea = eb[13 * k2 + (ODD ? j : i)];
-                x = rstep<ODD>(f0, e0, x);
-                cap(c0, x, m, ODD ? i : j);
+#if IMPC_SSTORE
+                xe[13 * k] = step(SA{}, f0, e0);
+#elif IMPC_HCAP
+                hist[m] = step(SA{}, f0, e0);
+#else
+                cap(c0, step(SA{}, f0, e0), m, ODD ? i : j);
+#endif
                 if (m + 1 < WC) {
                     const double f1 = fb, e1 = ebv;
                     fb = Fm[64 * k3 + l];
                     ebv = eb[13 * k3 + (ODD ? i : j)];
-                    x = rstep<!ODD>(f1, e1, x);
-                    cap(c1, x, m + 1, ODD ? j : i);
+#if IMPC_SSTORE
+                    xo[13 * (k - 1)] = step(SB{}, f1, e1);
+#elif IMPC_HCAP
+                    hist[m + 1] = step(SB{}, f1, e1);
+#else
+                    cap(c1, step(SB{}, f1, e1), m + 1, ODD ? j : i);
+#endif
                 }
             }
+#if IMPC_HCAP
+            // step m is stage WC - 1 - m; even steps' outputs at index j (ODD) / i, odd steps' at the other
+            if ((ODD ? i : j) == 0)
+                _Pragma("unroll") for (int m = 0; m < WC; m += 2) xb[13 * (WC - 1 - m) + (ODD ? j : i)] = hist[m];
+            if ((ODD ? j : i) == 0)
+                _Pragma("unroll") for (int m = 1; m < WC; m += 2) xb[13 * (WC - 1 - m) + (ODD ? i : j)] = hist[m];
+#elif !IMPC_SSTORE
             cap_store<ODD>(c0, c1, xb, WC, false, i, j);
+#endif
         } else {
             double *junk = lds + LD::JUNK_OFF + lo;
             const bool wri = j == 0, wrj = i == 0;
@@ -1431,14 +1565,12 @@ struct WaveQP {
                 const double f0 = fa, e0 = ea;
                 fa = Fm[64 * k2 + l];
                 ea = eb[13 * k2 + (ODD ? j : i)];
-                x = rstep<ODD>(f0, e0, x);
-                *(ODD ? (wrj ? xb + 13 * k + j : junk) : (wri ? xb + 13 * k + i : junk)) = x;
+                *(ODD ? (wrj ? xb + 13 * k + j : junk) : (wri ? xb + 13 * k + i : junk)) = step(SA{}, f0, e0);
                 if (k - 1 < 0) break;
                 const double f1 = fb, e1 = ebv;
                 fb = Fm[64 * k3 + l];
                 ebv = eb[13 * k3 + (ODD ? i : j)];
-                x = rstep<!ODD>(f1, e1, x);
-                *(ODD ? (wri ? xb + 13 * (k - 1) + i : junk) : (wrj ? xb + 13 * (k - 1) + j : junk)) = x;
+                *(ODD ? (wri ? xb + 13 * (k - 1) + i : junk) : (wrj ? xb + 13 * (k - 1) + j : junk)) = step(SB{}, f1, e1);
             }
         }
     }
@@ -1447,7 +1579,7 @@ struct WaveQP {
     IMPC_WF void write_v_products() {
         double *pb = pbuf();
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
-            if (gok[s]) {
+            if (IMPC_GFREE || gok[s]) {  // an empty slot writes a zero product to the discard slot
                 double vv = rhog_(s) * z[s] - y[s];
                 _Pragma("unroll") for (int e = 0; e < 4; e++) pb[gdst(s, e)] = a[s][e] * vv;
             }
@@ -1490,7 +1622,16 @@ struct WaveQP {
                     double rv[5];
                     _Pragma("unroll") for (int cc = 0; cc < 5; cc++) rv[cc] = rp[cc];
                     IMPC_LOADS_FIRST(5, 12);
+#if IMPC_TREE
+                    double tb2 = cp[s][1] * rv[1];
+                    tb2 += cp[s][3] * rv[3];
+                    t -= cp[s][0] * rv[0];
+                    t -= cp[s][2] * rv[2];
+                    t -= cp[s][4] * rv[4];
+                    t -= tb2;
+#else
                     _Pragma("unroll") for (int cc = 0; cc < 5; cc++) t -= cp[s][cc] * rv[cc];
+#endif
                 }
                 if constexpr (LD::PAIR) {
                     // pair-blocked forward: on the even stages k >= 2 the chain takes
@@ -1550,8 +1691,15 @@ struct WaveQP {
                 double rv[13];
                 _Pragma("unroll") for (int cc = 0; cc < 13; cc++) rv[cc] = rk[cc];
                 IMPC_LOADS_FIRST(7, 20);
+#if IMPC_TREE
+                double ea[4];
+                _Pragma("unroll") for (int u = 0; u < 4; u++) ea[u] = ainv[s][u] * rv[u];
+                _Pragma("unroll") for (int cc = 4; cc < 13; cc++) ea[cc & 3] += ainv[s][cc] * rv[cc];
+                const double e = (ea[0] + ea[1]) + (ea[2] + ea[3]);
+#else
                 double e = 0.0;
                 _Pragma("unroll") for (int cc = 0; cc < 13; cc++) e += ainv[s][cc] * rv[cc];
+#endif
                 eb[NL * s + L] = e;
             }
             wv.lsync();
@@ -1605,7 +1753,14 @@ struct WaveQP {
                 double xv[8];
                 _Pragma("unroll") for (int j = 0; j < 8; j++) xv[j] = xn[j];
                 IMPC_LOADS_FIRST(5, 16);
+#if IMPC_TREE
+                double tb2 = cp[s][1] * xv[1];
+                _Pragma("unroll") for (int j = 3; j < 8; j += 2) tb2 += cp[s][j] * xv[j];
+                _Pragma("unroll") for (int j = 0; j < 8; j += 2) t -= cp[s][j] * xv[j];
+                t -= tb2;
+#else
                 _Pragma("unroll") for (int j = 0; j < 8; j++) t -= cp[s][j] * xv[j];
+#endif
                 xb[NL * s + L] = t;
             }
             wv.lsync();
@@ -1614,9 +1769,23 @@ struct WaveQP {
         update_and_products(need_delta);
     }
 
-    // update_x and the box rows (update_z / project / update_y), the general rows, and the
-    // products of the next rhs (the end of every ADMM iteration)
     IMPC_WF void update_and_products(bool need_delta) {
+#if IMPC_NDT
+        if (need_delta)
+            update_and_products_t<true>();
+        else
+            update_and_products_t<false>();
+#else
+        update_and_products_t<false>(need_delta);
+#endif
+    }
+
+    // update_x and the box rows (update_z / project / update_y), the general rows, and the
+    // products of the next rhs (the end of every ADMM iteration).  ND: the check-iteration deltas
+    // are written (IMPC_NDT: a compile-time instance each; otherwise the runtime flag nd).
+    template <bool ND>
+    IMPC_WF void update_and_products_t(bool nd = ND) {
+        const bool need_delta = ND || nd;
         double *xb = xbuf();
         const double alpha = alp_, oma = (double)1.0 - alp_;
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
@@ -1633,16 +1802,21 @@ struct WaveQP {
             if (need_delta) dyb(s) = dy;
             zb[s] = zn;
         }
-        // general rows
+        // general rows (IMPC_GFREE: an empty slot's columns are the zero tail of the x exchange, its
+        // A values, bounds and iterates zero, so it computes zeros, without a per-slot branch)
         double xg[GS][4];
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
-            _Pragma("unroll") for (int e = 0; e < 4; e++) xg[s][e] = gok[s] ? xb[gcol(s, e)] : 0.0;
+            _Pragma("unroll") for (int e = 0; e < 4; e++) xg[s][e] = (IMPC_GFREE || gok[s]) ? xb[gcol(s, e)] : 0.0;
         }
         IMPC_LOADS_FIRST(4 * GS, 8 * GS);
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
-            if (!gok[s]) continue;
+            if (!IMPC_GFREE && !gok[s]) continue;
+#if IMPC_TREE
+            const double zt = (a[s][0] * xg[s][0] + a[s][1] * xg[s][1]) + (a[s][2] * xg[s][2] + a[s][3] * xg[s][3]);
+#else
             double zt = 0.0;
             _Pragma("unroll") for (int e = 0; e < 4; e++) zt += a[s][e] * xg[s][e];
+#endif
             double zr = alpha * zt + oma * z[s];
             double zn = dmin(dmax(zr + rhoig_(s) * y[s], lg[s]), ug[s]);
             double dy = rhog_(s) * (zr - zn);
