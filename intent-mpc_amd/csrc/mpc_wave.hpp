@@ -70,9 +70,15 @@ namespace impc {
 #ifndef IMPC_PRIO  // raise the wave priority of the stage-recursion wavefront during its sweeps
 #define IMPC_PRIO 0
 #endif
+#ifndef IMPC_PRIO_INV  // the inverse: every wave at this priority, the recursion wavefront drops to 0
+#define IMPC_PRIO_INV 0  // during its sweeps (the parallel phases win the SIMD's issue arbitration)
+#endif
 #if IMPC_PRIO
 #define IMPC_PRIO_HI() __builtin_amdgcn_s_setprio(IMPC_PRIO)
 #define IMPC_PRIO_LO() __builtin_amdgcn_s_setprio(0)
+#elif IMPC_PRIO_INV && defined(__HIP_DEVICE_COMPILE__)
+#define IMPC_PRIO_HI() __builtin_amdgcn_s_setprio(0)
+#define IMPC_PRIO_LO() __builtin_amdgcn_s_setprio(IMPC_PRIO_INV)
 #else
 #define IMPC_PRIO_HI() ((void)0)
 #define IMPC_PRIO_LO() ((void)0)
@@ -125,6 +131,15 @@ namespace impc {
 #endif
 #ifndef IMPC_TREE  // S1 / S3 / S5 / general-row dot products as two to four partial chains
 #define IMPC_TREE 0
+#endif
+#ifndef IMPC_PFREE  // rhs / S1 / S3 / S5 without the per-lane variable-kind branches (on: -0.6 %)
+#define IMPC_PFREE 1
+#endif
+#ifndef IMPC_VMAX  // the iteration's projections by v_max_f64 / v_min_f64 instead of compare + selects
+#define IMPC_VMAX 1  // (on: -1.2 %; with PFREE -1.7 %)
+#endif
+#ifndef IMPC_LOOPC  // the inner loop counts to the pass's next event (check / rho update / max_iter)
+#define IMPC_LOOPC 1  // computed once per pass, instead of per-iteration countdown bookkeeping
 #endif
 #ifndef IMPC_NDT  // the check-iteration deltas: update phase instantiated with and without them
 #define IMPC_NDT 0
@@ -464,6 +479,11 @@ struct WaveQP {
             hid_[s] = TIER && vok[s] ? T.col_hid[v] : -1;  // second products tier (TIER batches)
             x[s] = q[s] = pd[s] = ab[s] = zb[s] = yb[s] = lb[s] = ub[s] = dxv_[s] = dyb_[s] = 0.0;
             bt[s] = 0;
+#if IMPC_PFREE
+            // the branch-free phases read a slot's factor rows whether or not it holds a variable
+            _Pragma("unroll") for (int cc = 0; cc < 13; cc++) ainv[s][cc] = 0.0;
+            _Pragma("unroll") for (int cc = 0; cc < 8; cc++) cp[s][cc] = 0.0;
+#endif
             if (vok[s]) {
                 int ov = T.var_orig[v];
                 q[s] = io.q[bn + ov];
@@ -1598,9 +1618,10 @@ struct WaveQP {
         double *rb = rbuf(), *tb = tbuf(), *eb = ebuf(), *xb = xbuf();
         const double sigma = sig_;
         IMPC_REP(kSecRhs) {
-            // rhs = sigma x - q + A' v   (stage order)
+            // rhs = sigma x - q + A' v   (stage order; IMPC_PFREE: an empty slot's iterates, bounds
+            // and column are zero, so it writes 0)
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
-                if (!vok[s]) continue;
+                if (!IMPC_PFREE && !vok[s]) continue;
                 int v = NL * s + L;
                 double vb = rhob(s) * zb[s] - yb[s];
                 double r = sigma * x[s] - q[s];
@@ -1612,13 +1633,17 @@ struct WaveQP {
         }
         IMPC_SEC(kSecRhs);
         IMPC_REP(kSecS1) {
-            // S1: t_k = r_k[:8] - G_{k-1}[:, 8:] r_{k-1}[8:]
+            // S1: t_k = r_k[:8] - G_{k-1}[:, 8:] r_{k-1}[8:]  (IMPC_PFREE: every lane; a stage-0 or
+            // empty slot has zero coupling coefficients, a control lane's t lands in a slot nothing
+            // reads)
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
-                if (!vok[s] || vr_[s] >= 8) continue;
+                if (!IMPC_PFREE && (!vok[s] || vr_[s] >= 8)) continue;
                 int v = NL * s + L;
                 double t = rb[v];
-                if (vs_[s] > 0) {
-                    const double *rp = rb + 13 * (vs_[s] - 1) + 8;
+                if (IMPC_PFREE || vs_[s] > 0) {
+                    // (PFREE, stage 0: the zero tail of the x exchange, not LDS below rb -- past the
+                    // horizon's last F block that is another QP's data or uninitialised)
+                    const double *rp = !IMPC_PFREE || vs_[s] > 0 ? rb + 13 * (vs_[s] - 1) + 8 : xbuf() + LD::NMAX;
                     double rv[5];
                     _Pragma("unroll") for (int cc = 0; cc < 5; cc++) rv[cc] = rp[cc];
                     IMPC_LOADS_FIRST(5, 12);
@@ -1686,7 +1711,7 @@ struct WaveQP {
         IMPC_REP(kSecS3) {
             // S3: e_k = Ahat_k^{-1} rhat_k
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
-                if (!vok[s]) continue;
+                if (!IMPC_PFREE && !vok[s]) continue;
                 const double *rk = rb + 13 * vs_[s];
                 double rv[13];
                 _Pragma("unroll") for (int cc = 0; cc < 13; cc++) rv[cc] = rk[cc];
@@ -1745,9 +1770,10 @@ struct WaveQP {
         }
         IMPC_SEC(kSecBwd);
         IMPC_REP(kSecS5) {
-            // S5: controls x_k[8:] = e_k[8:] - G_k[:, 8:]' x_{k+1}[:8]
+            // S5: controls x_k[8:] = e_k[8:] - G_k[:, 8:]' x_{k+1}[:8]  (IMPC_PFREE: every lane, the
+            // state lanes' and empty slots' results to their discard slots)
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
-                if (!vok[s] || vr_[s] < 8) continue;
+                if (!IMPC_PFREE && (!vok[s] || vr_[s] < 8)) continue;
                 const double *xn = xb + 13 * (vs_[s] + 1);
                 double t = eb[NL * s + L];
                 double xv[8];
@@ -1761,12 +1787,26 @@ struct WaveQP {
 #else
                 _Pragma("unroll") for (int j = 0; j < 8; j++) t -= cp[s][j] * xv[j];
 #endif
+#if IMPC_PFREE
+                *(vok[s] && vr_[s] >= 8 ? xb + NL * s + L : lds + LD::JUNK_OFF + L) = t;
+#else
                 xb[NL * s + L] = t;
+#endif
             }
             wv.lsync();
         }
         IMPC_SEC(kSecS5);
         update_and_products(need_delta);
+    }
+
+    // project_z (auxil.h): min(max(v, l), u) as c_max / c_min, or (IMPC_VMAX) as v_max_f64 /
+    // v_min_f64 -- the same value except the sign of a zero when v equals a zero bound
+    IMPC_WF static double clampz(double v, double l, double u) {
+#if IMPC_VMAX
+        return __builtin_fmin(__builtin_fmax(v, l), u);
+#else
+        return dmin(dmax(v, l), u);
+#endif
     }
 
     IMPC_WF void update_and_products(bool need_delta) {
@@ -1796,7 +1836,7 @@ struct WaveQP {
             x[s] = xn;
             double zt = ab[s] * xt;
             double zr = alpha * zt + oma * zb[s];
-            double zn = dmin(dmax(zr + rhoib(s) * yb[s], lb[s]), ub[s]);
+            double zn = clampz(zr + rhoib(s) * yb[s], lb[s], ub[s]);
             double dy = rhob(s) * (zr - zn);
             yb[s] += dy;
             if (need_delta) dyb(s) = dy;
@@ -1818,7 +1858,7 @@ struct WaveQP {
             _Pragma("unroll") for (int e = 0; e < 4; e++) zt += a[s][e] * xg[s][e];
 #endif
             double zr = alpha * zt + oma * z[s];
-            double zn = dmin(dmax(zr + rhoig_(s) * y[s], lg[s]), ug[s]);
+            double zn = clampz(zr + rhoig_(s) * y[s], lg[s], ug[s]);
             double dy = rhog_(s) * (zr - zn);
             y[s] += dy;
             if (need_delta) dyg(s) = dy;
@@ -2477,6 +2517,9 @@ struct WaveQP {
         // the profiling record (qpt) starts at the same tick, so a QP stopped by its limit always
         // shows a recorded latency of at least that limit
         const uint64_t t0 = device_clock();
+#if IMPC_PRIO_INV && defined(__HIP_DEVICE_COMPILE__)
+        __builtin_amdgcn_s_setprio(IMPC_PRIO_INV);
+#endif
         rw = (int)(b % (NL / 64));  // spread the serial recursions of co-resident QPs over SIMDs
 #if IMPC_HWRW && defined(__HIP_DEVICE_COMPILE__)
         // recursion wave from the hardware placement (HW_REG_HW_ID: WAVE_ID [3:0], SIMD_ID [5:4]):
@@ -2613,6 +2656,40 @@ struct WaveQP {
             // the check and the update run between two passes of it, so their code and registers
             // sit outside it (the operations are those of one loop, in the same order)
             bool chk_now = false, rho_now = false, stop = false;
+#if IMPC_LOOPC
+            // the same iterations, flags and counters as the countdown loop below: the pass runs to
+            // its next event nxt = min(iterations left, chk_left, rho_left); only its last iteration
+            // can be a check / rho-update / max_iter one
+            if (iter <= max_iter) {
+                int nxt = max_iter - iter + 1;
+                if (chk && chk_left < nxt) nxt = chk_left;
+                if (rho_int && rho_left < nxt) nxt = rho_left;
+                const bool ce = chk && chk_left == nxt, re = rho_int && rho_left == nxt;
+                const bool nd_last = ce || iter + nxt - 1 == max_iter || tlim;
+                for (int t = 1;; t++) {
+                    iterate(t == nxt ? nd_last : tlim);
+                    if (tlim) {
+                        const double el = wv.max((double)(device_clock() - t0) * tick);
+                        if (el >= tl) {
+                            status = IMPC_TIME_LIMIT_REACHED;
+                            stop = true;
+                            if (t > 1) can_check = 0;  // the previous iteration was no check
+                            break;
+                        }
+                    }
+                    if (t == nxt) break;
+                    iter++;
+                }
+                if (!stop) {
+                    chk_now = ce;
+                    rho_now = re;
+                    if (chk) chk_left = ce ? chk : chk_left - nxt;
+                    if (rho_int) rho_left = re ? rho_int : rho_left - nxt;
+                    can_check = chk_now;
+                    if (!(chk_now || rho_now)) iter++;
+                }
+            }
+#else
             for (; iter <= max_iter; iter++) {
                 chk_now = chk && --chk_left == 0;
                 if (chk_now) chk_left = chk;
@@ -2633,6 +2710,7 @@ struct WaveQP {
                 can_check = chk_now;
                 if (chk_now || rho_now) break;
             }
+#endif
             if (stop || iter > max_iter) break;
             if (can_check) {
                 IMPC_SEC_START();

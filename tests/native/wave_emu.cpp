@@ -7,6 +7,7 @@
 #include <barrier>
 #include <cstring>
 #include <thread>
+#include <limits>
 #include <vector>
 
 #include "../../intent-mpc_amd/csrc/mpc_structure.hpp"
@@ -99,7 +100,9 @@ struct EmuWave {
 template <int VS, int GS, int WF, bool TIER>
 void run_w(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSettings &st) {
     using LD = impc::WaveLds<NL, VS, GS>;
-    std::vector<double> lds((size_t)LD::size(T), 0.0);
+    // LDS starts as NaN, not zero: the GPU's LDS is uninitialised, so a read of a slot the kernel
+    // has not written must show up here
+    std::vector<double> lds((size_t)LD::size(T), std::numeric_limits<double>::quiet_NaN());
     EmuShared sh;
     std::vector<std::thread> th;
     for (int l = 0; l < NL; l++)
