@@ -313,7 +313,18 @@ struct GpuTeam {
         return v;
 #endif
     }
+    // lane l's value paired with lane l ^ 4 (ds_swizzle bit mode: and 0x1f, xor 4; no LDS access)
+    __device__ static double xor4(double v) {
+        const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), (4 << 10) | 0x1F);
+        const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), (4 << 10) | 0x1F);
+        return __hiloint2double(hi, lo);
+    }
     __device__ double max(double v) {
+#if IMPC_DPPRED
+        double mv[1] = {v};
+        max_n(mv);  // order-independent: the same value as the butterfly below
+        return mv[0];
+#endif
         for (int mask = 32; mask >= 1; mask >>= 1) {
             double o = __shfl_xor(v, mask);
             v = o > v ? o : v;
@@ -362,8 +373,76 @@ struct GpuTeam {
         }
         __syncthreads();
     }
+    // KM maxima and KS sums at once, each bitwise the value max() / sum() gives, over one LDS round
+    // (the infeasibility tests' first stages: one team exchange instead of four)
+    template <int KM, int KS>
+    __device__ void max_sum_n(double (&mx)[KM], double (&sm)[KS]) {
+        static_assert((KM + KS) * (NL / 64) <= 64, "team reduction scratch (WaveLds RED_OFF) holds 64 doubles");
+        auto mxf = [](double a, double b) { return b > a ? b : a; };
+        _Pragma("unroll") for (int k = 0; k < KM; k++) {
+            double t = mx[k];
+            t = mxf(t, dpp<0xB1>(t));
+            t = mxf(t, dpp<0x4E>(t));
+            t = mxf(t, dpp<0x141>(t));
+            t = mxf(t, dpp<0x128>(t));
+            const int lo = __double2loint(t), hi = __double2hiint(t);
+            auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+            auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+            t = mxf(__hiloint2double(rh[0], rl[0]), __hiloint2double(rh[1], rl[1]));
+            const int lo2 = __double2loint(t), hi2 = __double2hiint(t);
+            auto ql = __builtin_amdgcn_permlane32_swap(lo2, lo2, false, false);
+            auto qh = __builtin_amdgcn_permlane32_swap(hi2, hi2, false, false);
+            mx[k] = mxf(__hiloint2double(qh[0], ql[0]), __hiloint2double(qh[1], ql[1]));
+        }
+        _Pragma("unroll") for (int k = 0; k < KS; k++) sm[k] = wave_sum(sm[k]);
+        if (NL == 64) return;
+        if ((threadIdx.x & 63) == 0) {
+            _Pragma("unroll") for (int k = 0; k < KM; k++) red[(threadIdx.x >> 6) * (KM + KS) + k] = mx[k];
+            _Pragma("unroll") for (int k = 0; k < KS; k++) red[(threadIdx.x >> 6) * (KM + KS) + KM + k] = sm[k];
+        }
+        __syncthreads();
+        _Pragma("unroll") for (int k = 0; k < KM; k++) {
+            double r = red[k];
+            for (int w = 1; w < NL / 64; w++) r = red[w * (KM + KS) + k] > r ? red[w * (KM + KS) + k] : r;
+            mx[k] = r;
+        }
+        _Pragma("unroll") for (int k = 0; k < KS; k++) {
+            double r = red[KM + k];
+            for (int w = 1; w < NL / 64; w++) r = r + red[w * (KM + KS) + KM + k];
+            sm[k] = r;
+        }
+        __syncthreads();
+    }
+    // sum() inside one wavefront: the xor butterfly (partners l ^ 32, 16, 8, 4, 2, 1, each level
+    // adding a commuted pair, so every lane holds bitwise the same value), exchanges by permlane /
+    // DPP / swizzle
+    __device__ double wave_sum(double v) {
+        {
+            const int lo = __double2loint(v), hi = __double2hiint(v);
+            auto ql = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+            auto qh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+            v = __hiloint2double(qh[0], ql[0]) + __hiloint2double(qh[1], ql[1]);
+        }
+        {
+            const int lo = __double2loint(v), hi = __double2hiint(v);
+            auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+            auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+            v = __hiloint2double(rh[0], rl[0]) + __hiloint2double(rh[1], rl[1]);
+        }
+        v = v + dpp<0x128>(v);  // row_ror:8 = lane ^ 8 within a row of 16
+        v = v + xor4(v);
+        v = v + dpp<0x4E>(v);   // quad_perm [2,3,0,1] = lane ^ 2
+        v = v + dpp<0xB1>(v);   // quad_perm [1,0,3,2] = lane ^ 1
+        return v;
+    }
     __device__ double sum(double v) {
+#if IMPC_DPPRED
+        // the same xor butterfly as below, its exchanges by permlane / DPP / swizzle instead of
+        // ds_bpermute: bitwise the same sum in every lane
+        v = wave_sum(v);
+#else
         for (int mask = 32; mask >= 1; mask >>= 1) v = v + __shfl_xor(v, mask);
+#endif
         v = bcast(v, 0);
         if (NL == 64) return v;
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;

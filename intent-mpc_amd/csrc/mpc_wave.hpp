@@ -127,13 +127,28 @@ namespace impc {
 #define IMPC_GFREE 1  // chains interleave; an empty slot computes zeros into the discard slot)
 #endif
 #ifndef IMPC_GUNROLL  // rhs column gather: the groups of a compile-time group count issued at once
-#define IMPC_GUNROLL 0  // (dispatch on CG4) instead of one LDS round trip per group of four
-#endif
+#define IMPC_GUNROLL 1  // (dispatch on CG4) instead of one LDS round trip per group of four (on, with
+#endif                  // IMPC_SDC: -1.3 %; measured neutral before the branch-free phases)
 #ifndef IMPC_TREE  // S1 / S3 / S5 / general-row dot products as two to four partial chains
 #define IMPC_TREE 0
 #endif
 #ifndef IMPC_PFREE  // rhs / S1 / S3 / S5 without the per-lane variable-kind branches (on: -0.6 %)
 #define IMPC_PFREE 1
+#endif
+#ifndef IMPC_DPPRED  // team max / sum (checks, infeasibility tests): the in-wave butterfly by DPP /
+#define IMPC_DPPRED 1  // permlane / swizzle exchanges instead of ds_bpermute (bitwise the same; on: -1.6 %)
+#endif
+#ifndef IMPC_CHKRED  // termination check: both infeasibility tests' first stages in one team reduction
+#define IMPC_CHKRED 1  // (bitwise the same values; on)
+#endif
+#ifndef IMPC_CMASK  // sweep captures selected by compile-time lane masks (SGPR constants; on: -0.3..-0.6 %)
+#define IMPC_CMASK 1
+#endif
+#ifndef IMPC_OBASE  // S1 / S3 / S5 reads from one opaque per-lane base with immediate offsets
+#define IMPC_OBASE 0  // (measured +1.3 %, off)
+#endif
+#ifndef IMPC_SDC  // default-horizon instances: the products stride as a compile-time constant, so
+#define IMPC_SDC 1  // the gather's reads take immediate offsets (on)
 #endif
 #ifndef IMPC_VMAX  // the iteration's projections by v_max_f64 / v_min_f64 instead of compare + selects
 #define IMPC_VMAX 1  // (on: -1.2 %; with PFREE -1.7 %)
@@ -295,7 +310,7 @@ struct WaveLds {
     // +PAD: the obstacle rows of one stage write their products to the same column in different
     // entry slots; a stride that is not a multiple of 16 doubles puts those ds_write_b64 (bank =
     // dword mod 32, 16-lane groups) on distinct banks.  Reads stay lane-contiguous.
-    static IMPC_WF int stride(int n) { return ((n + 63) & ~63) + IMPC_PSTRIDE_PAD; }
+    static constexpr IMPC_WF int stride(int n) { return ((n + 63) & ~63) + IMPC_PSTRIDE_PAD; }
     // the factorisation uses it as (4g + e) scratch followed by the general rows' rho (RHOG_P)
     static IMPC_WF int hsp(int HS) { return HS + 1; }  // second-tier row length
     static IMPC_WF int p_size(int CG, int n, int HS, int mg, int T1r) {
@@ -412,6 +427,15 @@ struct WaveQP {
         asm volatile("" : "+v"(l));
 #endif
         return l;
+    }
+
+    // IMPC_OBASE: a phase's per-lane LDS base formed as one opaque offset, so its reads take
+    // immediate offsets (a ds_read2 offset reaches 255 doubles) instead of one address add each
+    IMPC_WF const double *lds_at(int off) const {
+#if IMPC_OBASE
+        opaque(off);
+#endif
+        return lds + off;
     }
 
     // a per-lane value the optimiser must treat as freshly computed (see lane_o)
@@ -586,7 +610,9 @@ struct WaveQP {
     // column, h = its second-tier index (hid_, -1 for a light column) -- the second tier
     IMPC_WF double col_gather(int v, int h) {
         const double *pb = pbuf() + v;
-        const int C4 = c4_, sd = sd_;
+        // (IMPC_SDC: the compile-time horizon's products stride, n = 13 (WF + 1) - 5, so the gather's
+        // reads take immediate offsets instead of per-read address arithmetic)
+        const int C4 = c4_, sd = (IMPC_SDC && WF) ? LD::stride(13 * (WF + 1) - 5) : sd_;
         double s = 0.0;
         if constexpr (!TIER) {
             (void)h;
@@ -1410,6 +1436,24 @@ struct WaveQP {
     IMPC_WF static void cap(double (&c)[CQ], double r, int m, int other) {
         if (((m >> 1) & 7) == other) c[m >> 4] = r;
     }
+    // cap with the lane test as a compile-time lane mask (OI: `other` is the lane's i = l >> 3, else
+    // j = l & 7; lane l = 8 i + j of the recursion wavefront): IMPC_CMASK selects by that constant
+    // mask in an SGPR pair instead of a v_cmp per step
+    template <bool OI>
+    IMPC_WF static void capm(double (&c)[CQ], double r, int m, int other) {
+#if IMPC_CMASK && defined(__HIP_DEVICE_COMPILE__)
+        (void)other;
+        const int v = (m >> 1) & 7;
+        const uint64_t msk = OI ? (0xFFull << (8 * v)) : (0x0101010101010101ull << v);
+        double &d = c[m >> 4];
+        int lo = __double2loint(d), hi = __double2hiint(d);
+        asm("v_cndmask_b32 %0, %0, %1, %2" : "+v"(lo) : "v"(__double2loint(r)), "s"(msk));
+        asm("v_cndmask_b32 %0, %0, %1, %2" : "+v"(hi) : "v"(__double2hiint(r)), "s"(msk));
+        d = __hiloint2double(hi, lo);
+#else
+        cap(c, r, m, other);
+#endif
+    }
     // Store a sweep's W captured steps: even steps' outputs sit at index j (EJ) or i, odd steps'
     // at the other; step m is stage m + 1 (forward) or W - 1 - m (backward).
     template <bool EJ>
@@ -1467,7 +1511,7 @@ struct WaveQP {
 #elif IMPC_HCAP
                 hist[k] = step(ST{}, f0, t0);
 #else
-                cap(c0, step(ST{}, f0, t0), k, i);
+                capm<true>(c0, step(ST{}, f0, t0), k, i);
 #endif
                 if (k + 1 < WC) {
                     const double f1 = fo, t1 = to;
@@ -1478,7 +1522,7 @@ struct WaveQP {
 #elif IMPC_HCAP
                     hist[k + 1] = step(SC{}, f1, t1);
 #else
-                    cap(c1, step(SC{}, f1, t1), k + 1, j);
+                    capm<false>(c1, step(SC{}, f1, t1), k + 1, j);
 #endif
                 }
             }
@@ -1553,7 +1597,7 @@ struct WaveQP {
 #elif IMPC_HCAP
                 hist[m] = step(SA{}, f0, e0);
 #else
-                cap(c0, step(SA{}, f0, e0), m, ODD ? i : j);
+                capm<ODD>(c0, step(SA{}, f0, e0), m, ODD ? i : j);
 #endif
                 if (m + 1 < WC) {
                     const double f1 = fb, e1 = ebv;
@@ -1564,7 +1608,7 @@ struct WaveQP {
 #elif IMPC_HCAP
                     hist[m + 1] = step(SB{}, f1, e1);
 #else
-                    cap(c1, step(SB{}, f1, e1), m + 1, ODD ? j : i);
+                    capm<!ODD>(c1, step(SB{}, f1, e1), m + 1, ODD ? j : i);
 #endif
                 }
             }
@@ -1643,7 +1687,7 @@ struct WaveQP {
                 if (IMPC_PFREE || vs_[s] > 0) {
                     // (PFREE, stage 0: the zero tail of the x exchange, not LDS below rb -- past the
                     // horizon's last F block that is another QP's data or uninitialised)
-                    const double *rp = !IMPC_PFREE || vs_[s] > 0 ? rb + 13 * (vs_[s] - 1) + 8 : xbuf() + LD::NMAX;
+                    const double *rp = lds_at(!IMPC_PFREE || vs_[s] > 0 ? LD::R_OFF + 13 * (vs_[s] - 1) + 8 : LD::X_OFF + LD::NMAX);
                     double rv[5];
                     _Pragma("unroll") for (int cc = 0; cc < 5; cc++) rv[cc] = rp[cc];
                     IMPC_LOADS_FIRST(5, 12);
@@ -1712,7 +1756,7 @@ struct WaveQP {
             // S3: e_k = Ahat_k^{-1} rhat_k
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
                 if (!IMPC_PFREE && !vok[s]) continue;
-                const double *rk = rb + 13 * vs_[s];
+                const double *rk = lds_at(LD::R_OFF + 13 * vs_[s]);
                 double rv[13];
                 _Pragma("unroll") for (int cc = 0; cc < 13; cc++) rv[cc] = rk[cc];
                 IMPC_LOADS_FIRST(7, 20);
@@ -1774,7 +1818,7 @@ struct WaveQP {
             // state lanes' and empty slots' results to their discard slots)
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
                 if (!IMPC_PFREE && (!vok[s] || vr_[s] < 8)) continue;
-                const double *xn = xb + 13 * (vs_[s] + 1);
+                const double *xn = lds_at(LD::X_OFF + 13 * (vs_[s] + 1));
                 double t = eb[NL * s + L];
                 double xv[8];
                 _Pragma("unroll") for (int j = 0; j < 8; j++) xv[j] = xn[j];
@@ -2359,6 +2403,14 @@ struct WaveQP {
 
     // is_primal_infeasible (projects dy in place)
     IMPC_WF int primal_infeasible(double eps, const double D[VS], const double Eb[VS], const double Eg[GS]) {
+        double nrm, lhs;
+        pinf_partials(Eb, Eg, nrm, lhs);
+        nrm = wv.max(nrm);
+        lhs = wv.sum(lhs);
+        return pinf_stage2(eps, nrm, lhs, D);
+    }
+    // its lane-local part: the projected dy, ||E dy||_inf and u' max(dy, 0) + l' min(dy, 0)
+    IMPC_WF void pinf_partials(const double Eb[VS], const double Eg[GS], double &nrm_o, double &lhs_o) {
         const bool unsc = st.scaling > 0 && !st.scaled_termination;
         double nrm = 0.0, lhs = 0.0;
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
@@ -2383,8 +2435,12 @@ struct WaveQP {
             nrm = dmax(nrm, fabs(unsc ? Eg[s] * d : d));
             lhs += ug[s] * dmax(d, 0) + lg[s] * dmin(d, 0);
         }
-        nrm = wv.max(nrm);
-        lhs = wv.sum(lhs);
+        nrm_o = nrm;
+        lhs_o = lhs;
+    }
+    // ... and the rest, from the team-reduced norm and sum
+    IMPC_WF int pinf_stage2(double eps, double nrm, double lhs, const double D[VS]) {
+        const bool unsc = st.scaling > 0 && !st.scaled_termination;
         int res = 0;
         if (nrm > kDivTol && lhs < eps * nrm) {
             double *pb = pbuf();
@@ -2409,15 +2465,28 @@ struct WaveQP {
 
     // is_dual_infeasible
     IMPC_WF int dual_infeasible(double eps, const double D[VS], const double Eb[VS], const double Eg[GS]) {
+        double nrm, qdx;
+        dinf_partials(D, nrm, qdx);
+        nrm = wv.max(nrm);
+        qdx = wv.sum(qdx);
+        return dinf_stage2(eps, nrm, qdx, D, Eb, Eg);
+    }
+    // its lane-local part: ||D dx||_inf and q' dx
+    IMPC_WF void dinf_partials(const double D[VS], double &nrm_o, double &qdx_o) {
         const bool unsc = st.scaling > 0 && !st.scaled_termination;
-        double nrm = 0.0, qdx = 0.0, cs = unsc ? c : 1.0;
+        double nrm = 0.0, qdx = 0.0;
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (!vok[s]) continue;
             nrm = dmax(nrm, fabs(unsc ? D[s] * dxv(s) : dxv(s)));
             qdx += q[s] * dxv(s);
         }
-        nrm = wv.max(nrm);
-        qdx = wv.sum(qdx);
+        nrm_o = nrm;
+        qdx_o = qdx;
+    }
+    IMPC_WF int dinf_stage2(double eps, double nrm, double qdx, const double D[VS], const double Eb[VS],
+                            const double Eg[GS]) {
+        const bool unsc = st.scaling > 0 && !st.scaled_termination;
+        const double cs = unsc ? c : 1.0;
         int res = 0;
         if (nrm > kDivTol && qdx < cs * eps * nrm) {
             double mx = 0.0;
@@ -2472,6 +2541,21 @@ struct WaveQP {
             eps_dinf *= 10;
         }
         int prim_ok = 0, dual_ok = 0, prim_inf = 0, dual_inf = 0;
+#if IMPC_CHKRED
+        // the same tests as below, the two infeasibility tests' first-stage norms and sums reduced
+        // over the team in one exchange (bitwise the values of the separate reductions)
+        const bool ptest = T.m != 0 && !(inf.pri_res < eps_abs + eps_rel * inf.pri_norm_u);
+        prim_ok = !ptest;
+        dual_ok = inf.dua_res < eps_abs + eps_rel * inf.dua_norm_u;
+        if (ptest || !dual_ok) {
+            double mx[2] = {0.0, 0.0}, sm[2] = {0.0, 0.0};
+            if (ptest) pinf_partials(Eb, Eg, mx[0], sm[0]);
+            if (!dual_ok) dinf_partials(D, mx[1], sm[1]);
+            wv.max_sum_n(mx, sm);
+            if (ptest) prim_inf = pinf_stage2(eps_pinf, mx[0], sm[0], D);
+            if (!dual_ok) dual_inf = dinf_stage2(eps_dinf, mx[1], sm[1], D, Eb, Eg);
+        }
+#else
         if (T.m == 0) {
             prim_ok = 1;
         } else {
@@ -2484,6 +2568,7 @@ struct WaveQP {
             dual_ok = 1;
         else
             dual_inf = dual_infeasible(eps_dinf, D, Eb, Eg);
+#endif
         if (prim_ok && dual_ok) {
             status = approximate ? IMPC_SOLVED_INACCURATE : IMPC_SOLVED;
             return 1;

@@ -78,6 +78,11 @@ struct EmuWave {
     void max_n(double (&v)[K]) {
         for (int k = 0; k < K; k++) v[k] = max(v[k]);
     }
+    template <int KM, int KS>
+    void max_sum_n(double (&mx)[KM], double (&sm)[KS]) {  // the GPU's: bitwise max() / sum() each
+        for (int k = 0; k < KM; k++) mx[k] = max(mx[k]);
+        for (int k = 0; k < KS; k++) sm[k] = sum(sm[k]);
+    }
     double sum(double v) {  // per-wavefront xor butterfly (lane 0's value), waves added in order
         double *b = next_buf();
         b[l] = v;
