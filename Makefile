@@ -25,7 +25,6 @@ PROFLIB := $(LIBDIR)/libimpc_qp_prof.so
 ORACLE  := $(ORADIR)/libosqp_oracle.so
 HARNESS := $(HARNDIR)/libimpc_core_cpu.so
 EMU     := $(HARNDIR)/libwave_emu.so
-EMUTW   := $(HARNDIR)/libwave_emu_tw.so
 SHIMT   := $(HARNDIR)/shim_test
 REPLANX := $(HARNDIR)/replan_example
 
@@ -33,7 +32,7 @@ REPLANX := $(HARNDIR)/replan_example
 all: lib oracle harness
 lib: $(LIB)
 oracle: $(ORACLE)
-harness: $(HARNESS) $(EMU) $(EMUTW) $(SHIMT) $(REPLANX)
+harness: $(HARNESS) $(EMU) $(SHIMT) $(REPLANX)
 
 $(LIBDIR)/impc_qp.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symbolic.hpp $(CSRC)/mpc_wave.hpp \
 		$(CSRC)/mpc_structure.hpp $(CSRC)/select.hpp $(CSRC)/mpc_build.hpp $(CSRC)/mpc_qp_internal.hpp \
@@ -85,14 +84,6 @@ $(EMU): $(ROOT)/tests/native/wave_emu.cpp $(CSRC)/mpc_wave.hpp $(CSRC)/admm_core
 		$(CSRC)/mpc_structure.hpp
 	@mkdir -p $(HARNDIR)
 	$(HIPCC) -x hip --offload-host-only -std=c++20 -O2 -fPIC -shared -ffp-contract=off \
-		$(ROOT)/tests/native/wave_emu.cpp -x c++ $(CSRC)/mpc_structure.cpp -o $@
-
-# the same emulation with the twisted elimination of the default horizon (IMPC_TWIST, off in the
-# product): keeps that kernel path checked against the oracle
-$(EMUTW): $(ROOT)/tests/native/wave_emu.cpp $(CSRC)/mpc_wave.hpp $(CSRC)/admm_core.hpp $(CSRC)/mpc_structure.cpp \
-		$(CSRC)/mpc_structure.hpp
-	@mkdir -p $(HARNDIR)
-	$(HIPCC) -x hip --offload-host-only -std=c++20 -O2 -fPIC -shared -ffp-contract=off -DIMPC_TWIST=1 \
 		$(ROOT)/tests/native/wave_emu.cpp -x c++ $(CSRC)/mpc_structure.cpp -o $@
 
 # OsqpEigen shim driver (test-only Eigen stand-in; links the product library)

@@ -60,9 +60,6 @@ constexpr int kTile = 64;   // transpose tile edge
 #ifndef IMPC_VS
 #define IMPC_VS 1
 #endif
-#ifndef IMPC_DUPADD  // strided lane-grid sums: duplicated adds instead of copies before the swaps
-#define IMPC_DUPADD 1
-#endif
 #ifndef IMPC_WAVES_PER_SIMD
 #define IMPC_WAVES_PER_SIMD 2
 #endif
@@ -213,18 +210,8 @@ struct GpuTeam {
     double *red;  // >= NL/64 doubles of LDS
     __device__ int lane() const { return (int)threadIdx.x; }
     __device__ void sync() { __syncthreads(); }
-    // barrier for LDS-only exchanges: waits for this wave's LDS operations, not its global /
-    // scratch ones (register-spill stores are lane-private and need no wait at the barrier)
-    __device__ void lsync() {
-#if IMPC_LDSBAR
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0), vmcnt / expcnt left at their maxima
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-#else
-        __syncthreads();
-#endif
-    }
+    // barrier of the ADMM iteration's LDS exchanges (an LDS-only wait was measured slower)
+    __device__ void lsync() { __syncthreads(); }
     __device__ double bcast(double v, int src) {
         int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
         int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
@@ -259,21 +246,6 @@ struct GpuTeam {
         v = v + dpp<0x141>(v);  // row_half_mirror
         return v;
     }
-    // (x[low], x[high]) of the lane pair l, l ^ 16 (P16) or l, l ^ 32 (P32), gfx950 permlane swaps
-    template <bool P32>
-    __device__ static double pair_sum(double v) {
-        const int lo = __double2loint(v), hi = __double2hiint(v);
-        if (P32) {
-            auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-            auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-            return __hiloint2double(rh[0], rl[0]) + __hiloint2double(rh[1], rl[1]);
-        } else {
-            auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-            auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-            return __hiloint2double(rh[0], rl[0]) + __hiloint2double(rh[1], rl[1]);
-        }
-    }
-#if IMPC_DUPADD
     // x + y computed a second time into its own register, out of CSE's sight: the permlane swaps
     // need their operand in two registers, and a second add issued beside the first is off the
     // chain where a two-v_mov copy of the result was on it.  (The hazard recognizer pads the
@@ -296,22 +268,14 @@ struct GpuTeam {
         if (DUP) *dup = add_dup(x, y);
         return x + y;
     }
-#endif
     // sum over lanes {j, j+8, .., j+56}: row_ror 8 (xor 8), then xor 16 and xor 32 pair sums,
     // low + high in both partners: ((v0+v1)+(v2+v3)) + ((v4+v5)+(v6+v7)) over the 8 rows i
     __device__ double sum_stride8(double v) {
-#if IMPC_DUPADD
         const double d = dpp<0x128>(v);  // row_ror:8
         const double a = v + d, b = add_dup(v, d);
         double c2;
         const double c = pair_sum2<false, true>(a, b, &c2);
         return pair_sum2<true, false>(c, c2, nullptr);
-#else
-        v = v + dpp<0x128>(v);  // row_ror:8
-        v = pair_sum<false>(v);
-        v = pair_sum<true>(v);
-        return v;
-#endif
     }
     // lane l's value paired with lane l ^ 4 (ds_swizzle bit mode: and 0x1f, xor 4; no LDS access)
     __device__ static double xor4(double v) {
@@ -319,23 +283,12 @@ struct GpuTeam {
         const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), (4 << 10) | 0x1F);
         return __hiloint2double(hi, lo);
     }
+    // team maximum: the in-wave exchanges by DPP / permlane (max is order-independent), one LDS
+    // round across wavefronts
     __device__ double max(double v) {
-#if IMPC_DPPRED
         double mv[1] = {v};
-        max_n(mv);  // order-independent: the same value as the butterfly below
+        max_n(mv);
         return mv[0];
-#endif
-        for (int mask = 32; mask >= 1; mask >>= 1) {
-            double o = __shfl_xor(v, mask);
-            v = o > v ? o : v;
-        }
-        if (NL == 64) return v;
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-        __syncthreads();
-        double r = red[0];
-        for (int w = 1; w < NL / 64; w++) r = red[w] > r ? red[w] : r;
-        __syncthreads();
-        return r;
     }
     // K team maxima at once: DPP / permlane exchanges inside each wavefront (max is
     // order-independent, so any pairing that covers the wave will do), one LDS round across
@@ -435,14 +388,10 @@ struct GpuTeam {
         v = v + dpp<0xB1>(v);   // quad_perm [1,0,3,2] = lane ^ 1
         return v;
     }
+    // team sum: the in-wave xor butterfly (wave_sum, every lane bitwise the same), wavefronts
+    // added in order through LDS
     __device__ double sum(double v) {
-#if IMPC_DPPRED
-        // the same xor butterfly as below, its exchanges by permlane / DPP / swizzle instead of
-        // ds_bpermute: bitwise the same sum in every lane
         v = wave_sum(v);
-#else
-        for (int mask = 32; mask >= 1; mask >>= 1) v = v + __shfl_xor(v, mask);
-#endif
         v = bcast(v, 0);
         if (NL == 64) return v;
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
@@ -937,13 +886,10 @@ int launch_wave_w(impc_batch b, hipStream_t st, const impc::WaveIO &io, const ui
     HIP_OK(hipGetLastError());
     return IMPC_OK;
 }
-// the default-horizon instance (compile-time W) takes the batch: its W is the shape's WSPEC and,
-// for the one-variable-per-lane shape with the twisted elimination, the pattern qualifies for it
-// (MpcStructure::twist_ok)
+// the default-horizon instance (compile-time W) takes the batch when its W is the shape's WSPEC
 bool spec_ok(impc_batch b) {
     const int ws = b->vs == kWaveVS ? impc::WaveLds<kTeam, kWaveVS, 2>::WSPEC : impc::WaveLds<kTeam, kWaveVSLong, 2>::WSPEC;
-    const bool tw = b->vs == kWaveVS && impc::WaveLds<kTeam, kWaveVS, 2>::TW;
-    return b->ms->W == ws && (!tw || b->ms->twist_ok);
+    return b->ms->W == ws;
 }
 template <int VS, int GS>
 int launch_wave(impc_batch b, hipStream_t st, const impc::WaveIO &io, const uint32_t *ord) {
@@ -1159,7 +1105,7 @@ int prepare_structured(impc_batch b) {
     // per-QP HBM scratch for the scaling vectors: long-horizon shape only (the default shape keeps
     // them in LDS, mpc_wave.hpp WaveLds::ONCHIP)
     const size_t scal_bytes =
-        b->vs == kWaveVS && !IMPC_OFFCHIP_SCL ? 0 : sizeof(double) * (size_t)b->B * (size_t)(2 * s.n + s.mg);
+        b->vs == kWaveVS ? 0 : sizeof(double) * (size_t)b->B * (size_t)(2 * s.n + s.mg);
     if (scal_bytes) HIP_OK(hipMalloc((void **)&b->d_scal, scal_bytes));
     HIP_OK(hipMalloc((void **)&b->d_counter, 256));
     b->device_bytes += (int64_t)(scal_bytes + h.size() * 4 + 256);

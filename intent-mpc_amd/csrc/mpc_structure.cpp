@@ -112,30 +112,6 @@ std::string MpcStructure::analyse(int64_t n64, int64_t m64, const int64_t *Pp, c
         term_ptr[d + 1] = (int32_t)term.size();
     }
     if (term.empty()) term.push_back(0);
-    // twisted-elimination eligibility (mpc_structure.hpp twist_ok)
-    {
-        std::vector<int32_t> ups((size_t)n, 0);
-        bool ok = W > 2;
-        for (int32_t g = 0; g < mg && ok; g++) {
-            int32_t lo = 1 << 30, hi = -1, nhi = 0, cup = -1;
-            for (int e = 0; e < 4; e++) {
-                const int32_t c = gen_col[4 * g + e];
-                if (c < 0) continue;
-                lo = std::min(lo, c / 13);
-                hi = std::max(hi, c / 13);
-            }
-            if (hi < 0 || hi == lo) continue;
-            for (int e = 0; e < 4; e++) {
-                const int32_t c = gen_col[4 * g + e];
-                if (c >= 0 && c / 13 == hi) nhi++, cup = c;
-            }
-            ok = nhi == 1 && cup % 13 < 8;
-            if (ok) ups[(size_t)cup]++;
-        }
-        for (int32_t k = 1; k <= W && ok; k++)
-            for (int32_t i = 0; i < 8; i++) ok = ok && ups[(size_t)(13 * k + i)] == 1;
-        twist_ok = ok;
-    }
     return "";
 }
 

@@ -32,11 +32,6 @@ struct MpcStructure {
     int32_t HS = 0;
     std::vector<int32_t> col_hid;                                      // [n], -1 for light columns
     std::vector<int32_t> term_ptr, term;                               // factorisation assembly program
-    // Two-ended (twisted) elimination of the structured kernel (mpc_wave.hpp, IMPC_TWIST): every
-    // general row that couples stages k and k + 1 has exactly one entry in stage k + 1, on a state,
-    // and every state of stages 1 .. W is that entry of exactly one such row (the dynamics rows of
-    // mpcPlanner's QP).  Then the stage coupling B_k's row i is the single row's rho a_up a_(k, .).
-    bool twist_ok = false;
     // Returns "" when the pattern is stage-structured, else the reason it is not.
     std::string analyse(int64_t n, int64_t m, const int64_t *Pp, const int64_t *Pi, const int64_t *Ap,
                         const int64_t *Ai);

@@ -57,55 +57,18 @@ namespace impc {
 #endif
 #define IMPC_REP(X) for (int rep_ = 0; rep_ < (IMPC_DUP == (X) ? 2 : 1); rep_++)
 
-#ifndef IMPC_HWRW  // recursion wave from the waves' SIMD placement: +0.5-1 % (profiles/r02/exp/README.md,
-#define IMPC_HWRW 1  // profiles/r03/exp/README.md); re-validated on the GPU suite in round 3, on
-#endif
-#ifndef IMPC_NOCHUNK
-#define IMPC_NOCHUNK 1
-#endif
+// Variants measured slower and removed in round 4 (their numbers stay in profiles/r0*/exp/README.md,
+// their code in git history): the twisted two-ended elimination, pair-blocked and chunked stage
+// recursions, folded recursion subtractions, wave priorities, LDS-only barriers, register-held pair
+// captures, split dot-product chains, opaque phase bases, delta-less update instances, per-step
+// history / store captures, (c, S)-carried sweeps, off-chip scaling vectors, Cholesky / 1x1-pivot
+// stage inverses.  What is left is the measured-best form of each phase.
 
-#ifndef IMPC_LDSBAR  // LDS-only barriers inside the ADMM iteration (GpuTeam::lsync)
-#define IMPC_LDSBAR 0
-#endif
-#ifndef IMPC_PRIO  // raise the wave priority of the stage-recursion wavefront during its sweeps
-#define IMPC_PRIO 0
-#endif
-#ifndef IMPC_PRIO_INV  // the inverse: every wave at this priority, the recursion wavefront drops to 0
-#define IMPC_PRIO_INV 0  // during its sweeps (the parallel phases win the SIMD's issue arbitration)
-#endif
-#if IMPC_PRIO
-#define IMPC_PRIO_HI() __builtin_amdgcn_s_setprio(IMPC_PRIO)
-#define IMPC_PRIO_LO() __builtin_amdgcn_s_setprio(0)
-#elif IMPC_PRIO_INV && defined(__HIP_DEVICE_COMPILE__)
-#define IMPC_PRIO_HI() __builtin_amdgcn_s_setprio(0)
-#define IMPC_PRIO_LO() __builtin_amdgcn_s_setprio(IMPC_PRIO_INV)
-#else
-#define IMPC_PRIO_HI() ((void)0)
-#define IMPC_PRIO_LO() ((void)0)
-#endif
-#ifndef IMPC_RFOLD  // fold the recursion's subtraction into the first product (rstep): measured slower, off
-#define IMPC_RFOLD 0
-#endif
-#ifndef IMPC_PSTRIDE_PAD
-#define IMPC_PSTRIDE_PAD 1
-#endif
-#ifndef IMPC_TWIST  // twisted (two-ended) block elimination on the default horizon (WaveQP::TWIST):
-#define IMPC_TWIST 0  // built, parity green, measured slower (profiles/r03/exp/README.md), off
-#endif
-#ifndef IMPC_TWOPQ  // twisted chains: one address register per prefetch (no ds_read2 merging)
-#define IMPC_TWOPQ 0
-#endif
-#ifndef IMPC_PAIR  // pair-blocked stage recursions on the default horizon (WaveLds::PAIR): built,
-#define IMPC_PAIR 0  // measured slower (profiles/r02/exp/README.md), off
-#endif
 // Scheduling hint for the parallel phases' LDS reads: under the kernel's register pressure the
 // machine scheduler otherwise issues them one ds_read2 at a time, each followed by its own
 // lgkmcnt wait (S3 = 7 serialised LDS round trips); this asks for the phase's reads first, then
 // its arithmetic, so the round trips overlap.
-#ifndef IMPC_SGB
-#define IMPC_SGB 1
-#endif
-#if IMPC_SGB && defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
 #define IMPC_LOADS_FIRST(NR, NV)                            \
     do {                                                    \
         __builtin_amdgcn_sched_group_barrier(0x100, NR, 0); \
@@ -114,65 +77,6 @@ namespace impc {
 #else
 #define IMPC_LOADS_FIRST(NR, NV) ((void)0)
 #endif
-#ifndef IMPC_GJ  // stage inverses by Gauss-Jordan with 2x2 (2) or 1x1 (1) pivots, or Cholesky +
-#define IMPC_GJ 2  // L^-1 + L^-T L^-1 (0)
-#endif
-#ifndef IMPC_PCAP_REG  // pair sweeps: keep the stage results in registers until the sweep ends (1)
-#define IMPC_PCAP_REG 0  // or store each one as it is produced (0: measured faster, fewer spills)
-#endif
-// Round-3 iteration-latency experiments (tools/exp.sh, profiles/r03/exp/README.md "Branch-free
-// general rows and the other phase / sweep variants"): only IMPC_GFREE paid (-1.9..-2.2 % kernel
-// time, identical iterations) and is on; the rest were measured slower alone or beside it, off.
-#ifndef IMPC_GFREE  // general-row update / products without per-slot branches (the GS slots'
-#define IMPC_GFREE 1  // chains interleave; an empty slot computes zeros into the discard slot)
-#endif
-#ifndef IMPC_GUNROLL  // rhs column gather: the groups of a compile-time group count issued at once
-#define IMPC_GUNROLL 1  // (dispatch on CG4) instead of one LDS round trip per group of four (on, with
-#endif                  // IMPC_SDC: -1.3 %; measured neutral before the branch-free phases)
-#ifndef IMPC_TREE  // S1 / S3 / S5 / general-row dot products as two to four partial chains
-#define IMPC_TREE 0
-#endif
-#ifndef IMPC_PFREE  // rhs / S1 / S3 / S5 without the per-lane variable-kind branches (on: -0.6 %)
-#define IMPC_PFREE 1
-#endif
-#ifndef IMPC_DPPRED  // team max / sum (checks, infeasibility tests): the in-wave butterfly by DPP /
-#define IMPC_DPPRED 1  // permlane / swizzle exchanges instead of ds_bpermute (bitwise the same; on: -1.6 %)
-#endif
-#ifndef IMPC_CHKRED  // termination check: both infeasibility tests' first stages in one team reduction
-#define IMPC_CHKRED 1  // (bitwise the same values; on)
-#endif
-#ifndef IMPC_CMASK  // sweep captures selected by compile-time lane masks (SGPR constants; on: -0.3..-0.6 %)
-#define IMPC_CMASK 1
-#endif
-#ifndef IMPC_OBASE  // S1 / S3 / S5 reads from one opaque per-lane base with immediate offsets
-#define IMPC_OBASE 0  // (measured +1.3 %, off)
-#endif
-#ifndef IMPC_SDC  // default-horizon instances: the products stride as a compile-time constant, so
-#define IMPC_SDC 1  // the gather's reads take immediate offsets (on)
-#endif
-#ifndef IMPC_VMAX  // the iteration's projections by v_max_f64 / v_min_f64 instead of compare + selects
-#define IMPC_VMAX 1  // (on: -1.2 %; with PFREE -1.7 %)
-#endif
-#ifndef IMPC_LOOPC  // the inner loop counts to the pass's next event (check / rho update / max_iter)
-#define IMPC_LOOPC 1  // computed once per pass, instead of per-iteration countdown bookkeeping
-#endif
-#ifndef IMPC_NDT  // the check-iteration deltas: update phase instantiated with and without them
-#define IMPC_NDT 0
-#endif
-#ifndef IMPC_HCAP  // default-horizon sweeps: every step's output kept in its own register (no
-#define IMPC_HCAP 0  // per-step capture select), stored by one lane row / column after the sweep
-#endif
-#ifndef IMPC_SSTORE  // default-horizon sweeps: every stage result stored as produced by all lanes
-#define IMPC_SSTORE 0  // (same value, same address per output index) instead of register captures
-#endif
-#ifndef IMPC_SFOLD  // stage recursions carry (c, S) with a = c - S: the next product is
-#define IMPC_SFOLD 0  // fma(-f, S, f c), one dependent operation per step fewer
-#endif
-
-template <bool B>
-struct BoolC {
-    static constexpr bool value = B;
-};
 
 struct WaveTables {
     int32_t n, m, mg, N, W, CG, nnzP, nnzA;
@@ -257,44 +161,14 @@ struct WaveLds {
     static constexpr int RED_OFF = X_OFF + NP;              // team reduction scratch
     static constexpr int JUNK_OFF = RED_OFF + 64;           // per-lane discard slots [NL]
     static constexpr int GSLOT_OFF = JUNK_OFF + NL;         // int16 [4 NL GS]: general entry -> product slot
-    // Chunked stage recursions (default horizon of the one-variable-per-lane shape): the W + 1
-    // stages split into 4 chunks [S(c), S(c+1)), one per wavefront; the chunk-entry operators
-    // Psi_k (forward) / Phi_k (backward) and two cross-chunk products live here.
-    static constexpr bool CHUNK = VS == 1 && NL == 256 && !IMPC_NOCHUNK;
-    static IMPC_WF constexpr int S(int c) { return (c * (WSPEC + 1) + 2) / 4; }
-    static constexpr int NPF = WSPEC + 1 - S(1), NPB = S(3);   // Psi_k, k in [S1, W]; Phi_k, k in [0, S3)
-    static constexpr int PSI_OFF = GSLOT_OFF + NL * GS;     // [NPF + NPB + 2][64], row-major 8x8
-    static constexpr int PSI_N = CHUNK ? 64 * (NPF + NPB + 2) : 0;
     // One-variable-per-lane shape: the Ruiz scaling vectors D, E and the ADMM deltas of the
     // termination checks live here (the long-horizon shape keeps them in HBM / registers: its LDS
     // is full).  Layout of each: [var slots NMAX][box rows NMAX][general slots NL GS].
-#ifndef IMPC_OFFCHIP_SCL  // experiment: D, E in the per-QP HBM scratch and the deltas in registers also
-#define IMPC_OFFCHIP_SCL 0  // for the one-variable-per-lane shape (frees 2 x VEC_N doubles of LDS)
-#endif
-    static constexpr bool ONCHIP = VS == 1 && !IMPC_OFFCHIP_SCL;
+    static constexpr bool ONCHIP = VS == 1;
     static constexpr int VEC_N = 2 * NMAX + NL * GS;
-    // Pair-blocked stage recursions (default horizon of the one-variable-per-lane shape): the
-    // 8-dim recursions step over two stages at a time along the even stages, with the products
-    // H_k = F_{k+1} F_k and M_k = F_{k+1} G_k[:, 8:] (k = 0, 2, .., WSPEC - 3) formed by the
-    // factorisation; the odd stages come off the chain as independent side products.
-    static constexpr bool PAIR = VS == 1 && NL == 256 && IMPC_PAIR && !CHUNK;
-    static constexpr int NH = (WSPEC - 1) / 2;              // chain steps (9 at WSPEC = 19)
-    static_assert(!PAIR || (WSPEC & 1), "pair blocking needs an odd stage count");
-    static constexpr int H_OFF = PSI_OFF + PSI_N;           // [NH][64] H_k, recursion layout
-    static constexpr int M_OFF = H_OFF + (PAIR ? 64 * NH : 0);  // [NH][40] M_k, row-major 8 x 5
-    static constexpr int SCL_OFF = M_OFF + (PAIR ? 40 * NH : 0);  // D, E (scaling)
+    static constexpr int SCL_OFF = GSLOT_OFF + NL * GS;           // D, E (scaling)
     static constexpr int DLT_OFF = SCL_OFF + (ONCHIP ? VEC_N : 0);  // dx, dy (check iterations)
-    // Twisted (two-ended) elimination of the default horizon (IMPC_TWIST, WaveQP::TWIST): the middle
-    // stage's state lanes' G_{KM-1}[:, 8:] rows ([8][5]; their cp registers hold Abar^-1 Bbar' rows)
-    static constexpr bool TW = VS == 1 && NL == 256 && IMPC_TWIST && !CHUNK && !PAIR;
-    static constexpr int MID_OFF = DLT_OFF + (ONCHIP ? VEC_N : 0);
-    // ... and the coupling-row table (int32 per general-row slot: (upper entry << 16) | upper
-    // column for rows coupling stages k, k + 1 > KM, else -1), set per batch by load_tables
-    static constexpr int CPL_OFF = MID_OFF + (TW ? 40 : 0);
-    static constexpr int P_OFF = CPL_OFF + (TW ? NL * GS / 2 : 0);  // products, column-slot layout (size below)
-    // chunk-boundary exchange of the recursions (inside the team reduction scratch, past red[0..3])
-    static constexpr int XF_OFF = RED_OFF + 8;              // forward: a^_{S(c+1)-1}, c = 0..2
-    static constexpr int XB_OFF = RED_OFF + 32;             // backward: x^_{S(c)}, c = 1..3
+    static constexpr int P_OFF = DLT_OFF + (ONCHIP ? VEC_N : 0);    // products, column-slot layout (size below)
     static constexpr int CGM = 24;                          // max general entries per column
     // products region: entry t < T1r of column v at t * stride(n) + v (stride = n rounded up to
     // 64, plus a pad), so a column's gather is independent, conflict-free reads.  When that one
@@ -310,7 +184,7 @@ struct WaveLds {
     // +PAD: the obstacle rows of one stage write their products to the same column in different
     // entry slots; a stride that is not a multiple of 16 doubles puts those ds_write_b64 (bank =
     // dword mod 32, 16-lane groups) on distinct banks.  Reads stay lane-contiguous.
-    static constexpr IMPC_WF int stride(int n) { return ((n + 63) & ~63) + IMPC_PSTRIDE_PAD; }
+    static constexpr IMPC_WF int stride(int n) { return ((n + 63) & ~63) + 1; }
     // the factorisation uses it as (4g + e) scratch followed by the general rows' rho (RHOG_P)
     static IMPC_WF int hsp(int HS) { return HS + 1; }  // second-tier row length
     static IMPC_WF int p_size(int CG, int n, int HS, int mg, int T1r) {
@@ -322,10 +196,8 @@ struct WaveLds {
     // factorisation aliases (inside R..X region and the products buffer)
     static constexpr int FA = R_OFF, FL = FA + 169, FI = FL + 169, FB = FI + 169, FG = FB + 104, FE = FG + 104,
                          DIAGX = FE + 64;
-    // twisted elimination: Acheck_{k+1}^{-1}[:8, :8] of the stage eliminated last from the bottom
-    static constexpr int FEB = DIAGX + NMAX;
     // general rows' rho during the factorisation: products region + 4 mg
-    static_assert(FEB + 64 <= RED_OFF, "factorisation scratch does not fit");
+    static_assert(DIAGX + NMAX <= RED_OFF, "factorisation scratch does not fit");
 };
 
 struct WaveRho {
@@ -394,17 +266,6 @@ struct WaveQP {
     WaveRho R;
     double c = 1.0, cinv = 1.0;
     int rw = 0;  // the wavefront that runs the stage recursions for this QP
-    // Twisted (two-ended) block elimination, default horizon of the one-variable-per-lane shape:
-    // stages 0 .. KM-1 are eliminated top-down (the Schur complements Ahat_k, F_k as in the
-    // one-ended scheme), stages W .. KM+1 bottom-up (Acheck_k = M_kk - Bbar_k' Acheck_{k+1}^-1[:8,:8]
-    // Bbar_k, H_k = (Acheck_k^-1 Bbar_k')[:8, :]), and the middle stage KM takes both
-    // (Abar = M - E_{KM-1} - Bbar_KM' Acheck_{KM+1}^-1[:8,:8] Bbar_KM).  Each solve then runs its
-    // 8-dim recursions as two concurrent chains of (W - 1) / 2 steps on two wavefronts -- top-down
-    // and bottom-up, then outward from the middle -- instead of one chain of W steps.
-    static constexpr bool TWIST = LD::TW && WF == LD::WSPEC;
-    static constexpr int KM = (LD::WSPEC - 1) / 2;
-    // (the coupling-row table lives in LDS, WaveLds::CPL_OFF: kept in registers it was spilled and
-    // reloaded from scratch every iteration)
     // settings / pattern scalars the ADMM iteration reads, held in registers (a grouped launch's
     // tables and settings live in global memory: read in the loop, each is a scalar-memory round
     // trip after every barrier)
@@ -427,15 +288,6 @@ struct WaveQP {
         asm volatile("" : "+v"(l));
 #endif
         return l;
-    }
-
-    // IMPC_OBASE: a phase's per-lane LDS base formed as one opaque offset, so its reads take
-    // immediate offsets (a ds_read2 offset reaches 255 doubles) instead of one address add each
-    IMPC_WF const double *lds_at(int off) const {
-#if IMPC_OBASE
-        opaque(off);
-#endif
-        return lds + off;
     }
 
     // a per-lane value the optimiser must treat as freshly computed (see lane_o)
@@ -503,11 +355,9 @@ struct WaveQP {
             hid_[s] = TIER && vok[s] ? T.col_hid[v] : -1;  // second products tier (TIER batches)
             x[s] = q[s] = pd[s] = ab[s] = zb[s] = yb[s] = lb[s] = ub[s] = dxv_[s] = dyb_[s] = 0.0;
             bt[s] = 0;
-#if IMPC_PFREE
             // the branch-free phases read a slot's factor rows whether or not it holds a variable
             _Pragma("unroll") for (int cc = 0; cc < 13; cc++) ainv[s][cc] = 0.0;
             _Pragma("unroll") for (int cc = 0; cc < 8; cc++) cp[s][cc] = 0.0;
-#endif
             if (vok[s]) {
                 int ov = T.var_orig[v];
                 q[s] = io.q[bn + ov];
@@ -559,22 +409,6 @@ struct WaveQP {
         double *pb = lds + LD::P_OFF;
         for (int e = w.lane(); e < pz + 8; e += NL) pb[e] = 0.0;
         w.sync();
-        if constexpr (TWIST) {
-            // coupling rows: entries in stages k and k + 1 > KM, one of them in stage k + 1
-            // (MpcStructure::twist_ok, checked on the host) -- the upper entry, last in column order
-            int32_t *cpl = (int32_t *)(lds + LD::CPL_OFF);
-            for (int g = w.lane(); g < NL * GS; g += NL) {
-                int hi = -1, lo = 1 << 30, eu = 0, cu = 0;
-                for (int e = 0; e < 4 && g < T.mg; e++) {
-                    const int c = T.gen_col[4 * g + e];
-                    if (c < 0) continue;
-                    const int st_ = c / 13;
-                    if (st_ > hi) hi = st_, eu = e, cu = c;
-                    lo = st_ < lo ? st_ : lo;
-                }
-                cpl[g] = g < T.mg && hi == lo + 1 && hi > KM ? (eu << 16) | cu : -1;
-            }
-        }
         for (int e = w.lane(); e < T.n * T.CG; e += NL) {
             const int v = e / T.CG, t = e % T.CG, id = T.colg[e];
             if (id >= 0)
@@ -610,13 +444,12 @@ struct WaveQP {
     // column, h = its second-tier index (hid_, -1 for a light column) -- the second tier
     IMPC_WF double col_gather(int v, int h) {
         const double *pb = pbuf() + v;
-        // (IMPC_SDC: the compile-time horizon's products stride, n = 13 (WF + 1) - 5, so the gather's
-        // reads take immediate offsets instead of per-read address arithmetic)
-        const int C4 = c4_, sd = (IMPC_SDC && WF) ? LD::stride(13 * (WF + 1) - 5) : sd_;
+        // (a compile-time horizon's products stride is a constant, n = 13 (WF + 1) - 5, so the
+        // gather's reads take immediate offsets instead of per-read address arithmetic)
+        const int C4 = c4_, sd = WF ? LD::stride(13 * (WF + 1) - 5) : sd_;
         double s = 0.0;
         if constexpr (!TIER) {
             (void)h;
-#if IMPC_GUNROLL
             // the same sum, every read of the column issued before the first add (C4 is uniform)
             switch (C4) {
                 case 4: return gather_n<1>(pb, sd);
@@ -626,7 +459,6 @@ struct WaveQP {
                 case 20: return gather_n<5>(pb, sd);
                 default: break;
             }
-#endif
             for (int t = 0; t < C4; t += 4) {
                 const double p0 = pb[t * sd], p1 = pb[(t + 1) * sd], p2 = pb[(t + 2) * sd], p3 = pb[(t + 3) * sd];
                 s += (p0 + p1) + (p2 + p3);
@@ -764,10 +596,8 @@ struct WaveQP {
     // ------------------------------------------------------------ block factorisation
     // Returns 1 if a pivot is not positive (OSQP_NONCVX_ERROR).
     IMPC_WF int factorize() {
-        if constexpr (TWIST) return factorize_tw();
         const int n = T.n, W = Wst(), N = W + 1;
         double *w = pbuf(), *rhog = pbuf() + 4 * T.mg, *diagx = lds + LD::DIAGX;
-        const bool pair = LD::PAIR && W == LD::WSPEC;
         double *A = lds + LD::FA, *Li = lds + LD::FL, *Ai = lds + LD::FI, *Bb = lds + LD::FB, *G = lds + LD::FG,
                *E = lds + LD::FE, *Fm = F();
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
@@ -803,9 +633,7 @@ struct WaveQP {
                         val += rhog[g] * w[4 * g + e] * w[4 * g + f];
                     }
                     if (!isB && r == cc) val += diagx[13 * k + r];
-#if IMPC_GJ
                     if (!isB && k > 0 && r < 8 && cc < 8) val -= E[8 * r + cc];  // Schur complement
-#endif
                 }
                 if (isB)
                     Bb[dd] = val;
@@ -814,7 +642,6 @@ struct WaveQP {
             }
             wv.sync();
             IMPC_SEC(kSecFAsm);
-#if IMPC_GJ
             // Ahat_k^{-1} by Gauss-Jordan elimination: one element per lane, the pivots in order
             // (SPD, no pivoting needed; a non-positive-definite pivot flags the factorisation as
             // failed, as a failed Cholesky did), ping-pong between two LDS buffers so every step
@@ -824,7 +651,6 @@ struct WaveQP {
                 double *src = A, *dst = Li;
                 const int gi = L / 13, gc = L % 13;
                 const bool act = L < 169 && gi < sz && gc < sz;
-#if IMPC_GJ == 2
                 // two pivots per step (2x2 block pivot Q = P^-1, P = S[J][J], J = {j, j+1}):
                 //   D[J][J] = Q, D[J][c] = Q S[J][c], D[i][J] = -S[i][J] Q,
                 //   D[i][c] = S[i][c] - (S[i][J] Q) S[J][c]; a non-PD pivot block flags failure
@@ -875,84 +701,7 @@ struct WaveQP {
                     src = dst;
                     dst = t;
                 }
-#else
-                for (int j = 0; j < sz; j++) {
-                    const bool last = j == sz - 1;
-                    if (act) {
-                        const int i = last && gc > gi ? gc : gi, c = last && gc > gi ? gi : gc;
-                        const double p = src[13 * j + j];
-                        if (!(p > 0.0)) bad = 1;
-                        const double r = 1.0 / p;
-                        double v;
-                        if (i == j && c == j)
-                            v = r;
-                        else if (i == j)
-                            v = src[13 * j + c] * r;
-                        else if (c == j)
-                            v = -(src[13 * i + j] * r);
-                        else
-                            v = src[13 * i + c] - (src[13 * i + j] * r) * src[13 * j + c];
-                        (last ? Ai : dst)[13 * gi + gc] = v;
-                    }
-                    wv.sync();
-                    double *t = src;
-                    src = dst;
-                    dst = t;
-                }
-#endif
             }
-#else
-            if (k > 0) {
-                if (L < 64) {
-                    int i = L >> 3, j = L & 7;
-                    A[13 * i + j] -= E[8 * i + j];
-                }
-                wv.sync();
-            }
-            // Cholesky of A (sz x sz, stride 13)
-            for (int j = 0; j < sz; j++) {
-                if (L == 0) {
-                    double dj = A[13 * j + j];
-                    if (!(dj > 0.0)) bad = 1;
-                    A[13 * j + j] = sqrt(dj);
-                }
-                wv.sync();
-                if (L > j && L < sz) A[13 * L + j] /= A[13 * j + j];
-                wv.sync();
-                const int rem = sz - 1 - j, cnt = rem * (rem + 1) / 2;
-                for (int p = L; p < cnt; p += NL) {
-                    // p -> (i, cc) with j < cc <= i < sz, row-major over i
-                    int i = j + 1, off = p;
-                    while (off >= i - j) {
-                        off -= i - j;
-                        i++;
-                    }
-                    int cc = j + 1 + off;
-                    A[13 * i + cc] -= A[13 * i + j] * A[13 * cc + j];
-                }
-                wv.sync();
-            }
-            // Linv column by column (lane = column)
-            if (L < sz) {
-                const int cc = L;
-                Li[13 * cc + cc] = 1.0 / A[13 * cc + cc];
-                for (int i = cc + 1; i < sz; i++) {
-                    double s = 0.0;
-                    for (int t = cc; t < i; t++) s += A[13 * i + t] * Li[13 * t + cc];
-                    Li[13 * i + cc] = -s / A[13 * i + i];
-                }
-            }
-            wv.sync();
-            // Ainv = Linv' Linv
-            for (int p = L; p < sz * sz; p += NL) {
-                int r = p / sz, cc = p % sz;
-                int t0 = r > cc ? r : cc;
-                double s = 0.0;
-                for (int t = t0; t < sz; t++) s += Li[13 * t + r] * Li[13 * t + cc];
-                Ai[13 * r + cc] = s;
-            }
-            wv.sync();
-#endif
             _Pragma("unroll") for (int s = 0; s < VS; s++)
                 if (vok[s] && vs_[s] == k)
                     _Pragma("unroll") for (int cc = 0; cc < 13; cc++) ainv[s][cc] = cc < sz ? Ai[13 * vr_[s] + cc] : 0.0;
@@ -970,13 +719,8 @@ struct WaveQP {
                     for (int t = 0; t < 13; t++) s += G[13 * i + t] * Bb[13 * j + t];
                     E[8 * i + j] = s;
                     // recursion layout: lane (i,j) of step k reads F_k[j][i] when the column index
-                    // sits on i (k even, or pair_col_i(k) when pair-blocked), F_k[i][j] otherwise
-                    const bool ci = pair ? pair_col_i(k) : !(k & 1);
-                    Fm[64 * k + 8 * i + j] = ci ? G[13 * j + i] : G[13 * i + j];
-                } else if (pair && L < 104 && !(k & 1) && k < 2 * LD::NH) {
-                    // G_k[:, 8:] of the even stages, for M_k = F_{k+1} G_k[:, 8:] once F_{k+1} exists
-                    const int p = L - 64, q = p / 5, cc = p % 5;
-                    lds[LD::M_OFF + 40 * (k >> 1) + p] = G[13 * q + 8 + cc];
+                    // sits on i (k even), F_k[i][j] otherwise
+                    Fm[64 * k + 8 * i + j] = !(k & 1) ? G[13 * j + i] : G[13 * i + j];
                 }
                 _Pragma("unroll") for (int s = 0; s < VS; s++) {
                     if (!vok[s]) continue;
@@ -992,10 +736,6 @@ struct WaveQP {
         _Pragma("unroll") for (int s = 0; s < VS; s++)
             if (vok[s] && vs_[s] == 0 && vr_[s] < 8)
                 _Pragma("unroll") for (int j = 0; j < 8; j++) cp[s][j] = 0.0;
-        if constexpr (LD::CHUNK)
-            if (W == LD::WSPEC) chunk_operators();
-        if constexpr (LD::PAIR)
-            if (pair) pair_operators();
         bad = (int)wv.max((double)bad);  // set by lane 0 only: team-wide, so every wavefront agrees
         clear_exchange();
         zero_products();  // the (4g + e) factorisation scratch shared the products region
@@ -1003,427 +743,12 @@ struct WaveQP {
         return bad;
     }
 
-    // ---------------------------------------------------- pair-blocked stage recursions
-    // Forward: a_{k+1} = t_{k+1} - F_k a_k.  Over two stages, a_{k+2} = u_{k+2} + H_k a_k with
-    // u_{k+2} = t_{k+2} - F_{k+1} t_{k+1} (formed in S1) and H_k = F_{k+1} F_k, so the dependent
-    // chain runs over the even stages (a_0 -> a_2 -> .. -> a_{W-1}: (W - 1) / 2 steps) and each step
-    // also yields the odd stage a_{k+1} = t_{k+1} - F_k a_k from the same input: an independent
-    // second reduction that fills the chain's latency.  Backward likewise: x_k = v_k + H_k' x_{k+2}
-    // with v_k = e_k - F_k' e_{k+1} (the V phase) and the side x_{k+1} = e_{k+1} - F_{k+1}' x_{k+2}.
-    // Layout: the vector of even stage k = 2c sits at index i when c is even (j when odd); the
-    // matrices of stages k and k + 1 are stored with their column index on that index
-    // (pair_col_i), so every step reduces over its input's index and lands on the other one.
-    static IMPC_WF constexpr bool pair_col_i(int k) { return ((k >> 1) & 1) == 0; }
-    // F_k[r][c] in the pair layout
-    IMPC_WF double Fp(int k, int r, int c) const {
-        return pair_col_i(k) ? lds[LD::F_OFF + 64 * k + 8 * c + r] : lds[LD::F_OFF + 64 * k + 8 * r + c];
-    }
-
-    // H_k = F_{k+1} F_k (in the layout of step k) and M_k = F_{k+1} G_k[:, 8:] (row-major; the M
-    // slots hold G_k[:, 8:] until here), k = 0, 2, .., 2 (NH - 1)
-    IMPC_WF void pair_operators() {
-        wv.sync();
-        double *Hm = lds + LD::H_OFF, *Mm = lds + LD::M_OFF;
-        for (int p = L; p < 64 * LD::NH; p += NL) {
-            const int c = p >> 6, e = p & 63, k = 2 * c, i = e >> 3, j = e & 7;
-            const int r = pair_col_i(k) ? j : i, col = pair_col_i(k) ? i : j;
-            double a = 0.0;
-            for (int q = 0; q < 8; q++) a += Fp(k + 1, r, q) * Fp(k, q, col);
-            Hm[p] = a;
-        }
-        constexpr int NM = 40 * LD::NH, MR = (NM + NL - 1) / NL;
-        double mv[MR];
-        _Pragma("unroll") for (int t = 0; t < MR; t++) {
-            const int p = L + NL * t;
-            double a = 0.0;
-            if (p < NM) {
-                const int c = p / 40, e = p % 40, r = e / 5, cc = e % 5;
-                for (int q = 0; q < 8; q++) a += Fp(2 * c + 1, r, q) * Mm[40 * c + 5 * q + cc];
-            }
-            mv[t] = a;
-        }
-        wv.sync();
-        _Pragma("unroll") for (int t = 0; t < MR; t++)
-            if (L + NL * t < NM) Mm[L + NL * t] = mv[t];
-        wv.sync();
-    }
-
-    // Stage s's value r sits in the 8 lanes that share its index.  IMPC_PCAP_REG = 0: the lane
-    // whose other index is 0 stores it to buf right away (the others to their discard slot).
-    // IMPC_PCAP_REG = 1: the lane whose other index is s mod 8 keeps it in slot s / 8 of the array
-    // for values on index i (ci) or j (cj) and pcap_store writes them after the sweep (no LDS
-    // store per step, but 6 more live doubles: measured slower through register spills).
-    static constexpr int PQ = (LD::WSPEC + 8) / 8;
-    template <bool OUT_I>
-    IMPC_WF void pcap(double (&ci)[PQ], double (&cj)[PQ], double r, int s, int i, int j, double *buf, double *junk) {
-#if IMPC_PCAP_REG
-        (void)buf, (void)junk;
-        if (OUT_I) {
-            if (j == (s & 7)) ci[s >> 3] = r;
-        } else {
-            if (i == (s & 7)) cj[s >> 3] = r;
-        }
-#else
-        (void)ci, (void)cj;
-        if (OUT_I)
-            *(j == 0 ? buf + 13 * s + i : junk) = r;
-        else
-            *(i == 0 ? buf + 13 * s + j : junk) = r;
-#endif
-    }
-    // store the captured stages s0 .. s1 (stage s at 13 s + its index; out_i(s): on index i)
-    template <class OUTI>
-    IMPC_WF void pcap_store(const double (&ci)[PQ], const double (&cj)[PQ], double *buf, int s0, int s1, int i,
-                            int j, OUTI out_i) {
-        if (!IMPC_PCAP_REG) return;
-        double *junk = lds + LD::JUNK_OFF + lane_o();
-        _Pragma("unroll") for (int q = 0; q < PQ; q++) {
-            const int si = 8 * q + j, sj = 8 * q + i;
-            *((si >= s0 && si <= s1 && out_i(si)) ? buf + 13 * si + i : junk) = ci[q];
-            *((sj >= s0 && sj <= s1 && !out_i(sj)) ? buf + 13 * sj + j : junk) = cj[q];
-        }
-    }
-
-    // S2, pair-blocked (W = WSPEC): from a_0 = t_0 (index i), stages 1 .. W into rb; tb holds
-    // u_k on the even stages k >= 2 (S1).  Operands are loaded two steps ahead.
-    IMPC_WF void fwd_pair(const double *tb, double *rb) {
-        constexpr int NH = LD::NH, W = LD::WSPEC;
-        constexpr bool last_on_i = (NH & 1) == 0;  // input index of the final side step
-        const double *Fm = F(), *Hm = lds + LD::H_OFF;
-        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;
-        double *junk = lds + LD::JUNK_OFF + lo;
-        double ci[PQ], cj[PQ];
-        if (IMPC_PCAP_REG) _Pragma("unroll") for (int q = 0; q < PQ; q++) ci[q] = cj[q] = 0.0;
-        double a = tb[i];
-        // operands of step c: H_{2c}, F_{2c}, u_{2c+2}, t_{2c+1} (u, t on the step's output index);
-        // step NH is the final side step (F_{W-1}, t_W)
-        auto ld = [&](int c, double &h, double &f, double &u, double &t) {
-            const int k = 2 * c, xo = (c & 1) == 0 ? j : i;
-            if (c < NH) {
-                h = Hm[64 * c + l];
-                f = Fm[64 * k + l];
-                u = tb[13 * (k + 2) + xo];
-                t = tb[13 * (k + 1) + xo];
-            } else if (c == NH) {
-                f = Fm[64 * (W - 1) + l];
-                t = tb[13 * W + xo];
-            }
-        };
-        double h0 = 0, f0 = 0, u0 = 0, t0 = 0, h1 = 0, f1 = 0, u1 = 0, t1 = 0;
-        ld(0, h0, f0, u0, t0);
-        ld(1, h1, f1, u1, t1);
-        _Pragma("unroll") for (int c = 0; c < NH; c++) {
-            const int k = 2 * c;
-            const bool on_i = (c & 1) == 0;  // this step's input index (its outputs: the other)
-            const double h = h0, f = f0, u = u0, t = t0;
-            h0 = h1, f0 = f1, u0 = u1, t0 = t1;
-            ld(c + 2, h1, f1, u1, t1);
-            const double pc = prod_nc(h, a), ps = prod_nc(f, a);
-            double rc, rs;
-            if (on_i) {
-                rc = wv.sum_stride8(pc);
-                rs = wv.sum_stride8(ps);
-            } else {
-                rc = wv.sum_contig8(pc);
-                rs = wv.sum_contig8(ps);
-            }
-            const double as = t - rs;  // a_{k+1}
-            a = u + rc;                // a_{k+2}
-            if (on_i) {
-                pcap<false>(ci, cj, as, k + 1, i, j, rb, junk);
-                pcap<false>(ci, cj, a, k + 2, i, j, rb, junk);
-            } else {
-                pcap<true>(ci, cj, as, k + 1, i, j, rb, junk);
-                pcap<true>(ci, cj, a, k + 2, i, j, rb, junk);
-            }
-        }
-        const double ps = prod_nc(f0, a);
-        const double aw = t0 - (last_on_i ? wv.sum_stride8(ps) : wv.sum_contig8(ps));
-        pcap<!last_on_i>(ci, cj, aw, W, i, j, rb, junk);
-        pcap_store(ci, cj, rb, 1, W, i, j, [](int s) { return s == W ? !last_on_i : (((s - 1) >> 1) & 1) == 1; });
-    }
-
-    // S4, pair-blocked (W = WSPEC): from x_W = e_W, stages W-1 .. 0 into xb; eb holds v_k on the
-    // even stages k <= W - 3 (V phase).  Operands are loaded two steps ahead.
-    IMPC_WF void bwd_pair(const double *eb, double *xb) {
-        constexpr int NH = LD::NH, W = LD::WSPEC;
-        constexpr bool last_on_i = (NH & 1) == 0;  // x_{W-1} sits on index i (else j)
-        const double *Fm = F(), *Hm = lds + LD::H_OFF;
-        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;
-        double *junk = lds + LD::JUNK_OFF + lo;
-        double ci[PQ], cj[PQ];
-        if (IMPC_PCAP_REG) _Pragma("unroll") for (int q = 0; q < PQ; q++) ci[q] = cj[q] = 0.0;
-        // operands of step c (x_{2c+2} -> x_{2c}, x_{2c+1}): H_{2c}, F_{2c+1}, v_{2c}, e_{2c+1}, on
-        // the step's output index (i for even c)
-        auto ld = [&](int c, double &h, double &f, double &v, double &e) {
-            if (c < 0) return;
-            const int xo = (c & 1) == 0 ? i : j;
-            h = Hm[64 * c + l];
-            f = Fm[64 * (2 * c + 1) + l];
-            v = eb[13 * (2 * c) + xo];
-            e = eb[13 * (2 * c + 1) + xo];
-        };
-        double h0 = 0, f0 = 0, v0 = 0, e0 = 0, h1 = 0, f1 = 0, v1 = 0, e1 = 0;
-        ld(NH - 1, h0, f0, v0, e0);
-        ld(NH - 2, h1, f1, v1, e1);
-        // x_{W-1} = e_{W-1} - F_{W-1}' x_W, reduced over x_W's index
-        double x;
-        {
-            const double xW = eb[13 * W + (last_on_i ? j : i)], ew = eb[13 * (W - 1) + (last_on_i ? i : j)];
-            const double p = prod_nc(Fm[64 * (W - 1) + l], xW);
-            x = ew - (last_on_i ? wv.sum_contig8(p) : wv.sum_stride8(p));
-            pcap<last_on_i>(ci, cj, x, W - 1, i, j, xb, junk);
-        }
-        _Pragma("unroll") for (int c = NH - 1; c >= 0; c--) {
-            const bool out_i = (c & 1) == 0;
-            const double h = h0, f = f0, v = v0, e = e0;
-            h0 = h1, f0 = f1, v0 = v1, e0 = e1;
-            ld(c - 2, h1, f1, v1, e1);
-            const double pc = prod_nc(h, x), ps = prod_nc(f, x);
-            double rc, rs;
-            if (out_i) {  // input on index j
-                rc = wv.sum_contig8(pc);
-                rs = wv.sum_contig8(ps);
-            } else {
-                rc = wv.sum_stride8(pc);
-                rs = wv.sum_stride8(ps);
-            }
-            const double xs = e - rs;  // x_{2c+1}
-            x = v + rc;                // x_{2c}
-            if (out_i) {
-                pcap<true>(ci, cj, xs, 2 * c + 1, i, j, xb, junk);
-                pcap<true>(ci, cj, x, 2 * c, i, j, xb, junk);
-            } else {
-                pcap<false>(ci, cj, xs, 2 * c + 1, i, j, xb, junk);
-                pcap<false>(ci, cj, x, 2 * c, i, j, xb, junk);
-            }
-        }
-        pcap_store(ci, cj, xb, 0, W - 1, i, j, [](int s) { return s == W - 1 ? last_on_i : ((s >> 1) & 1) == 0; });
-    }
-
-    // ------------------------------------------------------- chunked stage recursions
-    // The forward recursion a_{k+1} = t_{k+1} - F_k a_k is linear in the chunk's entry value: for a
-    // chunk [S, E] entered from a_{S-1}, a_k = a^_k + Psi_k a_{S-1} with a^ the recursion started
-    // from a^_S = t_S, Psi_S = -F_{S-1}, Psi_{k+1} = -F_k Psi_k.  Likewise backward, x_k = x^_k +
-    // Phi_k x_{E+1} with x^_E = e_E, Phi_E = -F_E', Phi_k = -F_k' Phi_{k+1}.  Each wavefront runs
-    // its chunk's local recursion (phase A, S(c+1) - S(c) - 1 dependent steps), the boundary values
-    // meet in LDS, then every wavefront forms its entry value from the earlier chunks' boundary
-    // values (at most two independent 8x8 products, with the precomputed Psi_{S3-1} Psi_{S2-1} /
-    // Phi_{S1} Phi_{S2}) and corrects its stages with independent 8x8 products (phase B).  The
-    // dependent chain drops from W steps to 4 + 2.  Psi / Phi depend only on the factorisation.
-    IMPC_WF static double Fget(const double *Fm, int k, int r, int c) {  // F_k[r][c] (parity layout)
-        return (k & 1) ? Fm[64 * k + 8 * r + c] : Fm[64 * k + 8 * c + r];
-    }
-    IMPC_WF double *PF(int k) { return lds + LD::PSI_OFF + 64 * (k - LD::S(1)); }  // Psi_k, row-major
-    IMPC_WF double *PB(int k) { return lds + LD::PSI_OFF + 64 * (LD::NPF + k); }   // Phi_k
-    IMPC_WF double *PIF() { return lds + LD::PSI_OFF + 64 * (LD::NPF + LD::NPB); }
-    IMPC_WF double *PIB() { return PIF() + 64; }
-
-    IMPC_WF void chunk_operators() {
-        const double *Fm = F();
-        constexpr int CL = LD::S(4) - LD::S(3) > LD::S(1) ? LD::S(4) - LD::S(3) : LD::S(1);
-        static_assert(LD::S(2) - LD::S(1) <= CL && LD::S(3) - LD::S(2) <= CL, "chunk length");
-        for (int st = 0; st < CL; st++) {
-            for (int p = L; p < 6 * 64; p += NL) {
-                const int mtx = p >> 6, e = p & 63, r = e >> 3, cc = e & 7;
-                if (mtx < 3) {  // Psi_k of chunk c = mtx + 1
-                    const int c = mtx + 1, k = LD::S(c) + st;
-                    if (k >= LD::S(c + 1)) continue;
-                    double v;
-                    if (st == 0) {
-                        v = -Fget(Fm, k - 1, r, cc);
-                    } else {
-                        const double *Pp = PF(k - 1);
-                        double a = 0.0;
-                        for (int q = 0; q < 8; q++) a += Fget(Fm, k - 1, r, q) * Pp[8 * q + cc];
-                        v = -a;
-                    }
-                    PF(k)[e] = v;
-                } else {  // Phi_k of chunk c = mtx - 3
-                    const int c = mtx - 3, k = LD::S(c + 1) - 1 - st;
-                    if (k < LD::S(c)) continue;
-                    double v;
-                    if (st == 0) {
-                        v = -Fget(Fm, k, cc, r);
-                    } else {
-                        const double *Pn = PB(k + 1);
-                        double a = 0.0;
-                        for (int q = 0; q < 8; q++) a += Fget(Fm, k, q, r) * Pn[8 * q + cc];
-                        v = -a;
-                    }
-                    PB(k)[e] = v;
-                }
-            }
-            wv.sync();
-        }
-        for (int p = L; p < 128; p += NL) {
-            const int e = p & 63, r = e >> 3, cc = e & 7;
-            const double *X = p < 64 ? PF(LD::S(3) - 1) : PB(LD::S(1));
-            const double *Y = p < 64 ? PF(LD::S(2) - 1) : PB(LD::S(2));
-            double a = 0.0;
-            for (int q = 0; q < 8; q++) a += X[8 * r + q] * Y[8 * q + cc];
-            (p < 64 ? PIF() : PIB())[e] = a;
-        }
-        wv.sync();
-    }
-
-    // y = M v on the wavefront's 8x8 grid (M row-major in LDS): v at index i -> y at index j
-    // (l: the lane within the wavefront, formed once by the caller)
-    IMPC_WF double mv_i(const double *M, double v, int l) {
-        return wv.sum_stride8(prod_nc(M[8 * (l & 7) + (l >> 3)], v));
-    }
-    // v at index j -> y at index i
-    IMPC_WF double mv_j(const double *M, double v, int l) { return wv.sum_contig8(prod_nc(M[l], v)); }
-
-    // Phase A forward, chunk [K0, K1): a^_{K0} = t_{K0}; stores a^_k, K0 < k < K1, to rb and
-    // a^_{K1-1} to xo (XO).  Stage k's vector sits at index i (k even) / j (k odd).
-    template <int K0, int K1, bool XO>
-    IMPC_WF void fwd_chunk(const double *tb, double *rb, double *xo) {
-        const double *Fm = F();
-        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;
-        double *junk = lds + LD::JUNK_OFF + lo;
-        constexpr int NS = K1 - 1 - K0;
-        double a = tb[13 * K0 + ((K0 & 1) ? j : i)];
-        double cs = 0.0, cc = 0.0;  // step m kept by lane i == m (strided steps) / j == m (contiguous)
-        _Pragma("unroll") for (int k = K0; k < K1 - 1; k++) {
-            const double f = Fm[64 * k + l], t = tb[13 * (k + 1) + ((k & 1) ? i : j)];
-            if ((k & 1) == 0) {
-                a = rstep<true>(f, t, a);
-                cs = i == k - K0 ? a : cs;
-            } else {
-                a = rstep<false>(f, t, a);
-                cc = j == k - K0 ? a : cc;
-            }
-        }
-        const int ke = K0 + i, ko = K0 + j;
-        *((i < NS && !(ke & 1)) ? rb + 13 * (ke + 1) + j : junk) = cs;
-        *((j < NS && (ko & 1)) ? rb + 13 * (ko + 1) + i : junk) = cc;
-        if constexpr (XO) {
-            if constexpr (((K1 - 1) & 1) == 0)
-                *(j == 0 ? xo + i : junk) = a;
-            else
-                *(i == 0 ? xo + j : junk) = a;
-        }
-    }
-
-    // Phase B forward, chunk C >= 1: entry a_{S(C)-1} from the boundary values, then the stages
-    template <int C>
-    IMPC_WF void fwd_fix(const double *tb, double *rb) {
-        const double *X = lds + LD::XF_OFF;
-        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;
-        double *junk = lds + LD::JUNK_OFF + lo;
-        double v = X[8 * (C - 1) + j];
-        if constexpr (C >= 2) v = v + mv_i(PF(LD::S(C) - 1), X[8 * (C - 2) + i], l);
-        if constexpr (C == 3) v = v + mv_i(PIF(), X[i], l);
-        constexpr int K0 = LD::S(C), K1 = LD::S(C + 1);
-        double r[K1 - K0];
-        _Pragma("unroll") for (int k = K0; k < K1; k++) r[k - K0] = mv_j(PF(k), v, l);
-        _Pragma("unroll") for (int k = K0; k < K1; k++) {
-            const double ah = k == K0 ? tb[13 * k + i] : rb[13 * k + i];
-            *(j == 0 ? rb + 13 * k + i : junk) = ah + r[k - K0];
-        }
-    }
-
-    // Phase A backward, chunk [KB, KT]: x^_{KT} = e_{KT}; stores x^_k, KB <= k < KT, to xb and
-    // x^_{KB} to xo (XO)
-    template <int KB, int KT, bool XO>
-    IMPC_WF void bwd_chunk(const double *eb, double *xb, double *xo) {
-        const double *Fm = F();
-        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;
-        double *junk = lds + LD::JUNK_OFF + lo;
-        constexpr int NS = KT - KB;
-        double x = eb[13 * KT + ((KT & 1) ? j : i)];
-        double cs = 0.0, cc = 0.0;
-        _Pragma("unroll") for (int k = KT - 1; k >= KB; k--) {
-            const double f = Fm[64 * k + l], e = eb[13 * k + ((k & 1) ? j : i)];
-            if (k & 1) {
-                x = rstep<true>(f, e, x);
-                cs = i == KT - 1 - k ? x : cs;
-            } else {
-                x = rstep<false>(f, e, x);
-                cc = j == KT - 1 - k ? x : cc;
-            }
-        }
-        const int ks = KT - 1 - i, kc = KT - 1 - j;
-        *((i < NS && (ks & 1)) ? xb + 13 * ks + j : junk) = cs;
-        *((j < NS && !(kc & 1)) ? xb + 13 * kc + i : junk) = cc;
-        if constexpr (XO) {
-            if constexpr ((KB & 1) == 0)
-                *(j == 0 ? xo + i : junk) = x;
-            else
-                *(i == 0 ? xo + j : junk) = x;
-        }
-    }
-
-    // Phase B backward, chunk C <= 2: entry x_{S(C+1)}, then the stages
-    template <int C>
-    IMPC_WF void bwd_fix(const double *eb, double *xb) {
-        const double *X = lds + LD::XB_OFF;  // x^_{S(c)} at X + 8 (c - 1)
-        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;
-        double *junk = lds + LD::JUNK_OFF + lo;
-        double v = X[8 * C + j];
-        if constexpr (C <= 1) v = v + mv_i(PB(LD::S(C + 1)), X[8 * (C + 1) + i], l);
-        if constexpr (C == 0) v = v + mv_i(PIB(), X[16 + i], l);
-        constexpr int K0 = LD::S(C), K1 = LD::S(C + 1);
-        double r[K1 - K0];
-        _Pragma("unroll") for (int k = K0; k < K1; k++) r[k - K0] = mv_j(PB(k), v, l);
-        _Pragma("unroll") for (int k = K0; k < K1; k++) {
-            const double xh = k == K1 - 1 ? eb[13 * k + i] : xb[13 * k + i];
-            *(j == 0 ? xb + 13 * k + i : junk) = xh + r[k - K0];
-        }
-    }
-
-    IMPC_WF void fwd_chunked(const double *tb, double *rb) {
-        double *X = lds + LD::XF_OFF;
-        const int w = L >> 6;
-        if (w == 0) fwd_chunk<LD::S(0), LD::S(1), true>(tb, rb, X);
-        else if (w == 1) fwd_chunk<LD::S(1), LD::S(2), true>(tb, rb, X + 8);
-        else if (w == 2) fwd_chunk<LD::S(2), LD::S(3), true>(tb, rb, X + 16);
-        else fwd_chunk<LD::S(3), LD::S(4), false>(tb, rb, X);
-        wv.sync();
-        if (w == 1) fwd_fix<1>(tb, rb);
-        else if (w == 2) fwd_fix<2>(tb, rb);
-        else if (w == 3) fwd_fix<3>(tb, rb);
-    }
-
-    IMPC_WF void bwd_chunked(const double *eb, double *xb) {
-        double *X = lds + LD::XB_OFF;
-        const int w = L >> 6;
-        if (w == 0) bwd_chunk<LD::S(0), LD::S(1) - 1, false>(eb, xb, X);
-        else if (w == 1) bwd_chunk<LD::S(1), LD::S(2) - 1, true>(eb, xb, X);
-        else if (w == 2) bwd_chunk<LD::S(2), LD::S(3) - 1, true>(eb, xb, X + 8);
-        else bwd_chunk<LD::S(3), LD::S(4) - 1, true>(eb, xb, X + 16);
-        wv.sync();
-        if (w == 0) bwd_fix<0>(eb, xb);
-        else if (w == 1) bwd_fix<1>(eb, xb);
-        else if (w == 2) bwd_fix<2>(eb, xb);
-    }
-
     // One step of a stage recursion on the 8x8 lane grid: returns c - R(F v), R the strided
     // (STRIDE) or contiguous 8-lane sum.
     template <bool STRIDE>
     IMPC_WF double rstep(double f, double c, double v) {
-#if IMPC_RFOLD
-        // c - sum_q f_q v_q with c folded into the products: the lane at reduction index 0 forms
-        // fma(f, -v, c), the others f (-v); the select acts on the prefetched c, off the chain,
-        // and the chain loses its final subtraction.
-        const int l = L & 63;
-        const bool own = STRIDE ? (l >> 3) == 0 : (l & 7) == 0;
-        const double p = __builtin_fma(f, -v, own ? c : 0.0);
-        return STRIDE ? wv.sum_stride8(p) : wv.sum_contig8(p);
-#else
         const double p = prod_nc(f, v);
         return c - (STRIDE ? wv.sum_stride8(p) : wv.sum_contig8(p));
-#endif
-    }
-
-    // IMPC_SFOLD: a step's state is (c, S) with v = c - S (c the step's t / e value, S its 8-lane
-    // sum); the next step's product f v is formed as fma(-f, S, f c), with f c off the chain, so
-    // the subtraction leaves the dependent chain (v itself is formed only for the stores)
-    template <bool STRIDE>
-    IMPC_WF double fstep(double f, double c, double S) {
-        const double p = __builtin_fma(-f, S, prod_nc(f, c));
-        return STRIDE ? wv.sum_stride8(p) : wv.sum_contig8(p);
     }
 
     // Sweeps with a compile-time step count WC (= WSPEC) are fully unrolled: every LDS wait is
@@ -1437,11 +762,11 @@ struct WaveQP {
         if (((m >> 1) & 7) == other) c[m >> 4] = r;
     }
     // cap with the lane test as a compile-time lane mask (OI: `other` is the lane's i = l >> 3, else
-    // j = l & 7; lane l = 8 i + j of the recursion wavefront): IMPC_CMASK selects by that constant
-    // mask in an SGPR pair instead of a v_cmp per step
+    // j = l & 7; lane l = 8 i + j of the recursion wavefront): the select by that constant mask in
+    // an SGPR pair instead of a v_cmp per step (the CPU emulation takes the plain test)
     template <bool OI>
     IMPC_WF static void capm(double (&c)[CQ], double r, int m, int other) {
-#if IMPC_CMASK && defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
         (void)other;
         const int v = (m >> 1) & 7;
         const uint64_t msk = OI ? (0xFFull << (8 * v)) : (0x0101010101010101ull << v);
@@ -1476,63 +801,24 @@ struct WaveQP {
         // (F, t) of the next even / odd step, loaded two steps ahead (reads past the last stage
         // stay inside the LDS buffers and are never used)
         double fe = Fm[l], te = tb[13 + j], fo = Fm[64 + l], to = tb[26 + i];
-#if IMPC_SFOLD
-        double S = 0.0;  // a_0 = t_0 - 0
-#endif
-        // one step: a <- t - R(f a); SFOLD: (a, S) <- (t, R(fma(-f, S, f a))), the value t - S
-        auto step = [&](auto stride, double f, double t) -> double {
-#if IMPC_SFOLD
-            S = fstep<decltype(stride)::value>(f, a, S);
-            a = t;
-            return t - S;
-#else
-            a = rstep<decltype(stride)::value>(f, t, a);
-            return a;
-#endif
-        };
-        using ST = BoolC<true>;
-        using SC = BoolC<false>;
         if constexpr (WC > 0) {
             double c0[CQ], c1[CQ];
             _Pragma("unroll") for (int q = 0; q < CQ; q++) c0[q] = c1[q] = 0.0;
-#if IMPC_SSTORE
-            // each stage stored as produced by all 64 lanes: the 8 lanes of an output index hold
-            // bitwise the same value and write it to the same address (no lane mask, no capture)
-            double *rj = rb + j, *ri = rb + i;
-#elif IMPC_HCAP
-            double hist[WC];  // every step's output in registers (constant indices), stored after
-#endif
             _Pragma("unroll") for (int k = 0; k < WC; k += 2) {
                 const double f0 = fe, t0 = te;
                 fe = Fm[64 * (k + 2) + l];
                 te = tb[13 * (k + 3) + j];
-#if IMPC_SSTORE
-                rj[13 * (k + 1)] = step(ST{}, f0, t0);
-#elif IMPC_HCAP
-                hist[k] = step(ST{}, f0, t0);
-#else
-                capm<true>(c0, step(ST{}, f0, t0), k, i);
-#endif
+                a = rstep<true>(f0, t0, a);
+                capm<true>(c0, a, k, i);
                 if (k + 1 < WC) {
                     const double f1 = fo, t1 = to;
                     fo = Fm[64 * (k + 3) + l];
                     to = tb[13 * (k + 4) + i];
-#if IMPC_SSTORE
-                    ri[13 * (k + 2)] = step(SC{}, f1, t1);
-#elif IMPC_HCAP
-                    hist[k + 1] = step(SC{}, f1, t1);
-#else
-                    capm<false>(c1, step(SC{}, f1, t1), k + 1, j);
-#endif
+                    a = rstep<false>(f1, t1, a);
+                    capm<false>(c1, a, k + 1, j);
                 }
             }
-#if IMPC_HCAP
-            // even steps' outputs (index j) from the lanes i == 0, odd steps' (index i) from j == 0
-            if (i == 0) _Pragma("unroll") for (int k = 0; k < WC; k += 2) rb[13 * (k + 1) + j] = hist[k];
-            if (j == 0) _Pragma("unroll") for (int k = 1; k < WC; k += 2) rb[13 * (k + 1) + i] = hist[k];
-#elif !IMPC_SSTORE
             cap_store<true>(c0, c1, rb, WC, true, i, j);
-#endif
         } else {
             // one lane per element writes, the rest write to discard slots (no divergent branch)
             double *junk = lds + LD::JUNK_OFF + lo;
@@ -1541,12 +827,14 @@ struct WaveQP {
                 const double f0 = fe, t0 = te;
                 fe = Fm[64 * (k + 2) + l];
                 te = tb[13 * (k + 3) + j];
-                *(wrj ? rb + 13 * (k + 1) + j : junk) = step(ST{}, f0, t0);
+                a = rstep<true>(f0, t0, a);
+                *(wrj ? rb + 13 * (k + 1) + j : junk) = a;
                 if (k + 1 >= W) break;
                 const double f1 = fo, t1 = to;
                 fo = Fm[64 * (k + 3) + l];
                 to = tb[13 * (k + 4) + i];
-                *(wri ? rb + 13 * (k + 2) + i : junk) = step(SC{}, f1, t1);
+                a = rstep<false>(f1, t1, a);
+                *(wri ? rb + 13 * (k + 2) + i : junk) = a;
             }
         }
     }
@@ -1563,64 +851,26 @@ struct WaveQP {
         const int k1 = W - 2 > 0 ? W - 2 : 0;
         double fa = Fm[64 * (W - 1) + l], ea = eb[13 * (W - 1) + (ODD ? j : i)];
         double fb = Fm[64 * k1 + l], ebv = eb[13 * k1 + (ODD ? i : j)];
-#if IMPC_SFOLD
-        double S = 0.0;  // x_W = e_W - 0
-#endif
-        auto step = [&](auto stride, double f, double e) -> double {
-#if IMPC_SFOLD
-            S = fstep<decltype(stride)::value>(f, x, S);
-            x = e;
-            return e - S;
-#else
-            x = rstep<decltype(stride)::value>(f, e, x);
-            return x;
-#endif
-        };
-        using SA = BoolC<ODD>;
-        using SB = BoolC<!ODD>;
         if constexpr (WC > 0) {
             double c0[CQ], c1[CQ];
             _Pragma("unroll") for (int q = 0; q < CQ; q++) c0[q] = c1[q] = 0.0;
-#if IMPC_SSTORE
-            double *xe = xb + (ODD ? j : i), *xo = xb + (ODD ? i : j);  // even / odd steps' outputs
-#elif IMPC_HCAP
-            double hist[WC];
-#endif
             _Pragma("unroll") for (int m = 0; m < WC; m += 2) {
                 const int k = WC - 1 - m;
                 const int k2 = k - 2 > 0 ? k - 2 : 0, k3 = k - 3 > 0 ? k - 3 : 0;
                 const double f0 = fa, e0 = ea;
                 fa = Fm[64 * k2 + l];
                 ea = eb[13 * k2 + (ODD ? j : i)];
-#if IMPC_SSTORE
-                xe[13 * k] = step(SA{}, f0, e0);
-#elif IMPC_HCAP
-                hist[m] = step(SA{}, f0, e0);
-#else
-                capm<ODD>(c0, step(SA{}, f0, e0), m, ODD ? i : j);
-#endif
+                x = rstep<ODD>(f0, e0, x);
+                capm<ODD>(c0, x, m, ODD ? i : j);
                 if (m + 1 < WC) {
                     const double f1 = fb, e1 = ebv;
                     fb = Fm[64 * k3 + l];
                     ebv = eb[13 * k3 + (ODD ? i : j)];
-#if IMPC_SSTORE
-                    xo[13 * (k - 1)] = step(SB{}, f1, e1);
-#elif IMPC_HCAP
-                    hist[m + 1] = step(SB{}, f1, e1);
-#else
-                    capm<!ODD>(c1, step(SB{}, f1, e1), m + 1, ODD ? j : i);
-#endif
+                    x = rstep<!ODD>(f1, e1, x);
+                    capm<!ODD>(c1, x, m + 1, ODD ? j : i);
                 }
             }
-#if IMPC_HCAP
-            // step m is stage WC - 1 - m; even steps' outputs at index j (ODD) / i, odd steps' at the other
-            if ((ODD ? i : j) == 0)
-                _Pragma("unroll") for (int m = 0; m < WC; m += 2) xb[13 * (WC - 1 - m) + (ODD ? j : i)] = hist[m];
-            if ((ODD ? j : i) == 0)
-                _Pragma("unroll") for (int m = 1; m < WC; m += 2) xb[13 * (WC - 1 - m) + (ODD ? i : j)] = hist[m];
-#elif !IMPC_SSTORE
             cap_store<ODD>(c0, c1, xb, WC, false, i, j);
-#endif
         } else {
             double *junk = lds + LD::JUNK_OFF + lo;
             const bool wri = j == 0, wrj = i == 0;
@@ -1629,12 +879,14 @@ struct WaveQP {
                 const double f0 = fa, e0 = ea;
                 fa = Fm[64 * k2 + l];
                 ea = eb[13 * k2 + (ODD ? j : i)];
-                *(ODD ? (wrj ? xb + 13 * k + j : junk) : (wri ? xb + 13 * k + i : junk)) = step(SA{}, f0, e0);
+                x = rstep<ODD>(f0, e0, x);
+                *(ODD ? (wrj ? xb + 13 * k + j : junk) : (wri ? xb + 13 * k + i : junk)) = x;
                 if (k - 1 < 0) break;
                 const double f1 = fb, e1 = ebv;
                 fb = Fm[64 * k3 + l];
                 ebv = eb[13 * k3 + (ODD ? i : j)];
-                *(ODD ? (wri ? xb + 13 * (k - 1) + i : junk) : (wrj ? xb + 13 * (k - 1) + j : junk)) = step(SB{}, f1, e1);
+                x = rstep<!ODD>(f1, e1, x);
+                *(ODD ? (wri ? xb + 13 * (k - 1) + i : junk) : (wrj ? xb + 13 * (k - 1) + j : junk)) = x;
             }
         }
     }
@@ -1643,29 +895,22 @@ struct WaveQP {
     IMPC_WF void write_v_products() {
         double *pb = pbuf();
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
-            if (IMPC_GFREE || gok[s]) {  // an empty slot writes a zero product to the discard slot
-                double vv = rhog_(s) * z[s] - y[s];
-                _Pragma("unroll") for (int e = 0; e < 4; e++) pb[gdst(s, e)] = a[s][e] * vv;
-            }
+            // (an empty slot writes a zero product to the discard slot)
+            double vv = rhog_(s) * z[s] - y[s];
+            _Pragma("unroll") for (int e = 0; e < 4; e++) pb[gdst(s, e)] = a[s][e] * vv;
         }
         wv.lsync();
     }
 
     // --------------------------------------------------------------- one ADMM iteration
     IMPC_WF void iterate(bool need_delta) {
-        if constexpr (TWIST) {
-            iterate_tw(need_delta);
-            return;
-        }
         const int W = Wst();
-        const bool pair = LD::PAIR && W == LD::WSPEC;
         double *rb = rbuf(), *tb = tbuf(), *eb = ebuf(), *xb = xbuf();
         const double sigma = sig_;
         IMPC_REP(kSecRhs) {
-            // rhs = sigma x - q + A' v   (stage order; IMPC_PFREE: an empty slot's iterates, bounds
-            // and column are zero, so it writes 0)
+            // rhs = sigma x - q + A' v   (stage order; an empty slot's iterates, bounds and column
+            // are zero, so it writes 0)
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
-                if (!IMPC_PFREE && !vok[s]) continue;
                 int v = NL * s + L;
                 double vb = rhob(s) * zb[s] - yb[s];
                 double r = sigma * x[s] - q[s];
@@ -1677,48 +922,19 @@ struct WaveQP {
         }
         IMPC_SEC(kSecRhs);
         IMPC_REP(kSecS1) {
-            // S1: t_k = r_k[:8] - G_{k-1}[:, 8:] r_{k-1}[8:]  (IMPC_PFREE: every lane; a stage-0 or
-            // empty slot has zero coupling coefficients, a control lane's t lands in a slot nothing
-            // reads)
+            // S1: t_k = r_k[:8] - G_{k-1}[:, 8:] r_{k-1}[8:]  (every lane, without branches: a
+            // stage-0 or empty slot has zero coupling coefficients, a control lane's t lands in a
+            // slot nothing reads)
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
-                if (!IMPC_PFREE && (!vok[s] || vr_[s] >= 8)) continue;
                 int v = NL * s + L;
                 double t = rb[v];
-                if (IMPC_PFREE || vs_[s] > 0) {
-                    // (PFREE, stage 0: the zero tail of the x exchange, not LDS below rb -- past the
-                    // horizon's last F block that is another QP's data or uninitialised)
-                    const double *rp = lds_at(!IMPC_PFREE || vs_[s] > 0 ? LD::R_OFF + 13 * (vs_[s] - 1) + 8 : LD::X_OFF + LD::NMAX);
-                    double rv[5];
-                    _Pragma("unroll") for (int cc = 0; cc < 5; cc++) rv[cc] = rp[cc];
-                    IMPC_LOADS_FIRST(5, 12);
-#if IMPC_TREE
-                    double tb2 = cp[s][1] * rv[1];
-                    tb2 += cp[s][3] * rv[3];
-                    t -= cp[s][0] * rv[0];
-                    t -= cp[s][2] * rv[2];
-                    t -= cp[s][4] * rv[4];
-                    t -= tb2;
-#else
-                    _Pragma("unroll") for (int cc = 0; cc < 5; cc++) t -= cp[s][cc] * rv[cc];
-#endif
-                }
-                if constexpr (LD::PAIR) {
-                    // pair-blocked forward: on the even stages k >= 2 the chain takes
-                    // u_k = t_k - F_{k-1} t_{k-1} = t_k - F_{k-1} r_{k-1}[:8] + M_{k-2} r_{k-2}[8:]
-                    int k = vs_[s];
-                    if (pair && k >= 2 && !(k & 1)) {
-                        int r = vr_[s];
-                        opaque(k);  // per-lane addresses formed here, not hoisted out of the ADMM loop
-                        opaque(r);
-                        const double *r1 = rb + 13 * (k - 1), *r2 = rb + 13 * (k - 2) + 8;
-                        const double *Mk = lds + LD::M_OFF + 40 * ((k - 2) >> 1) + 5 * r;
-                        double fa = 0.0, fb = 0.0, mb = 0.0;
-                        _Pragma("unroll") for (int q = 0; q < 4; q++) fa += Fp(k - 1, r, q) * r1[q];
-                        _Pragma("unroll") for (int q = 4; q < 8; q++) fb += Fp(k - 1, r, q) * r1[q];
-                        _Pragma("unroll") for (int cc = 0; cc < 5; cc++) mb += Mk[cc] * r2[cc];
-                        t = (t - (fa + fb)) + mb;
-                    }
-                }
+                // (stage 0: the zero tail of the x exchange, not LDS below rb -- past the horizon's
+                // last F block that is another QP's data or uninitialised)
+                const double *rp = lds + (vs_[s] > 0 ? LD::R_OFF + 13 * (vs_[s] - 1) + 8 : LD::X_OFF + LD::NMAX);
+                double rv[5];
+                _Pragma("unroll") for (int cc = 0; cc < 5; cc++) rv[cc] = rp[cc];
+                IMPC_LOADS_FIRST(5, 12);
+                _Pragma("unroll") for (int cc = 0; cc < 5; cc++) t -= cp[s][cc] * rv[cc];
                 tb[v] = t;
             }
             wv.lsync();
@@ -1733,21 +949,11 @@ struct WaveQP {
             // One wavefront of the team (rw) runs it -- the others go straight to the barrier and
             // leave their SIMD's issue slots to the co-resident team.
             if (L < 8) rb[L] = tb[L];
-            if (LD::CHUNK && W == LD::WSPEC) {
-                if constexpr (LD::CHUNK) fwd_chunked(tb, rb);
-            } else if ((L >> 6) == rw) {
-                IMPC_PRIO_HI();
-                if constexpr (LD::PAIR) {
-                    if (pair) fwd_pair(tb, rb);
-                    else if (W == LD::WSPEC)
-                        fwd_sweep<LD::WSPEC>(tb, rb, W);
-                    else
-                        fwd_sweep<0>(tb, rb, W);
-                } else if (W == LD::WSPEC)
+            if ((L >> 6) == rw) {
+                if (W == LD::WSPEC)
                     fwd_sweep<LD::WSPEC>(tb, rb, W);
                 else
                     fwd_sweep<0>(tb, rb, W);
-                IMPC_PRIO_LO();
             }
             wv.lsync();
         }
@@ -1755,87 +961,43 @@ struct WaveQP {
         IMPC_REP(kSecS3) {
             // S3: e_k = Ahat_k^{-1} rhat_k
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
-                if (!IMPC_PFREE && !vok[s]) continue;
-                const double *rk = lds_at(LD::R_OFF + 13 * vs_[s]);
+                const double *rk = lds + LD::R_OFF + 13 * vs_[s];
                 double rv[13];
                 _Pragma("unroll") for (int cc = 0; cc < 13; cc++) rv[cc] = rk[cc];
                 IMPC_LOADS_FIRST(7, 20);
-#if IMPC_TREE
-                double ea[4];
-                _Pragma("unroll") for (int u = 0; u < 4; u++) ea[u] = ainv[s][u] * rv[u];
-                _Pragma("unroll") for (int cc = 4; cc < 13; cc++) ea[cc & 3] += ainv[s][cc] * rv[cc];
-                const double e = (ea[0] + ea[1]) + (ea[2] + ea[3]);
-#else
                 double e = 0.0;
                 _Pragma("unroll") for (int cc = 0; cc < 13; cc++) e += ainv[s][cc] * rv[cc];
-#endif
                 eb[NL * s + L] = e;
             }
             wv.lsync();
-            if constexpr (LD::PAIR) {
-                // V: v_k = e_k - F_k' e_{k+1} on the even stages k <= W - 3 (pair-blocked backward
-                // chain), in place: each lane reads only the odd stage k + 1 besides its own value
-                if (pair) {
-                    _Pragma("unroll") for (int s = 0; s < VS; s++) {
-                        int k = vs_[s], r = vr_[s];
-                        if (!vok[s] || r >= 8 || (k & 1) || k > W - 3) continue;
-                        opaque(k);
-                        opaque(r);
-                        const double *e1 = eb + 13 * (k + 1);
-                        double va = 0.0, vb = 0.0;
-                        _Pragma("unroll") for (int q = 0; q < 4; q++) va += Fp(k, q, r) * e1[q];
-                        _Pragma("unroll") for (int q = 4; q < 8; q++) vb += Fp(k, q, r) * e1[q];
-                        eb[NL * s + L] = eb[NL * s + L] - (va + vb);
-                    }
-                    wv.lsync();
-                }
-            }
         }
         IMPC_SEC(kSecS3);
         IMPC_REP(kSecBwd) {
             // S4: backward 8-dim recursion x_k[:8] = e_k[:8] - F_k' x_{k+1}[:8] on the same grid and
             // stored layout: even steps reduce over j (contiguous), odd steps over i (strided).
             if (L < 8) xb[13 * W + L] = eb[13 * W + L];
-            if (LD::CHUNK && W == LD::WSPEC) {
-                if constexpr (LD::CHUNK) bwd_chunked(eb, xb);
-            } else if ((L >> 6) == rw) {
-                IMPC_PRIO_HI();
-                if (LD::PAIR && pair) {
-                    if constexpr (LD::PAIR) bwd_pair(eb, xb);
-                } else if (W == LD::WSPEC)
+            if ((L >> 6) == rw) {
+                if (W == LD::WSPEC)
                     bwd_sweep<((LD::WSPEC - 1) & 1) != 0, LD::WSPEC>(eb, xb, W);
                 else if ((W - 1) & 1)
                     bwd_sweep<true, 0>(eb, xb, W);
                 else
                     bwd_sweep<false, 0>(eb, xb, W);
-                IMPC_PRIO_LO();
             }
             wv.lsync();
         }
         IMPC_SEC(kSecBwd);
         IMPC_REP(kSecS5) {
-            // S5: controls x_k[8:] = e_k[8:] - G_k[:, 8:]' x_{k+1}[:8]  (IMPC_PFREE: every lane, the
-            // state lanes' and empty slots' results to their discard slots)
+            // S5: controls x_k[8:] = e_k[8:] - G_k[:, 8:]' x_{k+1}[:8]  (every lane, the state lanes'
+            // and empty slots' results to their discard slots)
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
-                if (!IMPC_PFREE && (!vok[s] || vr_[s] < 8)) continue;
-                const double *xn = lds_at(LD::X_OFF + 13 * (vs_[s] + 1));
+                const double *xn = lds + LD::X_OFF + 13 * (vs_[s] + 1);
                 double t = eb[NL * s + L];
                 double xv[8];
                 _Pragma("unroll") for (int j = 0; j < 8; j++) xv[j] = xn[j];
                 IMPC_LOADS_FIRST(5, 16);
-#if IMPC_TREE
-                double tb2 = cp[s][1] * xv[1];
-                _Pragma("unroll") for (int j = 3; j < 8; j += 2) tb2 += cp[s][j] * xv[j];
-                _Pragma("unroll") for (int j = 0; j < 8; j += 2) t -= cp[s][j] * xv[j];
-                t -= tb2;
-#else
                 _Pragma("unroll") for (int j = 0; j < 8; j++) t -= cp[s][j] * xv[j];
-#endif
-#if IMPC_PFREE
                 *(vok[s] && vr_[s] >= 8 ? xb + NL * s + L : lds + LD::JUNK_OFF + L) = t;
-#else
-                xb[NL * s + L] = t;
-#endif
             }
             wv.lsync();
         }
@@ -1843,33 +1005,14 @@ struct WaveQP {
         update_and_products(need_delta);
     }
 
-    // project_z (auxil.h): min(max(v, l), u) as c_max / c_min, or (IMPC_VMAX) as v_max_f64 /
-    // v_min_f64 -- the same value except the sign of a zero when v equals a zero bound
-    IMPC_WF static double clampz(double v, double l, double u) {
-#if IMPC_VMAX
-        return __builtin_fmin(__builtin_fmax(v, l), u);
-#else
-        return dmin(dmax(v, l), u);
-#endif
-    }
-
-    IMPC_WF void update_and_products(bool need_delta) {
-#if IMPC_NDT
-        if (need_delta)
-            update_and_products_t<true>();
-        else
-            update_and_products_t<false>();
-#else
-        update_and_products_t<false>(need_delta);
-#endif
-    }
+    // project_z (auxil.h): min(max(v, l), u), as v_max_f64 / v_min_f64 -- the same value as the
+    // reference's c_max / c_min except the sign of a zero when v equals a zero bound
+    IMPC_WF static double clampz(double v, double l, double u) { return __builtin_fmin(__builtin_fmax(v, l), u); }
 
     // update_x and the box rows (update_z / project / update_y), the general rows, and the
-    // products of the next rhs (the end of every ADMM iteration).  ND: the check-iteration deltas
-    // are written (IMPC_NDT: a compile-time instance each; otherwise the runtime flag nd).
-    template <bool ND>
-    IMPC_WF void update_and_products_t(bool nd = ND) {
-        const bool need_delta = ND || nd;
+    // products of the next rhs (the end of every ADMM iteration).  need_delta: the check-iteration
+    // deltas are written.
+    IMPC_WF void update_and_products(bool need_delta) {
         double *xb = xbuf();
         const double alpha = alp_, oma = (double)1.0 - alp_;
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
@@ -1886,21 +1029,16 @@ struct WaveQP {
             if (need_delta) dyb(s) = dy;
             zb[s] = zn;
         }
-        // general rows (IMPC_GFREE: an empty slot's columns are the zero tail of the x exchange, its
-        // A values, bounds and iterates zero, so it computes zeros, without a per-slot branch)
+        // general rows, without a per-slot branch: an empty slot's columns are the zero tail of the
+        // x exchange, its A values, bounds and iterates zero, so it computes zeros
         double xg[GS][4];
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
-            _Pragma("unroll") for (int e = 0; e < 4; e++) xg[s][e] = (IMPC_GFREE || gok[s]) ? xb[gcol(s, e)] : 0.0;
+            _Pragma("unroll") for (int e = 0; e < 4; e++) xg[s][e] = xb[gcol(s, e)];
         }
         IMPC_LOADS_FIRST(4 * GS, 8 * GS);
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
-            if (!IMPC_GFREE && !gok[s]) continue;
-#if IMPC_TREE
-            const double zt = (a[s][0] * xg[s][0] + a[s][1] * xg[s][1]) + (a[s][2] * xg[s][2] + a[s][3] * xg[s][3]);
-#else
             double zt = 0.0;
             _Pragma("unroll") for (int e = 0; e < 4; e++) zt += a[s][e] * xg[s][e];
-#endif
             double zr = alpha * zt + oma * z[s];
             double zn = clampz(zr + rhoig_(s) * y[s], lg[s], ug[s]);
             double dy = rhog_(s) * (zr - zn);
@@ -1913,403 +1051,6 @@ struct WaveQP {
         IMPC_SEC(kSecUpdate);
         IMPC_REP(kSecProducts) write_v_products();
         IMPC_SEC(kSecProducts);
-    }
-
-    // ------------------------------------------------------ twisted elimination (TWIST)
-    // One 8-dim chain of S steps on the recursion grid (lane l = 8i + j of the calling wavefront):
-    //   v <- c - B v  (TR: c - B' v),  B = the stored block of stage k(m) = K0 + D m.
-    // F slot k holds its block with the column index on i for even k (factorize), so a plain
-    // product of an even stage reduces over i (input at i, output at j) and a transposed one over j,
-    // odd stages the other way round: consecutive steps alternate without moving data.  c of step m
-    // is read at cb + 13 (k + CO) + (output index); the result goes to ob + 13 (k + OO) + (output
-    // index), captured in registers during the sweep (each lane keeps at most one even and one odd
-    // step) and stored after it.  v: the input of step 0, at its index.
-    static IMPC_WF constexpr bool strd(int k, bool tr) { return ((k & 1) == 0) != tr; }
-    template <int S, int K0, int D, bool TR, int CO, int OO>
-    IMPC_WF void chain(const double *cb, double *ob, double v) {
-        static_assert(S >= 1 && S <= 16, "captures hold one even and one odd step per lane");
-        const double *Fm = lds + LD::F_OFF;
-        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;
-        double fq[2], cq[2], cap0 = 0.0, cap1 = 0.0;
-        // each prefetch from its own (opaque) address register: merged into one ds_read2 with the
-        // next prefetch of the same parity, a load would issue two steps late and its wait would
-        // sit on the chain (IMPC_TWOPQ)
-        auto ldF = [&](int k) {
-            int o = 64 * k + l;
-            if (IMPC_TWOPQ) opaque(o);
-            return Fm[o];
-        };
-        auto ldC = [&](int k) {
-            int o = 13 * (k + CO) + (strd(k, TR) ? j : i);
-            if (IMPC_TWOPQ) opaque(o);
-            return cb[o];
-        };
-        _Pragma("unroll") for (int m = 0; m < 2 && m < S; m++) {
-            const int k = K0 + D * m;
-            fq[m] = ldF(k);
-            cq[m] = ldC(k);
-        }
-        _Pragma("unroll") for (int m = 0; m < S; m++) {
-            const int k = K0 + D * m;
-            const double f0 = fq[m & 1], c0 = cq[m & 1];
-            if (m + 2 < S) {  // the next step of this parity, two steps ahead
-                fq[m & 1] = ldF(k + 2 * D);
-                cq[m & 1] = ldC(k + 2 * D);
-            }
-            if (strd(k, TR)) {
-                v = rstep<true>(f0, c0, v);
-                if (((m >> 1) & 7) == i) (m & 1 ? cap1 : cap0) = v;
-            } else {
-                v = rstep<false>(f0, c0, v);
-                if (((m >> 1) & 7) == j) (m & 1 ? cap1 : cap0) = v;
-            }
-        }
-        // even steps: output index (strd(K0) ? j : i), kept by the lane whose other index is m / 2
-        const bool se = strd(K0, TR), so = strd(K0 + D, TR);
-        const int me = 2 * (se ? i : j), mo = 2 * (so ? i : j) + 1;
-        if (me < S) ob[13 * (K0 + D * me + OO) + (se ? j : i)] = cap0;
-        if (mo < S) ob[13 * (K0 + D * mo + OO) + (so ? j : i)] = cap1;
-    }
-
-    // One ADMM iteration with the twisted solve.  Exchange vectors per stage k (13 slots each):
-    //   rb: r (rhs); a_k in [:8] for top stages 1..KM; u_{k-1} = Bbar_{k-1} x_{k-1} in [:8] for
-    //       bottom stages (written after r is consumed)
-    //   tb: t_k (top, k <= KM) / s_k = Acheck_k^-1[:8,:] r_k (bottom) in [:8]; then c_{k-1} =
-    //       Bbar_{k-1} zhat_{k-1} (bottom, k - 1 > KM) in [:8]
-    //   eb: e_k = Ahat_k^-1 (a_k, r_k[8:]) (top) / zhat_k = Acheck_k^-1 (r_k - Bbar_k' w_{k+1}) (bottom)
-    //   xb: w_k = (zhat_k)[:8] (bottom, chain A), then the solution x
-    IMPC_WF void iterate_tw(bool need_delta) {
-        constexpr int W = WF;
-        double *rb = rbuf(), *tb = tbuf(), *eb = ebuf(), *xb = xbuf();
-        const double sigma = sig_;
-        const int wave = L >> 6, rw2 = (rw + 2) & 3;
-        // rhs = sigma x - q + A' v   (stage order)
-        IMPC_REP(kSecRhs) {
-            _Pragma("unroll") for (int s = 0; s < VS; s++) {
-                if (!vok[s]) continue;
-                const int v = NL * s + L;
-                const double vb = rhob(s) * zb[s] - yb[s];
-                double r = sigma * x[s] - q[s];
-                r += ab[s] * vb;
-                r += col_gather(v, hid_[s]);
-                rb[v] = r;
-            }
-            wv.lsync();
-        }
-        IMPC_SEC(kSecRhs);
-        IMPC_REP(kSecS1) {
-            // P1: t_k = r_k[:8] - G_{k-1}[:, 8:] r_{k-1}[8:] (top and middle), s_k = Acheck_k^-1[:8,:] r_k (bottom)
-            _Pragma("unroll") for (int s = 0; s < VS; s++) {
-                if (!vok[s] || vr_[s] >= 8) continue;
-                const int v = NL * s + L, k = vs_[s];
-                double t;
-                if (k <= KM) {
-                    t = rb[v];
-                    if (k > 0) {
-                        const double *rp = rb + 13 * (k - 1) + 8, *mc = lds + LD::MID_OFF + 5 * vr_[s];
-                        double rv[5];
-                        _Pragma("unroll") for (int cc = 0; cc < 5; cc++) rv[cc] = rp[cc];
-                        // the middle stage's lanes hold Abar^-1 Bbar' rows in cp: their G_{KM-1}[:, 8:]
-                        // rows live in LDS
-                        _Pragma("unroll") for (int cc = 0; cc < 5; cc++) t -= (k == KM ? mc[cc] : cp[s][cc]) * rv[cc];
-                    }
-                } else {
-                    const double *rk = rb + 13 * k;
-                    double rv[13];
-                    _Pragma("unroll") for (int cc = 0; cc < 13; cc++) rv[cc] = rk[cc];
-                    t = 0.0;
-                    _Pragma("unroll") for (int cc = 0; cc < 13; cc++) t += ainv[s][cc] * rv[cc];
-                }
-                tb[v] = t;
-            }
-            wv.lsync();
-        }
-        IMPC_SEC(kSecS1);
-        IMPC_REP(kSecFwd) {
-            // chains A: a_{k+1} = t_{k+1} - F_k a_k (k = 0..KM-1) and w_k = s_k - H_k w_{k+1}
-            // (k = W-1..KM+1, w_W = s_W), on two wavefronts at once
-            if (L < 8) rb[L] = tb[L];                      // a_0 = t_0
-            if (L >= 64 && L < 72) xb[13 * W + L - 64] = tb[13 * W + L - 64];  // w_W = s_W
-            if (wave == rw) {
-                const int l = lane_o() & 63;
-                chain<KM, 0, 1, false, 1, 1>(tb, rb, tb[strd(0, false) ? (l >> 3) : (l & 7)]);
-            } else if (wave == rw2) {
-                const int l = lane_o() & 63;
-                chain<W - 1 - KM, W - 1, -1, false, 0, 0>(tb, xb,
-                                                           tb[13 * W + (strd(W - 1, false) ? (l >> 3) : (l & 7))]);
-            }
-            wv.lsync();
-        }
-        IMPC_SEC(kSecFwd);
-        IMPC_REP(kSecS3) {
-            // P3: e_k (top), x_KM = Abar^-1 ((a_KM, r_KM[8:]) - Bbar_KM' w_{KM+1}) (middle),
-            // zhat_k = Acheck_k^-1 r_k - (Acheck_k^-1 Bbar_k') w_{k+1} (bottom)
-            _Pragma("unroll") for (int s = 0; s < VS; s++) {
-                if (!vok[s]) continue;
-                const int v = NL * s + L, k = vs_[s];
-                // the coupling term first, kept apart from the 13-term product by a scheduling
-                // barrier, so the two operand sets are not live at once
-                double g = 0.0;
-                if (k >= KM && k < W) {
-                    const double *w1 = xb + 13 * (k + 1);
-                    double wv_[8];
-                    _Pragma("unroll") for (int p = 0; p < 8; p++) wv_[p] = w1[p];
-                    _Pragma("unroll") for (int p = 0; p < 8; p++) g += cp[s][p] * wv_[p];
-                }
-#if defined(__HIP_DEVICE_COMPILE__)
-                __builtin_amdgcn_sched_barrier(0);
-#endif
-                const double *rk = rb + 13 * k;
-                double rv[13];
-                _Pragma("unroll") for (int cc = 0; cc < 13; cc++) rv[cc] = rk[cc];
-                IMPC_LOADS_FIRST(7, 20);
-                double e = 0.0;
-                _Pragma("unroll") for (int cc = 0; cc < 13; cc++) e += ainv[s][cc] * rv[cc];
-                e -= g;
-                (k == KM ? xb : eb)[v] = e;
-            }
-            wv.lsync();
-        }
-        IMPC_SEC(kSecS3);
-        IMPC_REP(kSecFAsm) {
-            // P3b: u_KM = Bbar_KM x_KM and c_k = Bbar_k zhat_k (k > KM), one coupling row per state:
-            // Bbar_k row i = rho a_up a_(k, .) of the row whose stage-(k+1) entry is state i
-            _Pragma("unroll") for (int s = 0; s < GS; s++) {
-                const int cp_ = ((const int32_t *)(lds + LD::CPL_OFF))[NL * s + L];
-                if (cp_ < 0) continue;
-                const int cu = cp_ & 0xFFFF, eu = cp_ >> 16;
-                const bool m0 = cu / 13 == KM + 1;
-                const double *src = m0 ? xb : eb;
-                double acc = 0.0, au = 0.0;
-                _Pragma("unroll") for (int e = 0; e < 4; e++) {
-                    const bool up = e == eu;
-                    au = up ? a[s][e] : au;
-                    acc += up ? 0.0 : a[s][e] * src[gcol(s, e)];
-                }
-                (m0 ? rb : tb)[cu] = (rhog_(s) * au) * acc;
-            }
-            wv.lsync();
-        }
-        IMPC_REP(kSecBwd) {
-            // chains B: x_k[:8] = e_k[:8] - F_k' x_{k+1}[:8] (k = KM-1..0) and
-            // u_k = c_k - H_k' u_{k-1} (k = KM+1..W-1)
-            if (wave == rw) {
-                const int l = lane_o() & 63;
-                chain<KM, KM - 1, -1, true, 0, 0>(eb, xb, xb[13 * KM + (strd(KM - 1, true) ? (l >> 3) : (l & 7))]);
-            } else if (wave == rw2) {
-                const int l = lane_o() & 63;
-                chain<W - 1 - KM, KM + 1, 1, true, 1, 1>(tb, rb,
-                                                          rb[13 * (KM + 1) + (strd(KM + 1, true) ? (l >> 3) : (l & 7))]);
-            }
-            wv.lsync();
-        }
-        IMPC_SEC(kSecBwd);
-        IMPC_REP(kSecS5) {
-            // P5: controls of the top stages (S5), all of a bottom stage: x_k = zhat_k - Acheck_k^-1[:, :8] u_{k-1}
-            _Pragma("unroll") for (int s = 0; s < VS; s++) {
-                if (!vok[s]) continue;
-                const int v = NL * s + L, k = vs_[s];
-                if (k < KM && vr_[s] >= 8) {
-                    const double *xn = xb + 13 * (k + 1);
-                    double t = eb[v], xv[8];
-                    _Pragma("unroll") for (int jj = 0; jj < 8; jj++) xv[jj] = xn[jj];
-                    _Pragma("unroll") for (int jj = 0; jj < 8; jj++) t -= cp[s][jj] * xv[jj];
-                    xb[v] = t;
-                } else if (k > KM) {
-                    const double *uu = rb + 13 * k;
-                    double t = eb[v], uv[8];
-                    _Pragma("unroll") for (int jj = 0; jj < 8; jj++) uv[jj] = uu[jj];
-                    _Pragma("unroll") for (int jj = 0; jj < 8; jj++) t -= ainv[s][jj] * uv[jj];
-                    xb[v] = t;
-                }
-            }
-            wv.lsync();
-        }
-        IMPC_SEC(kSecS5);
-        update_and_products(need_delta);
-    }
-
-    // The twisted factorisation (TWIST): top stages 0..KM-1 as the one-ended scheme, bottom stages
-    // W..KM+1 from the bottom up, then the middle stage with both Schur complements.
-    IMPC_WF int factorize_tw() {
-        constexpr int W = WF, N = W + 1;
-        double *w = pbuf(), *rhog = pbuf() + 4 * T.mg, *diagx = lds + LD::DIAGX;
-        double *A = lds + LD::FA, *Li = lds + LD::FL, *Ai = lds + LD::FI, *Bb = lds + LD::FB, *G = lds + LD::FG,
-               *E = lds + LD::FE, *EB = lds + LD::FEB, *Fm = F();
-        _Pragma("unroll") for (int s = 0; s < GS; s++) {
-            const int g = NL * s + L;
-            if (gok[s]) {
-                _Pragma("unroll") for (int e = 0; e < 4; e++) w[4 * g + e] = a[s][e];
-                rhog[g] = rhog_(s);
-            }
-        }
-        _Pragma("unroll") for (int s = 0; s < VS; s++) {
-            if (vok[s]) {
-                const double rb = rhob(s);
-                diagx[NL * s + L] = (pd[s] + st.sigma) + rb * ab[s] * ab[s];
-            }
-        }
-        wv.sync();
-        int bad = 0;
-        for (int it = 0; it < N; it++) {
-            const int k = it < KM ? it : it < N - 1 ? W - (it - KM) : KM;
-            const int sz = k < W ? 13 : 8;
-            const bool top = k < KM, mid = k == KM;
-            // assemble M_kk (the top Schur complement E_{k-1} folded in for k <= KM) and Bbar_k
-            for (int d = L; d < kStageDests; d += NL) {
-                const bool isB = d >= 169;
-                if (isB && k == W) continue;
-                const int dd = isB ? d - 169 : d;
-                const int r = dd / 13, cc = dd % 13;
-                double val = 0.0;
-                if (isB || (r < sz && cc < sz)) {
-                    const int32_t t0 = T.term_ptr[(int64_t)k * kStageDests + d];
-                    const int32_t t1 = T.term_ptr[(int64_t)k * kStageDests + d + 1];
-                    for (int32_t t = t0; t < t1; t++) {
-                        const int32_t code = T.term[t];
-                        const int32_t g = code >> 4, e = (code >> 2) & 3, f = code & 3;
-                        val += rhog[g] * w[4 * g + e] * w[4 * g + f];
-                    }
-                    if (!isB && r == cc) val += diagx[13 * k + r];
-                    if (!isB && k > 0 && k <= KM && r < 8 && cc < 8) val -= E[8 * r + cc];
-                }
-                if (isB)
-                    Bb[dd] = val;
-                else
-                    A[dd] = val;
-            }
-            wv.sync();
-            IMPC_SEC(kSecFAsm);
-            if (!top && k < W) {
-                // bottom Schur complement: A -= Bbar_k' (Acheck_{k+1}^-1[:8,:8]) Bbar_k (T = EB Bbar_k in Li)
-                for (int p = L; p < 104; p += NL) {
-                    const int ii = p / 13, cc = p % 13;
-                    double sacc = 0.0;
-                    for (int qq = 0; qq < 8; qq++) sacc += EB[8 * ii + qq] * Bb[13 * qq + cc];
-                    Li[p] = sacc;
-                }
-                wv.sync();
-                for (int d = L; d < 169; d += NL) {
-                    const int r = d / 13, cc = d % 13;
-                    double sacc = 0.0;
-                    for (int p = 0; p < 8; p++) sacc += Bb[13 * p + r] * Li[13 * p + cc];
-                    A[d] -= sacc;
-                }
-                wv.sync();
-            }
-            // A^-1 by Gauss-Jordan with 2x2 pivot blocks (as factorize)
-            {
-                double *src = A, *dst = Li;
-                const int gi = L / 13, gc = L % 13;
-                const bool act = L < 169 && gi < sz && gc < sz;
-                for (int j = 0; j < sz; j += 2) {
-                    const bool two = j + 1 < sz, last = j + (two ? 2 : 1) >= sz;
-                    if (act) {
-                        const int i = last && gc > gi ? gc : gi, c = last && gc > gi ? gi : gc;
-                        double v;
-                        if (two) {
-                            const double p00 = src[13 * j + j], p01 = src[13 * j + j + 1];
-                            const double p10 = src[13 * (j + 1) + j], p11 = src[13 * (j + 1) + j + 1];
-                            const double det = p00 * p11 - p01 * p10;
-                            if (!(p00 > 0.0) || !(det > 0.0)) bad = 1;
-                            const double rd = 1.0 / det;
-                            const double q00 = p11 * rd, q01 = -(p01 * rd), q10 = -(p10 * rd), q11 = p00 * rd;
-                            const int ri = i - j, ci = c - j;
-                            const bool iJ = ri == 0 || ri == 1, cJ = ci == 0 || ci == 1;
-                            if (iJ && cJ) {
-                                v = ri == 0 ? (ci == 0 ? q00 : q01) : (ci == 0 ? q10 : q11);
-                            } else if (iJ) {
-                                const double s0 = src[13 * j + c], s1 = src[13 * (j + 1) + c];
-                                v = ri == 0 ? q00 * s0 + q01 * s1 : q10 * s0 + q11 * s1;
-                            } else {
-                                const double a0 = src[13 * i + j], a1 = src[13 * i + j + 1];
-                                const double u0 = a0 * q00 + a1 * q10, u1 = a0 * q01 + a1 * q11;
-                                if (cJ)
-                                    v = -(ci == 0 ? u0 : u1);
-                                else
-                                    v = src[13 * i + c] - (u0 * src[13 * j + c] + u1 * src[13 * (j + 1) + c]);
-                            }
-                        } else {
-                            const double p = src[13 * j + j];
-                            if (!(p > 0.0)) bad = 1;
-                            const double r = 1.0 / p;
-                            if (i == j && c == j)
-                                v = r;
-                            else if (i == j)
-                                v = src[13 * j + c] * r;
-                            else if (c == j)
-                                v = -(src[13 * i + j] * r);
-                            else
-                                v = src[13 * i + c] - (src[13 * i + j] * r) * src[13 * j + c];
-                        }
-                        (last ? Ai : dst)[13 * gi + gc] = v;
-                    }
-                    wv.sync();
-                    double *t = src;
-                    src = dst;
-                    dst = t;
-                }
-            }
-            _Pragma("unroll") for (int s = 0; s < VS; s++)
-                if (vok[s] && vs_[s] == k)
-                    _Pragma("unroll") for (int cc = 0; cc < 13; cc++) ainv[s][cc] = cc < sz ? Ai[13 * vr_[s] + cc] : 0.0;
-            if (top) {
-                // G_k = Bbar_k Ahat_k^-1, E_k = G_k Bbar_k', F_k (recursion layout), cp rows (S5 / S1)
-                for (int p = L; p < 104; p += NL) {
-                    const int ii = p / 13, cc = p % 13;
-                    double sacc = 0.0;
-                    for (int t = 0; t < 13; t++) sacc += Bb[13 * ii + t] * Ai[13 * t + cc];
-                    G[p] = sacc;
-                }
-                wv.sync();
-                if (L < 64) {
-                    const int ii = L >> 3, jj = L & 7;
-                    double sacc = 0.0;
-                    for (int t = 0; t < 13; t++) sacc += G[13 * ii + t] * Bb[13 * jj + t];
-                    E[8 * ii + jj] = sacc;
-                    Fm[64 * k + 8 * ii + jj] = !(k & 1) ? G[13 * jj + ii] : G[13 * ii + jj];
-                }
-                _Pragma("unroll") for (int s = 0; s < VS; s++) {
-                    if (!vok[s]) continue;
-                    if (vs_[s] == k && vr_[s] >= 8)
-                        _Pragma("unroll") for (int jj = 0; jj < 8; jj++) cp[s][jj] = G[13 * jj + vr_[s]];
-                    if (vs_[s] == k + 1 && vr_[s] < 8 && k + 1 < KM)
-                        _Pragma("unroll") for (int jj = 0; jj < 8; jj++) cp[s][jj] = jj < 5 ? G[13 * vr_[s] + 8 + jj] : 0.0;
-                }
-                if (k + 1 == KM && L < 40) lds[LD::MID_OFF + L] = G[13 * (L / 5) + 8 + L % 5];  // [8][5]
-                wv.sync();
-            } else if (k < W) {
-                // G'_k = A^-1 Bbar_k' (13 x 8, row-major at G[8 r + p]); bottom: H_k = G'_k[:8, :] in F
-                // slot k (recursion layout) and the stage's cp rows; middle: G'_KM to LDS
-                for (int p = L; p < 104; p += NL) {
-                    const int r = p >> 3, qq = p & 7;
-                    double sacc = 0.0;
-                    for (int cc = 0; cc < 13; cc++) sacc += Ai[13 * r + cc] * Bb[13 * qq + cc];
-                    G[p] = sacc;
-                }
-                wv.sync();
-                if (!mid && L < 64) {
-                    const int ii = L >> 3, jj = L & 7;
-                    Fm[64 * k + 8 * ii + jj] = !(k & 1) ? G[8 * jj + ii] : G[8 * ii + jj];
-                }
-                _Pragma("unroll") for (int s = 0; s < VS; s++)
-                    if (vok[s] && vs_[s] == k)
-                        _Pragma("unroll") for (int jj = 0; jj < 8; jj++) cp[s][jj] = G[8 * vr_[s] + jj];
-            }
-            if (!top && !mid) {
-                // Acheck_k^-1[:8, :8] for the next stage up
-                if (L < 64) EB[L] = Ai[13 * (L >> 3) + (L & 7)];
-            }
-            wv.sync();
-            IMPC_SEC(kSecFDense);
-        }
-        _Pragma("unroll") for (int s = 0; s < VS; s++)
-            if (vok[s] && vs_[s] == 0 && vr_[s] < 8)
-                _Pragma("unroll") for (int jj = 0; jj < 8; jj++) cp[s][jj] = 0.0;
-        bad = (int)wv.max((double)bad);
-        clear_exchange();
-        zero_products();
-        return bad;
     }
 
     // ------------------------------------------------------------ update_info + checks
@@ -2401,15 +1142,8 @@ struct WaveQP {
         wv.sync();
     }
 
-    // is_primal_infeasible (projects dy in place)
-    IMPC_WF int primal_infeasible(double eps, const double D[VS], const double Eb[VS], const double Eg[GS]) {
-        double nrm, lhs;
-        pinf_partials(Eb, Eg, nrm, lhs);
-        nrm = wv.max(nrm);
-        lhs = wv.sum(lhs);
-        return pinf_stage2(eps, nrm, lhs, D);
-    }
-    // its lane-local part: the projected dy, ||E dy||_inf and u' max(dy, 0) + l' min(dy, 0)
+    // is_primal_infeasible (projects dy in place), lane-local part: the projected dy, ||E dy||_inf
+    // and u' max(dy, 0) + l' min(dy, 0)
     IMPC_WF void pinf_partials(const double Eb[VS], const double Eg[GS], double &nrm_o, double &lhs_o) {
         const bool unsc = st.scaling > 0 && !st.scaled_termination;
         double nrm = 0.0, lhs = 0.0;
@@ -2463,15 +1197,7 @@ struct WaveQP {
         return res;
     }
 
-    // is_dual_infeasible
-    IMPC_WF int dual_infeasible(double eps, const double D[VS], const double Eb[VS], const double Eg[GS]) {
-        double nrm, qdx;
-        dinf_partials(D, nrm, qdx);
-        nrm = wv.max(nrm);
-        qdx = wv.sum(qdx);
-        return dinf_stage2(eps, nrm, qdx, D, Eb, Eg);
-    }
-    // its lane-local part: ||D dx||_inf and q' dx
+    // is_dual_infeasible, lane-local part: ||D dx||_inf and q' dx
     IMPC_WF void dinf_partials(const double D[VS], double &nrm_o, double &qdx_o) {
         const bool unsc = st.scaling > 0 && !st.scaled_termination;
         double nrm = 0.0, qdx = 0.0;
@@ -2541,7 +1267,6 @@ struct WaveQP {
             eps_dinf *= 10;
         }
         int prim_ok = 0, dual_ok = 0, prim_inf = 0, dual_inf = 0;
-#if IMPC_CHKRED
         // the same tests as below, the two infeasibility tests' first-stage norms and sums reduced
         // over the team in one exchange (bitwise the values of the separate reductions)
         const bool ptest = T.m != 0 && !(inf.pri_res < eps_abs + eps_rel * inf.pri_norm_u);
@@ -2555,20 +1280,6 @@ struct WaveQP {
             if (ptest) prim_inf = pinf_stage2(eps_pinf, mx[0], sm[0], D);
             if (!dual_ok) dual_inf = dinf_stage2(eps_dinf, mx[1], sm[1], D, Eb, Eg);
         }
-#else
-        if (T.m == 0) {
-            prim_ok = 1;
-        } else {
-            if (inf.pri_res < eps_abs + eps_rel * inf.pri_norm_u)
-                prim_ok = 1;
-            else
-                prim_inf = primal_infeasible(eps_pinf, D, Eb, Eg);
-        }
-        if (inf.dua_res < eps_abs + eps_rel * inf.dua_norm_u)
-            dual_ok = 1;
-        else
-            dual_inf = dual_infeasible(eps_dinf, D, Eb, Eg);
-#endif
         if (prim_ok && dual_ok) {
             status = approximate ? IMPC_SOLVED_INACCURATE : IMPC_SOLVED;
             return 1;
@@ -2602,11 +1313,8 @@ struct WaveQP {
         // the profiling record (qpt) starts at the same tick, so a QP stopped by its limit always
         // shows a recorded latency of at least that limit
         const uint64_t t0 = device_clock();
-#if IMPC_PRIO_INV && defined(__HIP_DEVICE_COMPILE__)
-        __builtin_amdgcn_s_setprio(IMPC_PRIO_INV);
-#endif
         rw = (int)(b % (NL / 64));  // spread the serial recursions of co-resident QPs over SIMDs
-#if IMPC_HWRW && defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
         // recursion wave from the hardware placement (HW_REG_HW_ID: WAVE_ID [3:0], SIMD_ID [5:4]):
         // the wave on SIMD (wave slot of the team's wave 0) mod 4, so co-resident teams, which sit
         // in different wave slots, run their recursions on different SIMDs; the QP-index choice
@@ -2615,7 +1323,7 @@ struct WaveQP {
 #endif
         IMPC_SEC_START();
         clear_exchange();
-#if IMPC_HWRW && defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
         {
             const int target = (int)lds[LD::JUNK_OFF] & 3;
             _Pragma("unroll") for (int w = NL / 64 - 1; w >= 0; w--)
@@ -2716,7 +1424,7 @@ struct WaveQP {
         int64_t info_iter = 0;
         const int chk = st.check_termination;
         int can_check = 0;
-        // countdowns instead of iter % interval (no integer division in the loop)
+        // counters of the next check / rho update instead of iter % interval
         // the loop's settings read once into registers (the batch's settings live in global memory
         // for a grouped launch: read in the loop they cost a scalar-memory round trip each
         // iteration, after every barrier)
@@ -2741,10 +1449,11 @@ struct WaveQP {
             // the check and the update run between two passes of it, so their code and registers
             // sit outside it (the operations are those of one loop, in the same order)
             bool chk_now = false, rho_now = false, stop = false;
-#if IMPC_LOOPC
-            // the same iterations, flags and counters as the countdown loop below: the pass runs to
-            // its next event nxt = min(iterations left, chk_left, rho_left); only its last iteration
-            // can be a check / rho-update / max_iter one
+            // the pass runs to its next event nxt = min(iterations left, chk_left, rho_left) (counted
+            // once per pass, not per iteration); only its last iteration can be a check /
+            // rho-update / max_iter one.  osqp_solve's time-limit test sits after the ADMM steps,
+            // before can_check is recomputed (so a stop keeps the previous iteration's value); one
+            // team-wide decision
             if (iter <= max_iter) {
                 int nxt = max_iter - iter + 1;
                 if (chk && chk_left < nxt) nxt = chk_left;
@@ -2774,28 +1483,6 @@ struct WaveQP {
                     if (!(chk_now || rho_now)) iter++;
                 }
             }
-#else
-            for (; iter <= max_iter; iter++) {
-                chk_now = chk && --chk_left == 0;
-                if (chk_now) chk_left = chk;
-                rho_now = rho_int && --rho_left == 0;
-                if (rho_now) rho_left = rho_int;
-                const bool need_delta = chk_now || iter == max_iter || tlim;
-                iterate(need_delta);
-                // osqp_solve (PROFILING build): checked after the ADMM steps, before can_check is
-                // recomputed (so it keeps the previous iteration's value); one team-wide decision
-                if (tlim) {
-                    const double el = wv.max((double)(device_clock() - t0) * tick);
-                    if (el >= tl) {
-                        status = IMPC_TIME_LIMIT_REACHED;
-                        stop = true;
-                        break;
-                    }
-                }
-                can_check = chk_now;
-                if (chk_now || rho_now) break;
-            }
-#endif
             if (stop || iter > max_iter) break;
             if (can_check) {
                 IMPC_SEC_START();

@@ -124,10 +124,10 @@ void run_w(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSet
 
 // the product's dispatch: the default-horizon specialisation when W matches (impc_qp.hip launch_wave)
 template <int VS, int GS>
-void run(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSettings &st, bool twist_ok) {
+void run(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSettings &st) {
     constexpr int WS = impc::WaveLds<NL, VS, GS>::WSPEC;
     const bool tier = T.T1r < impc::WaveLds<NL, VS, GS>::cg4(T.CG);
-    if (T.W == WS && (!impc::WaveLds<NL, VS, GS>::TW || twist_ok))
+    if (T.W == WS)
         tier ? run_w<VS, GS, WS, true>(T, io, st) : run_w<VS, GS, WS, false>(T, io, st);
     else
         tier ? run_w<VS, GS, 0, true>(T, io, st) : run_w<VS, GS, 0, false>(T, io, st);
@@ -172,13 +172,13 @@ extern "C" int emu_wave_solve_batch(int64_t n, int64_t m, const int64_t *Pp, con
     if (ms.n > 3 * NL || ms.CG > impc::WaveLds<NL, 1, 2>::CGM || ms.mg > 4 * NL) return 2;
     const int gs = ms.mg <= 2 * NL ? 2 : ms.mg <= 3 * NL ? 3 : 4;
     if (ms.n <= NL) {  // the product's shapes (impc_qp.hip kWaveVS / kWaveVSLong)
-        if (gs == 2) run<1, 2>(T, io, st, ms.twist_ok);
-        else if (gs == 3) run<1, 3>(T, io, st, ms.twist_ok);
-        else run<1, 4>(T, io, st, ms.twist_ok);
+        if (gs == 2) run<1, 2>(T, io, st);
+        else if (gs == 3) run<1, 3>(T, io, st);
+        else run<1, 4>(T, io, st);
     } else {
-        if (gs == 2) run<3, 2>(T, io, st, ms.twist_ok);
-        else if (gs == 3) run<3, 3>(T, io, st, ms.twist_ok);
-        else run<3, 4>(T, io, st, ms.twist_ok);
+        if (gs == 2) run<3, 2>(T, io, st);
+        else if (gs == 3) run<3, 3>(T, io, st);
+        else run<3, 4>(T, io, st);
     }
     return 0;
 }

@@ -98,17 +98,3 @@ def test_structured_emulation_default_horizon_batch(rho):
         compare(res, ref)
         if rho < 0.1:
             assert ref[2]["rho_updates"].max() >= 1
-
-
-@pytest.mark.parametrize("rho", [0.1, 1e-3])
-def test_structured_emulation_twisted_elimination(rho):
-    """The twisted (two-ended) block elimination of the default horizon (mpc_wave.hpp IMPC_TWIST:
-    stages 0..8 top-down, 19..10 bottom-up, the middle stage 9 from both sides; the two pairs of
-    9-step recursion chains; the coupling rows' Bbar_k products) against the oracle -- built, off in
-    the product (measured slower, profiles/r03/exp/README.md) -- with in-kernel refactorisations
-    at the small rho."""
-    s = impc.default_settings(rho=rho, **S25)
-    for name in ("config3_K8", "config2"):
-        cfg = take(CFG[name], 2)
-        res, ref = emulate(cfg, s, twist=True), oracle(cfg, s)
-        compare(res, ref)
