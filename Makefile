@@ -20,6 +20,12 @@ HOSTFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -Wall
 # RCCL (multi-GPU cost all-gather, include/impc_comm.h), from the same ROCm as the HIP runtime
 LDLIBS    := -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
+# build identity baked into the library (impc_build_id): every source compiled into it + the flags
+SRCS    := $(sort $(wildcard $(CSRC)/*.hip $(CSRC)/*.hpp $(CSRC)/*.cpp $(ROOT)/include/*.h))
+BUILD_ID := src-$(shell cat $(SRCS) | { cat; echo '$(HIPFLAGS) $(HOSTFLAGS)'; } | sha256sum | cut -c1-16)
+GIT_REV := $(shell git -C $(ROOT) rev-parse --short HEAD 2>/dev/null || echo unknown)
+IDFLAGS  = -DIMPC_BUILD_ID='"$(BUILD_ID)$(1)"' -DIMPC_GIT_REV='"$(GIT_REV)"'
+
 LIB     := $(LIBDIR)/libimpc_qp.so
 PROFLIB := $(LIBDIR)/libimpc_qp_prof.so
 ORACLE  := $(ORADIR)/libosqp_oracle.so
@@ -37,9 +43,10 @@ harness: $(HARNESS) $(EMU) $(SHIMT) $(REPLANX)
 $(LIBDIR)/impc_qp.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symbolic.hpp $(CSRC)/mpc_wave.hpp \
 		$(CSRC)/mpc_structure.hpp $(CSRC)/select.hpp $(CSRC)/mpc_build.hpp $(CSRC)/mpc_qp_internal.hpp \
 		$(CSRC)/fanout.hpp $(CSRC)/predict.hpp $(CSRC)/comm.hpp $(CSRC)/reftraj.hpp $(ROOT)/include/impc_qp.h $(ROOT)/include/impc_select.h \
-		$(ROOT)/include/impc_mpc.h $(ROOT)/include/impc_fanout.h $(ROOT)/include/impc_predict.h $(ROOT)/include/impc_comm.h
+		$(ROOT)/include/impc_mpc.h $(ROOT)/include/impc_fanout.h $(ROOT)/include/impc_predict.h $(ROOT)/include/impc_comm.h \
+		$(SRCS)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(call IDFLAGS,) -c $< -o $@
 
 # section-profiling variant of the library (tools/section_profile.py; never the product)
 prof: $(PROFLIB)
@@ -48,7 +55,7 @@ $(LIBDIR)/impc_qp_prof.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symb
 		$(CSRC)/fanout.hpp $(CSRC)/predict.hpp $(CSRC)/comm.hpp $(CSRC)/reftraj.hpp $(ROOT)/include/impc_qp.h $(ROOT)/include/impc_select.h $(ROOT)/include/impc_mpc.h \
 		$(ROOT)/include/impc_fanout.h $(ROOT)/include/impc_predict.h
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -DIMPC_SECTION_PROF -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(call IDFLAGS,-prof) -DIMPC_SECTION_PROF -c $< -o $@
 $(PROFLIB): $(LIBDIR)/impc_qp_prof.o $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o $(LIBDIR)/minsnap.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ -o $@ $(LDLIBS)
 
@@ -102,7 +109,7 @@ $(REPLANX): $(ROOT)/tests/native/replan_example.cpp $(ROOT)/include/impc_qp.h $(
 # kernel experiments (tools/ only): make variant V=name DEFS="-DX=1" -> lib/libimpc_qp_<name>.so,
 # selected at run time with IMPC_LIB_VARIANT=<name>
 variant: $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o $(LIBDIR)/minsnap.o
-	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(CSRC)/impc_qp.hip -o $(LIBDIR)/impc_qp_$(V).o
+	$(HIPCC) $(HIPFLAGS) $(call IDFLAGS,-$(V)) $(DEFS) -c $(CSRC)/impc_qp.hip -o $(LIBDIR)/impc_qp_$(V).o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(LIBDIR)/impc_qp_$(V).o $^ -o $(LIBDIR)/libimpc_qp_$(V).so $(LDLIBS)
 
 clean:

@@ -295,10 +295,11 @@ def main():
         qp_lat = None
 
     # results + parity-relevant statistics (outside the timed region)
-    iters_all, status_all, rho_all, recs = [], [], [], []
+    iters_all, status_all, rho_all, recs, results = [], [], [], [], []
     alg_bytes = alg_flops = 0.0
     for bk, b in batches:
         x, y, info = b.get()
+        results.append((x, y, info))
         pat = bk["pattern"]
         iters_all.append(info["iter"])
         status_all.append(info["status_val"])
@@ -336,26 +337,19 @@ def main():
     gbs = alg_bytes / (launch_ms * 1e-3) / 1e9
     values_mode = "shared" if len(nvar) == len(batches) else "full"
     nvar_desc = {str(bk["K"]): nv for (bk, _), nv in zip(batches, nvar)} if values_mode == "shared" else None
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_k_solve.json")
-    if os.path.exists(pmc_path):
-        try:
-            pm = json.load(open(pmc_path))
-            if pm.get("qps_per_launch") == total_qps and pm.get("kernel") == kernel_name and \
-                    pm.get("values", "full") == values_mode and pm.get("workload", "config3") == args.workload:
-                traffic = pm.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    build_id = impc.lib.impc_build_id().decode()
+    traffic, traffic_src = measured_traffic(build_id, total_qps, kernel_name, values_mode, args.workload)
 
     e2e = end_to_end(impc, ctx, batches, args, grouped) if args.e2e_steps > 0 else None
 
-    cpu = None
+    cpu = parity = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        cpu = cpu_baseline(bks, settings, args.cpu_sample, args.cpu_threads)
+        cpu, ref = cpu_baseline(bks, settings, args.cpu_sample, args.cpu_threads)
+        parity = parity_vs_oracle(results, ref)
         if args.cpu_all_cores:
             cores = len(os.sched_getaffinity(0))
-            allc = cpu_baseline(bks, settings, min(total_qps, args.cpu_sample * max(1, cores // args.cpu_threads)),
-                                cores)
+            allc, _ = cpu_baseline(bks, settings, min(total_qps, args.cpu_sample * max(1, cores // args.cpu_threads)),
+                                   cores)
             cpu["all_cores"] = {k: allc[k] for k in ("value", "unit", "cores", "sample")}
             cpu["all_cores"]["cgroup_cpu_quota"] = cpu_quota()
             cpu["all_cores"]["what"] = ("one oracle thread per CPU of os.sched_getaffinity(0); the box's cgroup "
@@ -416,13 +410,16 @@ def main():
             "unit": "TFLOP/s",
             "frac": tflops / PEAK_FP64_TFLOPS,
             "traffic": traffic,
+            "traffic_source": traffic_src,
             "kernel": kernel_name,
+            "build_id": build_id,
             "algorithmic_flops_per_launch": alg_flops,
             "what": "SURVEY.md 8d F_iter x each QP's iterations + 3.7k N per QP, over the mean event-timed launch",
             "hbm": {"achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
                     "algorithmic_bytes_per_launch": alg_bytes, "traffic_bytes_per_launch": traffic},
         },
         "cpu_baseline": cpu,
+        "parity": parity,
         "e2e": e2e,
         "selection": sel,
         "cost_allgather": gathered,
@@ -462,23 +459,66 @@ def select_candidates(impc, scenarios, ctx, buckets, batch_by_k, pd_params):
             "picked_histogram": [int(v) for v in picks]}
 
 
+def measured_traffic(build_id, qps, kernel, values_mode, workload):
+    """HBM bytes per launch from the committed PMC summary (tools/pmc_summary.py), only when it was
+    measured on this very library (its build_id equals impc_build_id()) and this workload; else
+    (None, reason)."""
+    path = os.path.join(ROOT, "profiles", "pmc_k_solve.json")
+    try:
+        pm = json.load(open(path))
+    except (OSError, ValueError):
+        return None, "no PMC summary (profiles/pmc_k_solve.json)"
+    if pm.get("build_id") != build_id:
+        return None, f"PMC summary is of build {pm.get('build_id')}, not the loaded library {build_id}"
+    if pm.get("qps_per_launch") != qps or pm.get("kernel") != kernel or pm.get("values", "full") != values_mode or \
+            pm.get("workload", "config3") != workload:
+        return None, "PMC summary is of another workload / kernel / value mode"
+    return pm.get("hbm_bytes_per_launch"), f"profiles/pmc_k_solve.json (build {build_id}, {pm.get('source', '')})"
+
+
+def parity_vs_oracle(results, ref):
+    """The benched launch's results for the QPs the CPU baseline solved (the first k of each
+    bucket) against the oracle's: identical status and iteration count, x and y within 1e-5
+    relative (BASELINE.json north_star; inf-norm per QP, over QPs with a solution)."""
+    n = st_eq = it_eq = 0
+    worst_x = worst_y = 0.0
+    for (x, y, info), (k, xo, yo, io) in zip(results, ref):
+        x, y, info = x[:k], y[:k], info[:k]
+        n += k
+        st_eq += int((info["status_val"] == io["status_val"]).sum())
+        it_eq += int((info["iter"] == io["iter"]).sum())
+        ok = np.isin(io["status_val"], (1, 2, -2, -6))
+        if ok.any():
+            rx = np.abs(x - xo).max(axis=1) / np.maximum(np.abs(xo).max(axis=1), 1e-12)
+            ry = np.abs(y - yo).max(axis=1) / np.maximum(np.abs(yo).max(axis=1), 1e-12)
+            worst_x = max(worst_x, float(rx[ok].max()))
+            worst_y = max(worst_y, float(ry[ok].max()))
+    return {"qps": n, "status_equal": st_eq, "iter_equal": it_eq, "max_rel_x": worst_x, "max_rel_y": worst_y,
+            "tolerance": 1e-5, "pass": bool(st_eq == n and it_eq == n and worst_x <= 1e-5 and worst_y <= 1e-5),
+            "what": "the timed launch's x, y, status, iterations for the CPU baseline's QPs vs the oracle "
+                    "(C restatement of OSQP 0.6.2; parity unpinned against the real libosqp, DESIGN.md 3)"}
+
+
 def cpu_baseline(bks, settings, sample, threads):
     """The oracle (C restatement of OSQP 0.6.2, reference per-call pattern: setup + warm start +
     solve per QP) on `threads` host threads of the GPU box, over a bounded sample of the same
-    workload (the first QPs of each bucket, bucket-proportional)."""
+    workload (the first QPs of each bucket, bucket-proportional).  Returns (line object,
+    [(k, x, y, info) per bucket])."""
     from oracle import osqp_oracle as ora
     total = sum(bk["values"]["q"].shape[0] for bk in bks)
     s = ora.settings_from(settings)
     t_all, n_all = 0.0, 0
+    ref = []
     for bk in bks:
         B = bk["values"]["q"].shape[0]
         k = min(B, max(1, int(round(sample * B / total))))
         v = bk["values"]
         t = time.perf_counter()
-        ora.solve_batch(bk["pattern"], v["Px"][:k], v["q"][:k], v["Ax"][:k], v["l"][:k], v["u"][:k], s,
-                        x_ws=None if bk.get("x_ws") is None else bk["x_ws"][:k], threads=threads)
+        xo, yo, io = ora.solve_batch(bk["pattern"], v["Px"][:k], v["q"][:k], v["Ax"][:k], v["l"][:k], v["u"][:k], s,
+                                     x_ws=None if bk.get("x_ws") is None else bk["x_ws"][:k], threads=threads)
         t_all += time.perf_counter() - t
         n_all += k
+        ref.append((k, xo, yo, io))
     # per-QP latency on one thread, the reference's own measures (SURVEY.md 8d): solveProblem only
     # (mpcPlanner.cpp:512-520) and setup + warm start + solve
     lat_s, lat_all = [], []
@@ -500,7 +540,7 @@ def cpu_baseline(bks, settings, sample, threads):
     return {"value": n_all / t_all, "unit": "QP-solves/s", "cores": threads, "kind": "port", "single_qp": single,
             "host_cpus": os.cpu_count(), "cpu_model": cpu_info(),
             "sample": f"{n_all} QPs of the same workload (first of each bucket), one setup+warm-start+solve "
-                      f"per QP, {threads} threads ({t_all:.1f} s wall)"}
+                      f"per QP, {threads} threads ({t_all:.1f} s wall)"}, ref
 
 
 if __name__ == "__main__":

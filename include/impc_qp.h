@@ -108,8 +108,12 @@ void impc_default_settings(impc_settings *s);
 /* Message of the last error on this host thread. */
 const char *impc_last_error(void);
 
-/* Library/ABI version string. */
+/* Library/ABI version string (with the git revision the library was built at). */
 const char *impc_version(void);
+/* Build identity of this library: "src-<16 hex>" = a hash of every source file compiled into it
+   and the compiler flags (kernel switches included).  Profiles record it (under profiles/); bench.py
+   quotes measured HBM traffic only from a PMC summary whose build id equals the loaded library's. */
+const char *impc_build_id(void);
 
 int impc_ctx_create(int device, impc_ctx *out);
 int impc_ctx_destroy(impc_ctx ctx);

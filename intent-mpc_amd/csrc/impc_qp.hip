@@ -33,7 +33,13 @@
 #include "queue.hpp"
 #include "symbolic.hpp"
 
-#define IMPC_VERSION "impc_qp 0.2.0 (OSQP 0.6.2 semantics, gfx950)"
+#ifndef IMPC_BUILD_ID  // set by the Makefile: hash of the compiled sources and flags
+#define IMPC_BUILD_ID "src-unknown"
+#endif
+#ifndef IMPC_GIT_REV
+#define IMPC_GIT_REV "unknown"
+#endif
+#define IMPC_VERSION "impc_qp 0.3.0 (OSQP 0.6.2 semantics, gfx950, git " IMPC_GIT_REV ")"
 
 namespace {
 
@@ -1145,6 +1151,7 @@ void impc_default_settings(impc_settings *s) {
 
 const char *impc_last_error(void) { return g_last_error.c_str(); }
 const char *impc_version(void) { return IMPC_VERSION; }
+const char *impc_build_id(void) { return IMPC_BUILD_ID; }
 
 int impc_ctx_create(int device, impc_ctx *out) {
     if (!out) return fail(IMPC_INVALID_ARGUMENT, "null output pointer");

@@ -92,6 +92,7 @@ def _sig(name, res, *args):
 _sig("impc_default_settings", None, C.POINTER(Settings))
 _sig("impc_last_error", C.c_char_p)
 _sig("impc_version", C.c_char_p)
+_sig("impc_build_id", C.c_char_p)
 _sig("impc_ctx_create", C.c_int, C.c_int, C.POINTER(_P))
 _sig("impc_ctx_destroy", C.c_int, _P)
 _sig("impc_ctx_stream", _P, _P)
@@ -216,7 +217,7 @@ KERNEL_AUTO, KERNEL_GENERIC, KERNEL_STRUCTURED = 0, 1, 2
 QUEUE_FIFO, QUEUE_LONGEST_FIRST = 0, 1
 
 EXPORTED = [
-    "impc_default_settings", "impc_last_error", "impc_version", "impc_ctx_create", "impc_ctx_destroy",
+    "impc_default_settings", "impc_last_error", "impc_version", "impc_build_id", "impc_ctx_create", "impc_ctx_destroy",
     "impc_ctx_stream", "impc_ctx_synchronize", "impc_batch_create", "impc_batch_destroy", "impc_batch_set_settings",
     "impc_batch_set_values", "impc_batch_set_values_device", "impc_batch_set_values_shared", "impc_batch_warm_start", "impc_batch_setup",
     "impc_batch_solve", "impc_batch_get", "impc_batch_device_results", "impc_batch_update_lin_cost",

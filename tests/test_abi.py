@@ -55,6 +55,8 @@ def test_default_settings_are_osqp_defaults():
 
 def test_version_string():
     assert impc.lib.impc_version().decode().startswith("impc")
+    bid = impc.lib.impc_build_id().decode()
+    assert bid.startswith("src-") and len(bid) >= 20 and bid != "src-unknown", bid
 
 
 def test_no_device_fails_loudly():
