@@ -155,6 +155,15 @@ int impc_batch_set_values_shared(impc_batch b, const double *Px, const double *A
  * structured kernel with a persistent workspace) it replaces the iterates and keeps scaling, rho
  * and factor.  Pass x = NULL to clear a pending warm start (the next setup cold-starts). */
 int impc_batch_warm_start(impc_batch b, const double *x, const double *y);
+/* The same from DEVICE arrays (QP-major x [B][n], y [B][m] or NULL = zero duals): the copies are
+ * queued on the context stream after every launch already issued, no host synchronisation (the
+ * closed replan loop hands each candidate the previous winner this way). */
+int impc_batch_warm_start_device(impc_batch b, const double *x, const double *y);
+/* Solve only the first `count` QPs of the batch (1 <= count <= B; B after create): a batch
+ * created once at a capacity serves smaller per-call sets (a replan's single-solve instances, the
+ * OsqpEigen front end's workspace pool).  Rows >= count are not read or written by the solves;
+ * their results keep whatever they held.  Changing the count discards a persistent workspace. */
+int impc_batch_set_active(impc_batch b, int64_t count);
 
 /* osqp_setup's numeric part on the device: Ruiz scaling, rho vector, KKT assembly and
  * factorisation, then the pending warm start.  Asynchronous on `stream` (NULL = ctx stream). */

@@ -26,6 +26,7 @@
 #include "../../include/impc_fanout.h"
 #include "../../include/impc_predict.h"
 #include "../../include/impc_comm.h"
+#include "../../include/impc_replan.h"
 #include "mpc_qp_internal.hpp"
 #include "admm_core.hpp"
 #include "mpc_structure.hpp"
@@ -566,6 +567,7 @@ struct impc_batch_s {
     int64_t n = 0, m = 0, nnzP = 0, nnzA = 0;
     std::vector<int64_t> Pp, Pi, Ap, Ai;  // pattern (host copy)
     int64_t B = 0, S = 0;
+    int64_t Bact = 0;  // QPs the solves take (impc_batch_set_active): the first Bact of B
     impc_settings settings{};
     impc::DevSettings dst{};
     int kernel_req = IMPC_KERNEL_AUTO;
@@ -685,7 +687,7 @@ int deinterleave(impc_batch b, const double *src, double *dst_dev, int64_t len, 
 
 // The structured kernel's view of a batch's inputs / outputs.
 impc::WaveIO wave_io(impc_batch b) {
-    impc::WaveIO io{b->B,        b->shared ? b->d_shPx : b->in_Px, b->in_q, b->shared ? b->d_shAx : b->in_Ax,
+    impc::WaveIO io{b->Bact,     b->shared ? b->d_shPx : b->in_Px, b->in_q, b->shared ? b->d_shAx : b->in_Ax,
                     b->in_l,     b->in_u,   b->in_xws, b->in_yws, b->has_ws ? (b->ws_y ? 1 : 2) : 0, b->d_xout, b->d_yout,
                     b->d_scal,   b->d_info};
     if (b->profile && b->d_qpt) io.qpt = b->d_qpt;
@@ -822,7 +824,7 @@ int generic_setup(impc_batch b, hipStream_t st) {
         if ((rc = interleave(b, b->in_yws, const_cast<double *>(w.yws), b->m, st))) return rc;
     }
     if (b->profile) HIP_OK(hipEventRecord(b->ev[0], st));
-    hipLaunchKernelGGL(k_setup, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk, b->dst, b->B,
+    hipLaunchKernelGGL(k_setup, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk, b->dst, b->Bact,
                        b->has_ws ? 1 : 0);
     HIP_OK(hipGetLastError());
     if (b->profile) {
@@ -845,7 +847,7 @@ int generic_solve(impc_batch b, hipStream_t st) {
     b->generic_first_run = false;
     b->dwk.tlim = b->tlim_on ? b->d_tlim : nullptr;
     if (b->profile) HIP_OK(hipEventRecord(b->ev[2], st));
-    hipLaunchKernelGGL(k_solve, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk, b->dst, b->B,
+    hipLaunchKernelGGL(k_solve, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk, b->dst, b->Bact,
                        first_run);
     HIP_OK(hipGetLastError());
     if (b->profile) HIP_OK(hipEventRecord(b->ev[3], st));
@@ -886,7 +888,7 @@ int launch_wave_w(impc_batch b, hipStream_t st, const impc::WaveIO &io, const ui
     using LD = impc::WaveLds<kTeam, VS, GS>;
     const size_t lds = sizeof(double) * (size_t)LD::size(b->wt);  // products sized by the pattern
     if (int rc = ensure_lds_attr(k_mpc_wave<kTeam, VS, GS, WPS, WF>, lds)) return rc;
-    const int64_t groups = resident_groups<VS>(b->ctx->num_cu, lds, b->B);
+    const int64_t groups = resident_groups<VS>(b->ctx->num_cu, lds, b->Bact);
     hipLaunchKernelGGL((k_mpc_wave<kTeam, VS, GS, WPS, WF>), dim3((unsigned)groups), dim3(kTeam), lds, st, b->wt, io,
                        b->dst, b->d_counter, ord);
     HIP_OK(hipGetLastError());
@@ -958,17 +960,17 @@ int queue_order(impc_batch *bs, const int64_t *firsts, int count, int64_t total,
     void *t = (void *)(out + h->qscr_cap);
     for (int k = 0; k < count; k++) {
         impc_batch b = bs[k];
-        if (b->B == 0) continue;
+        if (b->Bact == 0) continue;
         IMPC_TRY(build_queue_csr(b));
         impc::QueueKeyArgs a{};
-        a.B = b->B, a.n = b->n, a.m = b->m, a.first = firsts[k];
+        a.B = b->Bact, a.n = b->n, a.m = b->m, a.first = firsts[k];
         a.row_ptr = b->d_csr, a.row_col = b->d_csr + b->m + 1, a.row_ent = b->d_csr + b->m + 1 + b->nnzA;
         a.shared = b->shared ? 1 : 0;
         a.Ax = b->shared ? b->d_shAx : b->in_Ax;
         a.nvar = b->nvar, a.vmap = b->d_vmap, a.Ax_var = b->d_Axv;
         a.q = b->in_q, a.l = b->in_l, a.u = b->in_u, a.xws = b->in_xws, a.has_ws = b->has_ws ? 1 : 0;
         a.q_weight = b->queue_qw;
-        const unsigned grid = (unsigned)std::min<int64_t>(b->B, 4096);
+        const unsigned grid = (unsigned)std::min<int64_t>(b->Bact, 4096);
         hipLaunchKernelGGL(impc::k_queue_key, dim3(grid), dim3(256), 0, st, a, key, idx);
         HIP_OK(hipGetLastError());
     }
@@ -999,7 +1001,7 @@ int structured_solve(impc_batch b, hipStream_t st) {
     if (b->profile) HIP_OK(hipEventRecord(b->ev[2], st));
     const uint32_t *ord = nullptr;
     const int64_t first0 = 0;
-    IMPC_TRY(queue_order(&b, &first0, 1, b->B, st, &ord));
+    IMPC_TRY(queue_order(&b, &first0, 1, b->Bact, st, &ord));
     int rc;
     switch (b->vs * 8 + b->gs) {
         case kWaveVS * 8 + 2: rc = launch_wave<kWaveVS, 2>(b, st, io, ord); break;
@@ -1227,7 +1229,7 @@ int impc_batch_create(impc_ctx ctx, int64_t n, int64_t m, const int64_t *Pp, con
     b->Pi.assign(Pi ? Pi : Pp, Pi ? Pi + b->nnzP : Pp);
     b->Ap.assign(Ap, Ap + n + 1);
     b->Ai.assign(Ai, Ai + b->nnzA);
-    b->B = batch;
+    b->B = b->Bact = batch;
     b->S = (batch + kBlock - 1) / kBlock * kBlock;
     impc_default_settings(&b->settings);
     to_dev_settings(&b->settings, &b->dst);
@@ -1448,6 +1450,46 @@ int impc_batch_warm_start(impc_batch b, const double *x, const double *y) {
     return IMPC_OK;
 }
 
+int impc_batch_warm_start_device(impc_batch b, const double *x, const double *y) {
+    if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
+    HIP_OK(hipSetDevice(b->ctx->device));
+    if (!x) return impc_batch_warm_start(b, nullptr, nullptr);
+    hipStream_t st = b->ctx->stream;
+    // queued after every launch on every stream this context has used: none of them still reads
+    // the warm-start arrays when the copies land
+    IMPC_TRY(ctx_order_after_all(b->ctx, st));
+    const size_t B = (size_t)b->B;
+    HIP_OK(hipMemcpyAsync(b->in_xws, x, sizeof(double) * b->n * B, hipMemcpyDeviceToDevice, st));
+    if (b->m && y) HIP_OK(hipMemcpyAsync(b->in_yws, y, sizeof(double) * b->m * B, hipMemcpyDeviceToDevice, st));
+    b->ws_y = y != nullptr;
+    b->settings.warm_start = 1;  // as impc_batch_warm_start (osqp_warm_start)
+    b->dst.warm_start = 1;
+    if (!use_structured(b) && b->generic_setup_done && !b->generic_dirty) {
+        int rc = interleave(b, b->in_xws, const_cast<double *>(b->dwk.xws), b->n, st);
+        if (!rc && !b->ws_y && b->m) HIP_OK(hipMemsetAsync(b->in_yws, 0, sizeof(double) * b->m * B, st));
+        if (!rc) rc = interleave(b, b->in_yws, const_cast<double *>(b->dwk.yws), b->m, st);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_warm_start, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk,
+                           b->dst, b->Bact);
+        HIP_OK(hipGetLastError());
+        return IMPC_OK;
+    }
+    b->has_ws = true;
+    b->generic_dirty = true;
+    return IMPC_OK;
+}
+
+int impc_batch_set_active(impc_batch b, int64_t count) {
+    if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
+    if (count < 1 || count > b->B) return fail(IMPC_INVALID_ARGUMENT, "active count must be in [1, B]");
+    if (count != b->Bact) {
+        b->Bact = count;
+        b->persist_valid = b->q_by_update = false;  // the stored workspaces cover other QPs
+        b->generic_dirty = true;
+    }
+    return IMPC_OK;
+}
+
 int impc_batch_setup(impc_batch b, void *stream) {
     if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
     if (!b->values_set) return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "values not set");
@@ -1517,7 +1559,7 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
         e.io = wave_io(b);
         e.st = b->dst;
         e.first = L.total;
-        L.total += b->B;
+        L.total += b->Bact;
         b->ev_solve = false;
         b->ev_setup = false;
     }
@@ -1886,3 +1928,6 @@ int impc_copy_to_host(impc_ctx ctx, void *dst, const void *src, int64_t bytes) {
 
 // ---------------------------------------------------------------- reference trajectory (getXRef)
 #include "reftraj.hpp"
+
+// ---------------------------------------------------------------- replan state (impc_replan.h)
+#include "replan.hpp"

@@ -1,0 +1,64 @@
+// replan.hpp -- the planner state a batched makePlanWithPred carries on the device between replans
+// (include/impc_replan.h), included by impc_qp.hip.  One workgroup per committed instance: the
+// plan's n values are copied by its lanes into the instance's warm start (plan_x) and states
+// (plan_states), lane 0 sets the flags.  Reference: mpcPlanner.cpp:636-639 (fan-out branch) and
+// :653-657 (single solve): currentStatesSol_ / currentControlsSol_ = the plan, firstTime_ = false.
+#pragma once
+
+namespace impc_replan {
+
+__global__ __launch_bounds__(256) void k_commit(int32_t N, int64_t n, int64_t count, const int64_t *__restrict__ inst,
+                                                const uint64_t *__restrict__ x_cand, int32_t ncand,
+                                                const int32_t *__restrict__ best, const double *__restrict__ x_rows,
+                                                const impc_info *__restrict__ info_rows, double *__restrict__ plan_x,
+                                                double *__restrict__ plan_states, int32_t *__restrict__ prev_count,
+                                                int8_t *__restrict__ first_time, int8_t *__restrict__ valid) {
+    for (int64_t r = blockIdx.x; r < count; r += gridDim.x) {
+        const int64_t i = inst[r];
+        const double *src = nullptr;
+        if (x_cand) {
+            const int32_t c = best[r];
+            if (c >= 0 && c < ncand) src = (const double *)x_cand[r * ncand + c];
+        } else if (info_rows[r].status_val != IMPC_NON_CVX) {  // solveTraj's successSolve (:513-518)
+            src = x_rows + r * n;
+        }
+        if (src) {
+            for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
+                const double v = src[k];
+                plan_x[i * n + k] = v;
+                if (k < 8 * (int64_t)N) plan_states[i * 8 * (int64_t)N + k] = v;
+            }
+        }
+        if (threadIdx.x == 0) {
+            valid[i] = src ? 1 : 0;
+            if (src) {
+                first_time[i] = 0;
+                prev_count[i] = N;
+            }
+        }
+    }
+}
+
+}  // namespace impc_replan
+
+extern "C" int impc_replan_commit_device(impc_ctx ctx, int32_t horizon, int64_t n, int64_t count, const int64_t *inst,
+                                         const uint64_t *x_cand, int32_t ncand, const int32_t *best_cand,
+                                         const double *x_rows, const impc_info *info_rows, double *plan_x,
+                                         double *plan_states, int32_t *prev_count, int8_t *first_time, int8_t *valid,
+                                         void *stream) {
+    if (!ctx || horizon < 2 || n != 13 * (int64_t)horizon - 5 || count < 0)
+        return fail(IMPC_INVALID_ARGUMENT, "replan commit: n must be 13 horizon - 5, count >= 0");
+    if (!count) return IMPC_OK;
+    if (!inst || !plan_x || !plan_states || !prev_count || !first_time || !valid ||
+        (x_cand ? (!best_cand || ncand < 1 || x_rows) : (!x_rows || !info_rows)))
+        return fail(IMPC_INVALID_ARGUMENT, "replan commit: one of x_cand (+ best_cand) or x_rows (+ info_rows)");
+    HIP_OK(hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    // after the solves and the selection, wherever they ran
+    IMPC_TRY(ctx_order_after_all(ctx, st));
+    const unsigned blocks = (unsigned)std::min<int64_t>(count, (int64_t)ctx->num_cu * 8);
+    hipLaunchKernelGGL(impc_replan::k_commit, dim3(blocks), dim3(256), 0, st, horizon, n, count, inst, x_cand, ncand,
+                       best_cand, x_rows, info_rows, plan_x, plan_states, prev_count, first_time, valid);
+    HIP_OK(hipGetLastError());
+    return ctx_note_launch(ctx, st);
+}

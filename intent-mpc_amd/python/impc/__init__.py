@@ -104,6 +104,11 @@ _sig("impc_batch_set_values", C.c_int, _P, _dp, _dp, _dp, _dp, _dp)
 _sig("impc_batch_set_values_device", C.c_int, _P, _P, _P, _P, _P, _P)
 _sig("impc_batch_set_values_shared", C.c_int, _P, _dp, _dp, C.c_int64, _i64p, _dp, _dp, _dp, _dp)
 _sig("impc_batch_warm_start", C.c_int, _P, _dp, _dp)
+_sig("impc_batch_warm_start_device", C.c_int, _P, _P, _P)
+_sig("impc_batch_set_active", C.c_int, _P, C.c_int64)
+_sig("impc_gather_rows_device", C.c_int, _P, _P, C.c_int64, _P, C.c_int64, _P, _P)
+_sig("impc_replan_commit_device", C.c_int, _P, C.c_int32, C.c_int64, C.c_int64, _P, _P, C.c_int32, _P, _P, _P, _P, _P,
+     _P, _P, _P, _P)
 _sig("impc_batch_setup", C.c_int, _P, _P)
 _sig("impc_batch_solve", C.c_int, _P, _P)
 _sig("impc_batch_get", C.c_int, _P, _dp, _dp, C.c_void_p)
@@ -233,7 +238,8 @@ EXPORTED = [
     "impc_minsnap_corridor_bounds",
     "impc_reference_traj_device", "impc_repeat_rows_device", "impc_comm_unique_id", "impc_comm_create", "impc_comm_destroy", "impc_comm_allgather", "impc_comm_gather_info",
     "impc_comm_max", "impc_ctx_timer_mark", "impc_ctx_timer_read", "impc_batch_set_time_limits",
-    "impc_ctx_clock_rate", "impc_ctx_clock_check", "impc_batch_set_queue_order",
+    "impc_ctx_clock_rate", "impc_ctx_clock_check", "impc_batch_set_queue_order", "impc_batch_warm_start_device",
+    "impc_batch_set_active", "impc_gather_rows_device", "impc_replan_commit_device",
 ]
 
 
@@ -360,6 +366,15 @@ class Batch:
         if ya is not None and ya.size != self.B * self.m:
             raise ValueError(f"warm_start: y has {ya.size} values, expected B*m = {self.B * self.m}")
         _check(lib.impc_batch_warm_start(self.h, _d(xa), _d(ya)), "impc_batch_warm_start")
+
+    def warm_start_device(self, x_ptr, y_ptr=None):
+        """impc_batch_warm_start_device: QP-major device arrays x [B][n] (y [B][m] or None = 0)."""
+        _check(lib.impc_batch_warm_start_device(self.h, _P(x_ptr) if x_ptr else None, _P(y_ptr) if y_ptr else None),
+               "impc_batch_warm_start_device")
+
+    def set_active(self, count):
+        """impc_batch_set_active: the solves take the first `count` QPs."""
+        _check(lib.impc_batch_set_active(self.h, int(count)), "impc_batch_set_active")
 
     def setup(self, stream=None):
         _check(lib.impc_batch_setup(self.h, stream), "impc_batch_setup")
@@ -671,6 +686,12 @@ def repeat_rows_device(ctx, src_ptr, rows, row_bytes, repeat, dst_ptr, stream=No
     """impc_repeat_rows_device: dst row r * repeat + c = src row r (device pointers)."""
     _check(lib.impc_repeat_rows_device(ctx.h, _P(src_ptr), int(rows), int(row_bytes), int(repeat), _P(dst_ptr),
                                        _P(stream) if stream else None), "impc_repeat_rows_device")
+
+
+def gather_rows_device(ctx, src_ptr, row_bytes, idx_ptr, count, dst_ptr, stream=None):
+    """impc_gather_rows_device: dst row r = src row idx[r] (device pointers, idx int64)."""
+    _check(lib.impc_gather_rows_device(ctx.h, _P(src_ptr), int(row_bytes), _P(idx_ptr), int(count), _P(dst_ptr),
+                                       _P(stream) if stream else None), "impc_gather_rows_device")
 
 
 def comm_unique_id():

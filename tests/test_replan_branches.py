@@ -1,0 +1,148 @@
+"""makePlanWithPred's two branches in the batched replan, and the planner state carried between
+replans on the device (impc.replan.DeviceReplan + PlanState, include/impc_replan.h), against the
+restatement oracle/replan_ref.py (mpcPlanner.cpp:571-661).
+
+One mixed batch of instances: on a first plan with and without predictions, with predictions
+(the fan-out), without predictions and with / without current dynamic obstacles.  Per replan and
+instance: the branch taken; the fan-out's closest obstacle and candidate order; every assembled
+QP bit for bit (restatement of solveTraj's assembly with the instance's own warm start and
+linearisation point); every solution against the OSQP oracle (identical status and iterations,
+1e-5); the selection, recomputed by the restatement on the GPU's solutions, bit for bit; the
+committed plan (the chosen solution, bitwise) and firstTime_.  Three chained replans: the second
+and third start from the state the device committed (x0 from the plan's next state, predictions
+advanced one step), so first-plan instances move on to the fan-out.  Parity of the solutions
+unpinned against the real libosqp."""
+import numpy as np
+import pytest
+
+import impc
+from impc import scenarios
+from impc.replan import FANOUT, SINGLE_CURRENT, SINGLE_FIRST, DeviceReplan, PlanState
+from oracle import replan_ref as ref
+
+from helpers import compare
+
+I, K, N = 24, 3, 20
+
+
+def _scenario(seed=4242):
+    buckets = scenarios.intent_config(N=N, K=K, instances=I, hyps=6, seed=seed)
+    inst = next(iter(buckets.values()))["instances"]
+    p, pd = impc.mpc_params(horizon=N)
+    pred_size = np.broadcast_to(inst["size"], inst["pred"].shape).copy()
+    return p, pd, inst, pred_size
+
+
+def test_branch_table():
+    """:606 -- fan-out only with predictions and not firstTime_; a first plan never keeps obstacles."""
+    assert ref.branch(0, True) == ref.FANOUT
+    assert ref.branch(1, True) == ref.SINGLE_FIRST
+    assert ref.branch(1, False, 3) == ref.SINGLE_FIRST
+    assert ref.branch(0, False, 0) == ref.SINGLE_FIRST
+    assert ref.branch(0, False, 3) == ref.SINGLE_CURRENT
+    from impc.replan import branches
+    got = branches([0, 1, 1, 0, 0], [1, 1, 0, 0, 0], [0, 0, 3, 0, 3])
+    np.testing.assert_array_equal(got, [FANOUT, SINGLE_FIRST, SINGLE_FIRST, SINGLE_FIRST, SINGLE_CURRENT])
+
+
+def test_oracle_chain_first_plan_then_fanout():
+    """CPU: the restatement's state machine -- a first-plan instance solves the obstacle-free QP,
+    commits it, and fans out on the next replan (warm-started from that plan)."""
+    p, pd, inst, pred_size = _scenario(seed=11)
+    s = impc.default_settings(verbose=0)
+    i = 0
+    st = dict(first_time=1, plan_x=None)
+    r1 = ref.make_plan_with_pred(pd, pd, s, st, inst["pos"][i], inst["vel"][i], inst["xref"][i], inst["obp"][i],
+                                 inst["pred"][i], pred_size[i], inst["prob_all"][i], True)
+    assert r1["branch"] == ref.SINGLE_FIRST and r1["valid"] and st["first_time"] == 0
+    np.testing.assert_array_equal(st["plan_x"], r1["x"])
+    r2 = ref.make_plan_with_pred(pd, pd, s, st, inst["pos"][i], inst["vel"][i], inst["xref"][i], inst["obp"][i],
+                                 inst["pred"][i], pred_size[i], inst["prob_all"][i], True)
+    assert r2["branch"] == ref.FANOUT and r2["valid"] and 0 <= r2["best"] < 6
+
+
+def _check_replan(out, before, pos, vel, xref, dyn_cur, pred, pred_size, prob, has_pred, cur_size, cur_count, pd, s):
+    plan_x, first, _, _ = before
+    for i in range(I):
+        assert out["branch"][i] == ref.branch(first[i], has_pred[i], cur_count[i]), i
+    expect = plan_x.copy()
+    expect_first = first.copy()
+
+    def check_qp(pat_vals, rows_vals, msg):
+        pat, vals = pat_vals
+        for key, got in zip(("Px", "q", "Ax", "l", "u"), rows_vals):
+            np.testing.assert_array_equal(got, vals[key], err_msg=f"{msg} {key}")
+
+    for j, i in enumerate(out["inst_fanout"]):
+        px = plan_x[i] if out["branch"][i] == FANOUT else None
+        fo, qps = ref.fanout_qps(pd, 0, px, pos[i], vel[i], xref[i], dyn_cur[i], pred[i], pred_size[i], prob[i])
+        assert out["ob_idx"][i] == fo["ob_idx"], i
+        np.testing.assert_array_equal(out["cand_type"][i], fo["types"])
+        xs, stats = [], []
+        for c in range(6):
+            slot = out["cand_slot"][i][c]
+            nm, row = ("single", 4 * j + slot) if slot < 4 else ("pair", 2 * j + slot - 4)
+            x, info = out["x_" + nm][row], out["info_" + nm][row]
+            check_qp(qps[c][:2], [v[row] for v in out["vals_" + nm]], f"instance {i} candidate {c}")
+            xo, yo, io = ref.solve(*qps[c], s)
+            compare((x[None], out["y_" + nm][row][None], info[None]), (xo[None], yo[None], io[None]))
+            xs.append(x)
+            stats.append(int(info["status_val"]))
+        best = ref.select(pd, pd, 0, px, xref[i], fo, xs, stats, prob[i][fo["ob_idx"]])
+        assert out["best_cand"][i] == best, (i, out["best_cand"][i], best)
+        if best >= 0:
+            expect[i] = xs[best]
+            expect_first[i] = 0
+    for nm, idx, br in (("first", out["inst_first"], SINGLE_FIRST), ("current", out["inst_current"], SINGLE_CURRENT)):
+        for j, i in enumerate(idx):
+            cur = br == SINGLE_CURRENT
+            pat, vals, ws = ref.single_qp(pd, first[i], plan_x[i], pos[i], vel[i], xref[i],
+                                          dyn_cur[i] if cur else None, cur_size[i] if cur else None)
+            check_qp((pat, vals), [v[j] for v in out["vals_" + nm]], f"instance {i} single ({nm})")
+            x, info = out["x_" + nm][j], out["info_" + nm][j]
+            xo, yo, io = ref.solve(pat, vals, ws, s)
+            compare((x[None], out["y_" + nm][j][None], info[None]), (xo[None], yo[None], io[None]))
+            if int(info["status_val"]) != ref.NON_CVX:
+                expect[i] = x
+                expect_first[i] = 0
+    return expect, expect_first
+
+
+@pytest.mark.gpu
+def test_mixed_branches_three_chained_replans(ctx):
+    p, pd, inst, pred_size = _scenario()
+    s = impc.default_settings(verbose=0)
+    L = inst["pred"].shape[3]
+    idx = np.arange(I)
+    first = (idx % 4 == 0).astype(np.int8)                   # first plans (half of them with predictions)
+    has_pred = [idx % 3 != 1, idx % 5 != 2, idx % 7 != 3]    # per replan: obPredPos_ non-empty
+    cur_count = np.where(idx % 2 == 0, K, 0)                  # current obstacles kept without predictions
+    cur_size = np.broadcast_to(inst["size"], (I, K, 3)).copy()
+    state = PlanState(ctx, I, N, inst["prev"], first, np.full(I, N, np.int32))
+    rp = DeviceReplan(ctx, p, pd, I, K, L, s)
+    pos, vel, pred = inst["pos"].copy(), inst["vel"].copy(), inst["pred"].copy()
+    seen = set()
+    try:
+        for step in range(3):
+            before = state.plans()
+            dyn_cur = pred[:, :, 0, 0, :]                     # the obstacles' current positions
+            out = rp.run(pos, vel, inst["xref"], dyn_cur=dyn_cur, pred_pos=pred, pred_size=pred_size,
+                         prob=inst["prob_all"], state=state, has_pred=has_pred[step], cur_size=cur_size,
+                         cur_count=cur_count)
+            seen.update(int(b) for b in out["branch"])
+            expect, expect_first = _check_replan(out, before, pos, vel, inst["xref"], dyn_cur, pred, pred_size,
+                                                 inst["prob_all"], has_pred[step], cur_size, cur_count, pd, s)
+            plan_x, ft, pc, valid = state.plans()
+            np.testing.assert_array_equal(plan_x, expect)       # the committed plans, bitwise
+            np.testing.assert_array_equal(ft, expect_first)
+            assert (pc[ft == 0] == N).all()
+            # next replan: x0 = the plan's next state, predictions one step on
+            pos = np.where(valid[:, None] == 1, plan_x[:, 8:11], pos)
+            vel = np.where(valid[:, None] == 1, plan_x[:, 11:14], vel)
+            pred = np.concatenate([pred[:, :, :, 1:], pred[:, :, :, -1:]], axis=3)
+        assert seen == {FANOUT, SINGLE_FIRST, SINGLE_CURRENT}
+        # every first-plan instance with a plan fanned out on a later replan with predictions
+        assert (state.plans()[1] == 0).all()
+    finally:
+        rp.close()
+        state.close()

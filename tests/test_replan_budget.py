@@ -121,28 +121,6 @@ def test_budget_time_limit_and_cutoff(ctx):
 
 
 @pytest.mark.gpu
-def test_budget_no_time_limit_on_first_plan(ctx):
-    """setTimeLimit only when not firstTime_ (mpcPlanner.cpp:442-444): with instances alternating
-    first_time, a limit every QP would exceed stops only the candidates of the others."""
-    I = 16
-    ft = (np.arange(I) % 2).astype(np.int8)
-    p, pd, I, K, L, args = _scenario(I=I, first_time=ft)
-    rp = DeviceReplan(ctx, p, pd, I, K, L, impc.default_settings(verbose=0))
-    try:
-        free = rp.run(*args)
-        tiny = rp.run(*args, solver_time_limit=1e-9)
-        for nm, cnt in (("single", 4), ("pair", 2)):
-            first = np.repeat(ft == 1, cnt)
-            st = tiny["info_" + nm]["status_val"]
-            assert (st[first] != impc.TIME_LIMIT_REACHED).all()
-            np.testing.assert_array_equal(tiny["x_" + nm][first], free["x_" + nm][first])
-            np.testing.assert_array_equal(tiny["info_" + nm]["iter"][first], free["info_" + nm]["iter"][first])
-            assert (st[~first] == impc.TIME_LIMIT_REACHED).mean() >= 0.5
-    finally:
-        rp.close()
-
-
-@pytest.mark.gpu
 def test_per_qp_time_limits_generic_and_structured(ctx):
     """impc_batch_set_time_limits on both kernels: QPs with limit 0 run to completion bit-identically,
     QPs with a limit below their solve time stop with OSQP_TIME_LIMIT_REACHED; clearing restores

@@ -1,8 +1,14 @@
 """A whole makePlanWithPred replan on the device (impc.replan.DeviceReplan): intent fan-out ->
 on-device QP assembly of both candidate shapes -> one grouped solve -> candidate selection,
 against the host-built path of the same scenario (scenarios.intent_config, hypotheses 0-5 =
-getIntentComb's candidates, first-call closest obstacle).  Every stage must agree bit for bit:
-the candidate order, the assembled QP values, the solutions and the selected candidate."""
+getIntentComb's candidates, the distance-based closest obstacle).  Every stage must agree bit for
+bit: the candidate order, the assembled QP values, the solutions and the selected candidate.
+
+Every instance here is on the fan-out branch (not firstTime_, predictions present); its previous
+plan holds a single state (prev_count = 1), so findClosestObstacle takes its distance fallback
+(mpcPlanner.cpp:676-685) -- the scenario's closest obstacle -- while the QPs are linearised at and
+warm-started from the scenario's whole previous plan.  The branch selection itself is
+tests/test_replan_branches.py."""
 import numpy as np
 import pytest
 
@@ -25,10 +31,11 @@ def test_device_replan_matches_host_path(ctx):
     rp = DeviceReplan(ctx, p, pd, I, K, L, s)
     try:
         pred_size = np.broadcast_to(inst["size"], inst["pred"].shape).copy()
-        out = rp.run(inst["pos"], inst["vel"], inst["xref"], inst["prev"], np.ones(I, np.int8),
-                     np.full(I, N, np.int32), inst["obp"], inst["pred"], pred_size, inst["prob_all"])
+        out = rp.run(inst["pos"], inst["vel"], inst["xref"], inst["prev"], np.zeros(I, np.int8),
+                     np.ones(I, np.int32), inst["obp"], inst["pred"], pred_size, inst["prob_all"])
     finally:
         rp.close()
+    assert (out["branch"] == 0).all()
     assert np.array_equal(out["ob_idx"], inst["closest"])
     for nm, kk in (("single", K), ("pair", K + 1)):
         bk = buckets[kk]
@@ -53,8 +60,8 @@ def test_device_replan_matches_host_path(ctx):
         d = scenarios.selection_arrays(buckets, {kk: b.device_results()[0] for kk, b in batches.items()})
         params = dict(horizon=N, num_candidates=6, max_dynamic=d["kmax"], pred_len=d["L"], num_static=0, prev_len=N,
                       dynamic_safety_dist=pd["dynamic_safety_dist"], static_safety_dist=pd["static_safety_dist"])
-        ref = impc.select_best(ctx, params, d["x_ptrs"], np.ones((I, 6), np.int8), np.ones(I, np.int8), d["prev"],
-                               np.full(I, N, np.int32), d["xref"], np.zeros((I, 0, 3)), np.zeros((I, 0, 3)),
+        ref = impc.select_best(ctx, params, d["x_ptrs"], np.ones((I, 6), np.int8), np.zeros(I, np.int8), d["prev"],
+                               np.ones(I, np.int32), d["xref"], np.zeros((I, 0, 3)), np.zeros((I, 0, 3)),
                                d["dyn_count"], d["dyn_pos"], d["dyn_size"], d["prob"])
     finally:
         for b in batches.values():
@@ -86,7 +93,7 @@ def test_device_replan_from_paths(ctx):
     try:
         pos = inst["pos"].copy()
         for step in range(2):
-            out = rp.run(pos, inst["vel"], dev, inst["prev"], np.ones(I, np.int8), np.full(I, N, np.int32),
+            out = rp.run(pos, inst["vel"], dev, inst["prev"], np.zeros(I, np.int8), np.ones(I, np.int32),
                          inst["obp"], inst["pred"], pred_size, inst["prob_all"])
             exp = np.array([r.xref(pos[i]) for i, r in enumerate(refs)])
             assert np.array_equal(out["xref"], exp), step
@@ -115,8 +122,8 @@ def test_cpp_replan_example_matches_python_replan(ctx, tmp_path):
     L = inst["pred"].shape[3]
     s = impc.default_settings(verbose=0)
     pred_size = np.broadcast_to(inst["size"], inst["pred"].shape).copy()
-    first = np.ones(I, np.int8)
-    pcount = np.full(I, N, np.int32)
+    first = np.zeros(I, np.int8)
+    pcount = np.ones(I, np.int32)
     rp = DeviceReplan(ctx, p, pd, I, K, L, s)
     try:
         out = rp.run(inst["pos"], inst["vel"], inst["xref"], inst["prev"], first, pcount, inst["obp"], inst["pred"],
