@@ -21,7 +21,11 @@
  *
  * Each Solver owns a one-QP batch on a process-wide context (device IMPC_DEVICE, default 0); the
  * context belongs to the thread that first initialises a solver (the reference's single mpc
- * worker thread, mpcNavigation.cpp:177-178).  Differences from OsqpEigen, all benign for the
+ * worker thread, mpcNavigation.cpp:177-178).  The batch comes from the context's workspace pool
+ * (impc_batch_acquire / impc_batch_release): solveTraj builds a new Solver on every call
+ * (mpcPlanner.cpp:436, :527), and a Solver on a pattern the process has seen before takes a
+ * released batch's device buffers and analysis instead of allocating and analysing again
+ * (IMPC_SHIM_NOPOOL=1 creates and destroys a batch per Solver instead, for comparison).  Differences from OsqpEigen, all benign for the
  * reference's call pattern: Data copies vectors when they are set (OsqpEigen keeps the caller's
  * pointer until initSolver); osqp_setup's numeric work runs on the device at the first solve, so
  * a non-convex P surfaces as ErrorExitFlag::NonCvxError from solveProblem instead of a failed
@@ -89,6 +93,15 @@ inline void debug(const char *what) { std::fprintf(stderr, "[OsqpEigen/impc] %s\
 
 inline void debug_impc(const char *what, int rc) {
     std::fprintf(stderr, "[OsqpEigen/impc] %s failed (%d): %s\n", what, rc, impc_last_error());
+}
+
+/* Workspace pool off (IMPC_SHIM_NOPOOL=1): a batch is created and destroyed per Solver. */
+inline bool no_pool() {
+    static const bool off = [] {
+        const char *e = std::getenv("IMPC_SHIM_NOPOOL");
+        return e && e[0] == '1';
+    }();
+    return off;
 }
 
 /* Process-wide context, created on first use. */
@@ -247,6 +260,10 @@ class Solver {
     bool m_persistent = false;     // structured batch with a persistent workspace
     bool m_setup_current = false;  // the device workspace is set up on the current data
 
+    void release() {
+        if (m_batch) (detail::no_pool() ? impc_batch_destroy : impc_batch_release)(m_batch);
+        m_batch = nullptr;
+    }
     bool structured() const {
         impc_batch_stats st{};
         return m_batch && impc_batch_get_stats(m_batch, &st) == IMPC_OK && st.kernel == IMPC_KERNEL_STRUCTURED;
@@ -317,15 +334,15 @@ public:
         impc_ctx ctx = detail::context();
         if (!ctx) return false;
         const Data &d = *m_data;
-        int rc = impc_batch_create(ctx, d.numberOfVariables(), d.numberOfConstraints(), d.Pp.data(), d.Pi.data(),
-                                   d.Ap.data(), d.Ai.data(), 1, &m_batch);
-        if (rc) { detail::debug_impc("impc_batch_create", rc); m_batch = nullptr; return false; }
+        int rc = (detail::no_pool() ? impc_batch_create : impc_batch_acquire)(
+            ctx, d.numberOfVariables(), d.numberOfConstraints(), d.Pp.data(), d.Pi.data(), d.Ap.data(), d.Ai.data(), 1,
+            &m_batch);
+        if (rc) { detail::debug_impc("impc_batch_acquire", rc); m_batch = nullptr; return false; }
         rc = impc_batch_set_settings(m_batch, &m_settings->getSettings());
         if (!rc) rc = impc_batch_set_values(m_batch, d.Px.data(), d.q.data(), d.Ax.data(), d.l.data(), d.u.data());
         if (rc) {
             detail::debug_impc("osqp_setup equivalent", rc);
-            impc_batch_destroy(m_batch);
-            m_batch = nullptr;
+            release();
             return false;
         }
         // updateGradient / updateBounds between solves keep the solver state, as osqp_update_*
@@ -341,8 +358,7 @@ public:
     }
 
     void clearSolver() {
-        if (m_batch) impc_batch_destroy(m_batch);
-        m_batch = nullptr;
+        release();
         m_solved = false;
         m_persistent = false;
         m_setup_current = false;

@@ -128,6 +128,17 @@ int impc_ctx_synchronize(impc_ctx ctx);
 int impc_batch_create(impc_ctx ctx, int64_t n, int64_t m, const int64_t *Pp, const int64_t *Pi, const int64_t *Ap,
                       const int64_t *Ai, int64_t batch, impc_batch *out);
 int impc_batch_destroy(impc_batch b);
+/* A batch from the context's workspace pool: a released batch with the same pattern (n, m, P and
+ * A compared entry by entry) and capacity is reused -- no symbolic or structure analysis, no
+ * device allocation, no synchronisation -- else a new one is created.  It comes back in the state
+ * impc_batch_create leaves (default settings, no values, no warm start, no time limits, FIFO
+ * queue, every QP active, persistent workspace off, profiling off).  impc_batch_release returns it
+ * to the pool: the next acquire's uploads are stream-ordered after anything still reading it.
+ * impc_ctx_destroy frees the pool.  The OsqpEigen front end's Solver (one per solveTraj call,
+ * mpcPlanner.cpp:436 / :527) lives on it. */
+int impc_batch_acquire(impc_ctx ctx, int64_t n, int64_t m, const int64_t *Pp, const int64_t *Pi, const int64_t *Ap,
+                       const int64_t *Ai, int64_t batch, impc_batch *out);
+int impc_batch_release(impc_batch b);
 
 int impc_batch_set_settings(impc_batch b, const impc_settings *s);
 

@@ -486,6 +486,8 @@ struct impc_ctx_s {
     hipEvent_t ev_order = nullptr;
     std::vector<hipEvent_t> ev_pool, ev_pending;
     std::vector<hipEvent_t> timer_marks;  // impc_ctx_timer_mark
+    // released batches (impc_batch_acquire / impc_batch_release), with their pattern hashes
+    std::vector<std::pair<uint64_t, impc_batch_s *>> pool;
 };
 
 // Every host->device transfer and fill below goes through the context's stream and has finished
@@ -622,6 +624,12 @@ struct impc_batch_s {
     bool profile = false;
     hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     bool ev_setup = false, ev_solve = false;
+    // small batches: pinned host staging of the inputs, warm start and results (one DMA each way
+    // instead of a pageable copy + synchronisation per array), regions [inputs][x ws][y ws][x][y][info]
+    double *h_stage = nullptr;
+    hipEvent_t ev_in = nullptr, ev_ws = nullptr;  // the last staged input / warm-start DMA
+    bool in_pending = false, ws_pending = false;
+    uint64_t pool_hash = 0;
 };
 
 namespace {
@@ -1121,6 +1129,55 @@ int prepare_structured(impc_batch b) {
     return IMPC_OK;
 }
 
+// ---- pinned staging of small batches (impc_batch_set_values / _warm_start / _get)
+constexpr size_t kStageMax = (size_t)8 << 20;  // bytes: inputs + warm start + results of the batch
+size_t stage_in_len(const impc_batch_s *b) { return (size_t)b->B * (size_t)(b->nnzP + b->n + b->nnzA + 2 * b->m); }
+size_t stage_len(const impc_batch_s *b) {
+    return stage_in_len(b) + (size_t)b->B * (size_t)(2 * (b->n + b->m)) + (size_t)b->B * sizeof(impc_info) / 8;
+}
+bool stage_ok(const impc_batch_s *b) { return 8 * stage_len(b) <= kStageMax; }
+double *stage_xws(impc_batch b) { return b->h_stage + stage_in_len(b); }
+double *stage_xout(impc_batch b) { return stage_xws(b) + (size_t)b->B * (size_t)(b->n + b->m); }
+int stage_ensure(impc_batch b) {
+    if (b->h_stage) return IMPC_OK;
+    HIP_OK(hipHostMalloc((void **)&b->h_stage, 8 * stage_len(b), hipHostMallocDefault));
+    HIP_OK(hipEventCreateWithFlags(&b->ev_in, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&b->ev_ws, hipEventDisableTiming));
+    return IMPC_OK;
+}
+
+// the state impc_batch_create leaves (a batch taken from the workspace pool)
+void reset_batch(impc_batch b) {
+    impc_default_settings(&b->settings);
+    to_dev_settings(&b->settings, &b->dst);
+    b->dst.tick_s = b->ctx->tick_s;
+    b->kernel_req = IMPC_KERNEL_AUTO;
+    b->values_set = b->has_ws = b->ws_y = b->tlim_on = false;
+    b->persist_on = b->persist_valid = b->q_by_update = false;
+    b->profile = b->qpt_valid = b->ev_setup = b->ev_solve = false;
+    b->queue_mode = IMPC_QUEUE_FIFO;
+    b->queue_qw = 0.0;
+    b->Bact = b->B;
+    b->shared = b->shared_expanded = false;
+    b->generic_dirty = true;
+    b->generic_setup_done = b->generic_first_run = false;
+}
+
+uint64_t pattern_hash(int64_t n, int64_t m, int64_t batch, const int64_t *Pp, const int64_t *Pi, const int64_t *Ap,
+                      const int64_t *Ai) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const int64_t *a, int64_t len) {
+        for (int64_t k = 0; k < len; k++) h = (h ^ (uint64_t)a[k]) * 1099511628211ull;
+    };
+    const int64_t hdr[3] = {n, m, batch};
+    mix(hdr, 3);
+    mix(Pp, n + 1);
+    if (Pi) mix(Pi, Pp[n]);
+    mix(Ap, n + 1);
+    mix(Ai, Ap[n]);
+    return h;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1188,6 +1245,8 @@ int impc_ctx_destroy(impc_ctx ctx) {
     if (!ctx) return IMPC_OK;
     (void)hipSetDevice(ctx->device);
     (void)ctx_quiesce(ctx);
+    for (auto &e : ctx->pool) (void)impc_batch_destroy(e.second);
+    ctx->pool.clear();
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->d_group) (void)hipFree(ctx->d_group);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
@@ -1274,12 +1333,54 @@ int impc_batch_destroy(impc_batch b) {
     }
     for (hipEvent_t e : b->ev)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {b->ev_in, b->ev_ws})
+        if (e) (void)hipEventDestroy(e);
+    if (b->h_stage) (void)hipHostFree(b->h_stage);
     void *ptrs[] = {b->d_in,     b->d_xout,  b->d_yout,  b->d_info,  b->d_tables, b->d_scal, b->d_counter,
                     b->d_sym,    b->d_work,  b->d_sec,   b->d_shPx,  b->d_shAx,   b->d_Axv,  b->d_vmap,
                     b->d_qpt,    b->d_persist, b->d_tlim, b->d_csr, b->d_qscr};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete b;
+    return IMPC_OK;
+}
+
+int impc_batch_acquire(impc_ctx ctx, int64_t n, int64_t m, const int64_t *Pp, const int64_t *Pi, const int64_t *Ap,
+                       const int64_t *Ai, int64_t batch, impc_batch *out) {
+    if (!ctx || !out) return fail(IMPC_INVALID_ARGUMENT, "null context or output");
+    *out = nullptr;
+    if (n <= 0 || m < 0 || !Pp || !Ap || batch <= 0) return fail(IMPC_DATA_VALIDATION_ERROR, "invalid dimensions or pattern");
+    const uint64_t h = pattern_hash(n, m, batch, Pp, Pi, Ap, Ai);
+    for (size_t k = ctx->pool.size(); k-- > 0;) {
+        impc_batch b = ctx->pool[k].second;
+        if (ctx->pool[k].first != h || b->n != n || b->m != m || b->B != batch || b->nnzP != Pp[n] ||
+            b->nnzA != Ap[n])
+            continue;
+        if (!std::equal(b->Pp.begin(), b->Pp.end(), Pp) || (b->nnzP && !std::equal(b->Pi.begin(), b->Pi.end(), Pi)) ||
+            !std::equal(b->Ap.begin(), b->Ap.end(), Ap) || !std::equal(b->Ai.begin(), b->Ai.end(), Ai))
+            continue;
+        ctx->pool.erase(ctx->pool.begin() + (std::ptrdiff_t)k);
+        reset_batch(b);
+        *out = b;
+        return IMPC_OK;
+    }
+    int rc = impc_batch_create(ctx, n, m, Pp, Pi, Ap, Ai, batch, out);
+    if (!rc) (*out)->pool_hash = h;
+    return rc;
+}
+
+int impc_batch_release(impc_batch b) {
+    if (!b) return IMPC_OK;
+    impc_ctx ctx = b->ctx;
+    if (!b->pool_hash)  // a batch of impc_batch_create: hash it now
+        b->pool_hash = pattern_hash(b->n, b->m, b->B, b->Pp.data(), b->nnzP ? b->Pi.data() : nullptr, b->Ap.data(),
+                                    b->Ai.data());
+    constexpr size_t kPoolMax = 64;  // released batches kept per context (oldest freed first)
+    if (ctx->pool.size() >= kPoolMax) {
+        (void)impc_batch_destroy(ctx->pool.front().second);
+        ctx->pool.erase(ctx->pool.begin());
+    }
+    ctx->pool.emplace_back(b->pool_hash, b);
     return IMPC_OK;
 }
 
@@ -1323,8 +1424,33 @@ int impc_batch_set_values(impc_batch b, const double *Px, const double *q, const
             return fail(IMPC_DATA_VALIDATION_ERROR, msg);
         }
     HIP_OK(hipSetDevice(b->ctx->device));
-    IMPC_TRY(ctx_quiesce(b->ctx));  // no solve in flight on any stream reads the arrays replaced below
     const size_t B = (size_t)b->B;
+    if (stage_ok(b)) {
+        // small batch: the five arrays packed into pinned staging (the device inputs Px, q, Ax, l, u
+        // are contiguous in that order), one DMA queued after every launch that may still read
+        // the inputs -- no host synchronisation
+        IMPC_TRY(stage_ensure(b));
+        if (b->in_pending) HIP_OK(hipEventSynchronize(b->ev_in));
+        double *s = b->h_stage;
+        const size_t len[5] = {(size_t)b->nnzP * B, (size_t)b->n * B, (size_t)b->nnzA * B, (size_t)b->m * B,
+                               (size_t)b->m * B};
+        const double *src[5] = {Px, q, Ax, l, u};
+        for (int k = 0; k < 5; k++) {
+            if (len[k]) std::memcpy(s, src[k], sizeof(double) * len[k]);
+            s += len[k];
+        }
+        hipStream_t st = b->ctx->stream;
+        IMPC_TRY(ctx_order_after_all(b->ctx, st));
+        HIP_OK(hipMemcpyAsync(b->in_Px, b->h_stage, sizeof(double) * stage_in_len(b), hipMemcpyHostToDevice, st));
+        HIP_OK(hipEventRecord(b->ev_in, st));
+        b->in_pending = true;
+        b->shared = false;
+        b->persist_valid = b->q_by_update = false;
+        b->values_set = true;
+        b->generic_dirty = true;
+        return IMPC_OK;
+    }
+    IMPC_TRY(ctx_quiesce(b->ctx));  // no solve in flight on any stream reads the arrays replaced below
     IMPC_TRY(h2d_sync(b->ctx->stream, b->in_Px, Px, sizeof(double) * b->nnzP * B));
     IMPC_TRY(h2d_sync(b->ctx->stream, b->in_q, q, sizeof(double) * b->n * B));
     IMPC_TRY(h2d_sync(b->ctx->stream, b->in_Ax, Ax, sizeof(double) * b->nnzA * B));
@@ -1418,17 +1544,31 @@ int impc_batch_set_values_device(impc_batch b, const double *Px, const double *q
 int impc_batch_warm_start(impc_batch b, const double *x, const double *y) {
     if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
     HIP_OK(hipSetDevice(b->ctx->device));
-    IMPC_TRY(ctx_quiesce(b->ctx));
     if (!x) {
         b->has_ws = false;
         b->generic_dirty = true;
         return IMPC_OK;
     }
     const size_t B = (size_t)b->B;
-    IMPC_TRY(h2d_sync(b->ctx->stream, b->in_xws, x, sizeof(double) * b->n * B));
-    // y = 0 (the solveTraj warm start, mpcPlanner.cpp:480-497): nothing is uploaded, the structured
-    // kernel reads no duals (WaveIO::has_ws == 2) and the generic path zero-fills its copy
-    if (b->m && y) IMPC_TRY(h2d_sync(b->ctx->stream, b->in_yws, y, sizeof(double) * b->m * B));
+    if (stage_ok(b)) {  // x (and y) through the pinned staging, stream-ordered, one DMA
+        IMPC_TRY(stage_ensure(b));
+        if (b->ws_pending) HIP_OK(hipEventSynchronize(b->ev_ws));
+        double *s = stage_xws(b);
+        std::memcpy(s, x, sizeof(double) * b->n * B);
+        const size_t len = (size_t)b->n * B + (b->m && y ? (size_t)b->m * B : 0);
+        if (b->m && y) std::memcpy(s + (size_t)b->n * B, y, sizeof(double) * b->m * B);
+        hipStream_t st = b->ctx->stream;
+        IMPC_TRY(ctx_order_after_all(b->ctx, st));
+        HIP_OK(hipMemcpyAsync(b->in_xws, s, sizeof(double) * len, hipMemcpyHostToDevice, st));  // in_yws follows in_xws
+        HIP_OK(hipEventRecord(b->ev_ws, st));
+        b->ws_pending = true;
+    } else {
+        IMPC_TRY(ctx_quiesce(b->ctx));  // no solve in flight on any stream reads the arrays replaced below
+        IMPC_TRY(h2d_sync(b->ctx->stream, b->in_xws, x, sizeof(double) * b->n * B));
+        // y = 0 (the solveTraj warm start, mpcPlanner.cpp:480-497): nothing is uploaded, the
+        // structured kernel reads no duals (WaveIO::has_ws == 2) and the generic path zero-fills
+        if (b->m && y) IMPC_TRY(h2d_sync(b->ctx->stream, b->in_yws, y, sizeof(double) * b->m * B));
+    }
     b->ws_y = y != nullptr;
     // osqp_warm_start turns the warm_start setting on (osqp.c, oracle ora_warm_start)
     b->settings.warm_start = 1;
@@ -1622,6 +1762,22 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
 int impc_batch_get(impc_batch b, double *x, double *y, impc_info *info) {
     if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
     HIP_OK(hipSetDevice(b->ctx->device));
+    if (stage_ok(b)) {  // results through the pinned staging: three DMAs, one synchronisation
+        IMPC_TRY(stage_ensure(b));
+        hipStream_t st = b->ctx->stream;
+        IMPC_TRY(ctx_order_after_all(b->ctx, st));  // after the solves, on whichever stream
+        double *sx = stage_xout(b), *sy = sx + (size_t)b->B * b->n;
+        impc_info *si = (impc_info *)(sy + (size_t)b->B * b->m);
+        const size_t B = (size_t)b->B;
+        if (x) HIP_OK(hipMemcpyAsync(sx, b->d_xout, sizeof(double) * b->n * B, hipMemcpyDeviceToHost, st));
+        if (y && b->m) HIP_OK(hipMemcpyAsync(sy, b->d_yout, sizeof(double) * b->m * B, hipMemcpyDeviceToHost, st));
+        if (info) HIP_OK(hipMemcpyAsync(si, b->d_info, sizeof(impc_info) * B, hipMemcpyDeviceToHost, st));
+        IMPC_TRY(ctx_quiesce(b->ctx));
+        if (x) std::memcpy(x, sx, sizeof(double) * b->n * B);
+        if (y && b->m) std::memcpy(y, sy, sizeof(double) * b->m * B);
+        if (info) std::memcpy(info, si, sizeof(impc_info) * B);
+        return IMPC_OK;
+    }
     HIP_OK(hipStreamSynchronize(b->ctx->stream));
     HIP_OK(hipDeviceSynchronize());
     if (x) HIP_OK(hipMemcpy(x, b->d_xout, sizeof(double) * b->n * b->B, hipMemcpyDeviceToHost));

@@ -99,6 +99,8 @@ _sig("impc_ctx_stream", _P, _P)
 _sig("impc_ctx_synchronize", C.c_int, _P)
 _sig("impc_batch_create", C.c_int, _P, C.c_int64, C.c_int64, _i64p, _i64p, _i64p, _i64p, C.c_int64, C.POINTER(_P))
 _sig("impc_batch_destroy", C.c_int, _P)
+_sig("impc_batch_acquire", C.c_int, _P, C.c_int64, C.c_int64, _i64p, _i64p, _i64p, _i64p, C.c_int64, C.POINTER(_P))
+_sig("impc_batch_release", C.c_int, _P)
 _sig("impc_batch_set_settings", C.c_int, _P, C.POINTER(Settings))
 _sig("impc_batch_set_values", C.c_int, _P, _dp, _dp, _dp, _dp, _dp)
 _sig("impc_batch_set_values_device", C.c_int, _P, _P, _P, _P, _P, _P)
@@ -239,7 +241,8 @@ EXPORTED = [
     "impc_reference_traj_device", "impc_repeat_rows_device", "impc_comm_unique_id", "impc_comm_create", "impc_comm_destroy", "impc_comm_allgather", "impc_comm_gather_info",
     "impc_comm_max", "impc_ctx_timer_mark", "impc_ctx_timer_read", "impc_batch_set_time_limits",
     "impc_ctx_clock_rate", "impc_ctx_clock_check", "impc_batch_set_queue_order", "impc_batch_warm_start_device",
-    "impc_batch_set_active", "impc_gather_rows_device", "impc_replan_commit_device",
+    "impc_batch_set_active", "impc_gather_rows_device", "impc_replan_commit_device", "impc_batch_acquire",
+    "impc_batch_release",
 ]
 
 

@@ -10,8 +10,17 @@
 //                   <in>, optionally followed by updateGradient -> solveProblem -> updateBounds ->
 //                   solveProblem; results to <out> for tests/test_shim.py to check against the
 //                   oracle (not against the C-ABI)
+//   shim_test bench <in> <calls> : the per-call cost of the drop-in path -- host wall time of the
+//                   whole solveTraj sequence (Solver construction -> settings -> set* -> initSolver
+//                   -> setWarmStart -> solveProblem -> getSolution -> clearSolver) over <calls>
+//                   calls cycling through the QPs of <in>, next to the device time of the same
+//                   QPs solved alone on a direct one-QP batch (HIP events around the launch, and
+//                   the kernel's own dequeue-to-results latency); one JSON line
+#include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include <OsqpEigen/OsqpEigen.h>
@@ -203,8 +212,113 @@ static int replay(const char *in, const char *out) {
     return fails ? 1 : 0;
 }
 
+static double pct(std::vector<double> v, double p) {
+    std::sort(v.begin(), v.end());
+    return v.empty() ? 0.0 : v[(size_t)std::min<double>((double)v.size() - 1, p * (double)(v.size() - 1) + 0.5)];
+}
+
+static int bench(const char *in, long calls) {
+    FILE *f = std::fopen(in, "rb");
+    if (!f) return 2;
+    int64_t h[6];
+    if (std::fread(h, sizeof h, 1, f) != 1) return 2;
+    const int64_t n = h[0], m = h[1], nnzP = h[2], nnzA = h[3], nqp = h[4], flags = h[5];
+    auto rd = [&](auto &v, size_t k) { v.resize(k); return std::fread(v.data(), sizeof(v[0]), k, f) == k; };
+    std::vector<int64_t> Pp, Pi, Ap, Ai;
+    if (!rd(Pp, n + 1) || !rd(Pi, nnzP) || !rd(Ap, n + 1) || !rd(Ai, nnzA)) return 2;
+    struct QP {
+        std::vector<double> Px, q, Ax, l, u, xw;
+        Eigen::SparseMatrix<double> P, A;
+    };
+    std::vector<QP> qps((size_t)nqp);
+    for (QP &Q : qps) {
+        if (!rd(Q.Px, nnzP) || !rd(Q.q, n) || !rd(Q.Ax, nnzA) || !rd(Q.l, m) || !rd(Q.u, m)) return 2;
+        if ((flags & 1) && !rd(Q.xw, n)) return 2;
+        Q.P = Eigen::SparseMatrix<double>((Eigen::Index)n, (Eigen::Index)n);
+        Q.A = Eigen::SparseMatrix<double>((Eigen::Index)m, (Eigen::Index)n);
+        for (int64_t j = 0; j < n; j++) {
+            for (int64_t k = Pp[j]; k < Pp[j + 1]; k++) Q.P.insert(Pi[k], j) = Q.Px[k];
+            for (int64_t k = Ap[j]; k < Ap[j + 1]; k++) Q.A.insert(Ai[k], j) = Q.Ax[k];
+        }
+    }
+    std::fclose(f);
+    auto vec = [](const std::vector<double> &v) {
+        Eigen::VectorXd e((Eigen::Index)v.size());
+        for (size_t k = 0; k < v.size(); k++) e((Eigen::Index)k) = v[k];
+        return e;
+    };
+    // the drop-in path, timed per call on the host clock (the first call of each QP shape also
+    // creates the context / pool entry: warm-up calls are not timed)
+    std::vector<double> wall;
+    const long warm = std::min<long>(8, calls);
+    for (long c = 0; c < calls + warm; c++) {
+        const QP &Q = qps[(size_t)(c % nqp)];
+        const auto t0 = std::chrono::steady_clock::now();
+        {
+            OsqpEigen::Solver solver;  // mpcPlanner.cpp:436-527
+            solver.settings()->setVerbosity(false);
+            solver.settings()->setWarmStart(true);
+            solver.data()->setNumberOfVariables((int)n);
+            solver.data()->setNumberOfConstraints((int)m);
+            Eigen::VectorXd qv = vec(Q.q), lv = vec(Q.l), uv = vec(Q.u);
+            bool ok = solver.data()->setHessianMatrix(Q.P) && solver.data()->setGradient(qv) &&
+                      solver.data()->setLinearConstraintsMatrix(Q.A) && solver.data()->setLowerBound(lv) &&
+                      solver.data()->setUpperBound(uv) && solver.initSolver();
+            Eigen::VectorXd x0 = (flags & 1) ? vec(Q.xw) : Eigen::VectorXd(), y0;
+            if (!(flags & 1)) x0.setZero((Eigen::Index)n);
+            y0.setZero((Eigen::Index)m);
+            ok = ok && solver.setWarmStart(x0, y0) && solver.solveProblem() == OsqpEigen::ErrorExitFlag::NoError;
+            const Eigen::VectorXd &x = solver.getSolution();
+            ok = ok && x.size() == n;
+            solver.clearSolver();
+            if (!ok) {
+                std::printf("bench: call %ld failed\n", c);
+                return 1;
+            }
+        }
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (c >= warm) wall.push_back(ms);
+    }
+    // the same QPs alone on a direct one-QP batch: HIP-event time of the solve call (queue order +
+    // kernel) and the kernel's dequeue-to-results latency
+    impc_ctx ctx = nullptr;
+    if (impc_ctx_create(0, &ctx)) return 1;
+    impc_batch b = nullptr;
+    if (impc_batch_create(ctx, n, m, Pp.data(), Pi.data(), Ap.data(), Ai.data(), 1, &b)) return 1;
+    impc_settings st;
+    impc_default_settings(&st);
+    st.verbose = 0;
+    impc_batch_set_settings(b, &st);
+    impc_batch_set_profiling(b, 1);
+    std::vector<double> ev_ms, lat_ms;
+    const long dev_calls = std::min<long>(calls, 256);
+    for (long c = 0; c < dev_calls + warm; c++) {
+        const QP &Q = qps[(size_t)(c % nqp)];
+        if (impc_batch_set_values(b, Q.Px.data(), Q.q.data(), Q.Ax.data(), Q.l.data(), Q.u.data())) return 1;
+        std::vector<double> x0 = (flags & 1) ? Q.xw : std::vector<double>((size_t)n, 0.0);
+        if (impc_batch_warm_start(b, x0.data(), nullptr) || impc_batch_solve(b, nullptr)) return 1;
+        double su = 0, so = 0, ou = 0, lat = 0;
+        if (impc_batch_get_timings(b, &su, &so, &ou) || impc_batch_get_qp_latency(b, &lat)) return 1;
+        if (c >= warm) {
+            ev_ms.push_back(so);
+            lat_ms.push_back(lat);
+        }
+    }
+    impc_batch_destroy(b);
+    impc_ctx_destroy(ctx);
+    std::printf("{\"calls\": %ld, \"qps\": %lld, \"n\": %lld, \"m\": %lld, \"pool\": %s, "
+                "\"host_wall_ms\": {\"p50\": %.4f, \"p90\": %.4f, \"mean\": %.4f}, "
+                "\"device_event_ms\": {\"p50\": %.4f, \"p90\": %.4f}, \"kernel_latency_ms\": {\"p50\": %.4f, "
+                "\"p90\": %.4f}, \"overhead_p50_ms\": %.4f}\n",
+                (long)wall.size(), (long long)nqp, (long long)n, (long long)m, OsqpEigen::detail::no_pool() ? "false" : "true",
+                pct(wall, 0.5), pct(wall, 0.9), [&] { double s = 0; for (double v : wall) s += v; return s / (double)wall.size(); }(),
+                pct(ev_ms, 0.5), pct(ev_ms, 0.9), pct(lat_ms, 0.5), pct(lat_ms, 0.9), pct(wall, 0.5) - pct(ev_ms, 0.5));
+    return 0;
+}
+
 int main(int argc, char **argv) {
     if (argc > 3 && std::strcmp(argv[1], "replay") == 0) return replay(argv[2], argv[3]);
+    if (argc > 3 && std::strcmp(argv[1], "bench") == 0) return bench(argv[2], std::atol(argv[3]));
     const bool gpu = argc > 1 && std::strcmp(argv[1], "gpu") == 0;
     // OSQP demo problem: P = [[4,1],[1,2]] (both triangles inserted, as Eigen users do),
     // q = (1,1), A = [[1,1],[1,0],[0,1]], l = (1,0,0), u = (1,0.7,0.7); x* = (0.3,0.7), y* = (-2.9,0,0.2)

@@ -131,3 +131,75 @@ def test_shim_update_sequence_vs_persistent_oracle(tmp_path):
             got = tuple(a[i:i + 1] for a in steps[s])
             _check(got, (xo[None], yo[None], np.array([io["status_val"]]), np.array([io["iter"]]),
                          np.array([io["obj_val"]])))
+
+
+def _bench_file(tmp_path, cfg):
+    pat, v = cfg["pattern"], cfg["values"]
+    n, m = int(pat["n"]), int(pat["m"])
+    B = v["q"].shape[0]
+    xw = cfg.get("x_ws")
+    fin = tmp_path / "bench_in.bin"
+    with open(fin, "wb") as f:
+        np.array([n, m, len(pat["Pi"]), len(pat["Ai"]), B, 1 if xw is not None else 0], np.int64).tofile(f)
+        for k in ("Pp", "Pi", "Ap", "Ai"):
+            np.ascontiguousarray(pat[k], np.int64).tofile(f)
+        for i in range(B):
+            for k in ("Px", "q", "Ax", "l", "u"):
+                np.ascontiguousarray(v[k][i], float).tofile(f)
+            if xw is not None:
+                np.ascontiguousarray(xw[i], float).tofile(f)
+    return fin
+
+
+@pytest.mark.gpu
+def test_shim_per_call_cost(tmp_path):
+    """The drop-in path's cost per solveTraj call (Solver -> initSolver -> setWarmStart -> solveProblem
+    -> getSolution -> clearSolver) on a known pattern: with the workspace pool the host wall time
+    stays within 0.25 ms of the device time of the same QP (measured ~0.1 ms, profiles/r04)."""
+    import json
+    from impc import scenarios
+    cfg = next(iter(scenarios.intent_config(N=20, K=8, instances=4, hyps=8, seed=31).values()))
+    fin = _bench_file(tmp_path, cfg)
+    p = subprocess.run([EXE, "bench", str(fin), "200"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    print(r)
+    assert r["pool"] and r["calls"] == 200
+    assert r["host_wall_ms"]["p50"] <= r["device_event_ms"]["p50"] + 0.25, r
+
+
+@pytest.mark.gpu
+def test_workspace_pool_reuses_and_resets(ctx):
+    """impc_batch_acquire / impc_batch_release: a released batch of the same pattern comes back
+    (same handle, default settings, no warm start, all QPs active), another pattern does not."""
+    import ctypes as C
+    import impc
+    from impc import scenarios
+    cfg = scenarios.first_call_config(batch=2, seed=5)
+    pat, v = cfg["pattern"], cfg["values"]
+    arrs = [np.ascontiguousarray(pat[k], np.int64) for k in ("Pp", "Pi", "Ap", "Ai")]
+    ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int64))  # noqa: E731
+    h1, h2, h3 = C.c_void_p(), C.c_void_p(), C.c_void_p()
+    assert impc.lib.impc_batch_acquire(ctx.h, pat["n"], pat["m"], *[ip(a) for a in arrs], 2, C.byref(h1)) == 0
+    b = impc.Batch.__new__(impc.Batch)
+    b.ctx, b.h, b.n, b.m, b.B = ctx, h1, int(pat["n"]), int(pat["m"]), 2
+    b.nnzP, b.nnzA = int(arrs[0][-1]), int(arrs[2][-1])
+    s = impc.default_settings(verbose=0, max_iter=7)
+    b.set_settings(s)
+    b.set_values(v["Px"], v["q"], v["Ax"], v["l"], v["u"])
+    b.set_active(1)
+    b.solve()
+    _, _, info = b.get()
+    assert info["iter"][0] <= 7
+    assert impc.lib.impc_batch_release(h1) == 0
+    assert impc.lib.impc_batch_acquire(ctx.h, pat["n"], pat["m"], *[ip(a) for a in arrs], 2, C.byref(h2)) == 0
+    assert h2.value == h1.value
+    b.h = h2
+    b.set_values(v["Px"], v["q"], v["Ax"], v["l"], v["u"])
+    b.solve()  # default settings again (max_iter 4000), both QPs active
+    _, _, info2 = b.get()
+    assert (info2["iter"] > 7).all() and (info2["status_val"] == 1).all()
+    assert impc.lib.impc_batch_acquire(ctx.h, pat["n"], pat["m"], *[ip(a) for a in arrs], 1, C.byref(h3)) == 0
+    assert h3.value != h2.value  # other capacity: a new batch
+    for h in (h2, h3):
+        assert impc.lib.impc_batch_release(h) == 0
