@@ -165,6 +165,79 @@ def end_to_end(impc, ctx, batches, args, grouped):
                     "impc_batch_warm_start (H2D, pageable) -> solve -> impc_batch_get (x, y, info D2H)"}
 
 
+def end_to_end_pipelined(impc, ctx, bks, settings, args, queue_weight):
+    """PCIe-inclusive throughput of a stream of batches (end to end) with the
+    transfers overlapped: two sets of the workload's batches; while one set solves (the context's
+    stream), the copy stream downloads the other set's previous results and uploads its next inputs
+    (impc_batch_set_values_async / get_async from pinned host arrays, impc_host_alloc).  Host wall
+    clock over `steps` steps, from the first upload to the last download: every QP's inputs cross
+    PCIe in and its x, y and info come back inside the measured time."""
+    steps = max(2, args.e2e_steps)
+    C = impc.Stream(ctx)
+    sets, host = [], []
+    try:
+        for _ in range(2):
+            bs, hs = [], []
+            for bk in bks:
+                b, _ = make_batch(impc, ctx, bk, settings, False, False, queue_weight)
+                v = bk["values"]
+                Px0, Ax0, var, Axv = impc.shared_split(v["Px"], v["Ax"])
+                h = {k: impc.HostArray(ctx, a.shape) for k, a in (("Axv", Axv), ("q", v["q"]), ("l", v["l"]),
+                                                                  ("u", v["u"]), ("x_ws", bk["x_ws"]))}
+                for k, a in (("Axv", Axv), ("q", v["q"]), ("l", v["l"]), ("u", v["u"]), ("x_ws", bk["x_ws"])):
+                    h[k].a[...] = a  # the producer's data, already in pinned memory when the step starts
+                h["x"] = impc.HostArray(ctx, (b.B, b.n))
+                h["y"] = impc.HostArray(ctx, (b.B, b.m))
+                h["info"] = impc.HostArray(ctx, (b.B,), impc.INFO_DTYPE)
+                bs.append(b)
+                hs.append(h)
+            sets.append(bs)
+            host.append(hs)
+
+        def upload(s):
+            for b, h in zip(sets[s], host[s]):
+                b.set_values_async(h["Axv"], h["q"], h["l"], h["u"], h["x_ws"], stream=C)
+
+        def download(s):
+            for b, h in zip(sets[s], host[s]):
+                b.get_async(h["x"], h["y"], h["info"], stream=C)
+
+        for rep in range(2):  # rep 0: warm-up (module load, scratch growth)
+            ctx.synchronize()
+            t0 = time.perf_counter()
+            upload(0)
+            impc.ctx_stream_wait(ctx, C)
+            for t in range(steps):
+                s = t % 2
+                impc.solve_group(sets[s])                  # context stream
+                if t + 1 < steps:
+                    upload(1 - s)                          # after set 1-s's previous solve (C waited for it)
+                    impc.ctx_stream_wait(ctx, C)           # the next solve waits for that upload
+                C.wait(None)                               # after this solve
+                download(s)
+            C.synchronize()
+            ctx.synchronize()
+            el = time.perf_counter() - t0
+        ok = all(np.array_equal(host[(steps - 1) % 2][k]["info"].a["iter"], b.get()[2]["iter"])
+                 for k, b in enumerate(sets[(steps - 1) % 2]))
+        qps = sum(b.B for b in sets[0])
+    finally:
+        for bs in sets:
+            for b in bs:
+                b.close()
+        for hs in host:
+            for h in hs:
+                for a in h.values():
+                    a.free()
+        C.close()
+    ms = 1000.0 * el / steps
+    return {"qps_per_s": qps / (ms * 1e-3), "ms_per_step": ms, "steps": steps, "qps": qps, "results_match": bool(ok),
+            "what": "host wall clock per step of a pipelined stream of batches: per-QP inputs (pinned host arrays) "
+                    "-> impc_batch_set_values_async on a copy stream, solve on the context stream, x, y, info -> "
+                    "pinned host arrays (impc_batch_get_async); the next batch set's upload and the previous one's "
+                    "download overlap each solve; first upload and last download inside the measured time"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -184,7 +257,7 @@ def main():
                     help="work-queue order of the persistent launches (impc_batch_set_queue_order)")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="single-GPU study: run only rank 0's shard of a W-way strong split (not a headline line)")
-    ap.add_argument("--e2e-steps", type=int, default=2,
+    ap.add_argument("--e2e-steps", type=int, default=4,
                     help="end-to-end steps after the timed region: host arrays in -> solve -> results on the host")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--full-values", action="store_true",
@@ -340,7 +413,12 @@ def main():
     build_id = impc.lib.impc_build_id().decode()
     traffic, traffic_src = measured_traffic(build_id, total_qps, kernel_name, values_mode, args.workload)
 
-    e2e = end_to_end(impc, ctx, batches, args, grouped) if args.e2e_steps > 0 else None
+    e2e = e2e_serial = None
+    if args.e2e_steps > 0:
+        e2e_serial = end_to_end(impc, ctx, batches, args, grouped)
+        if grouped and not args.full_values and all(bk.get("x_ws") is not None for bk in bks):
+            e2e = end_to_end_pipelined(impc, ctx, bks, settings, args, qw)
+            e2e["frac_of_resident"] = e2e["qps_per_s"] / (total_qps * args.steps / elapsed) if world == 1 else None
 
     cpu = parity = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
@@ -421,6 +499,7 @@ def main():
         "cpu_baseline": cpu,
         "parity": parity,
         "e2e": e2e,
+        "e2e_serial": e2e_serial,
         "selection": sel,
         "cost_allgather": gathered,
         "gen_seconds": t_gen,

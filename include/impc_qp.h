@@ -221,6 +221,26 @@ int impc_device_free(impc_ctx ctx, void *ptr);
 int impc_copy_to_device(impc_ctx ctx, void *dst, const void *src, int64_t bytes);
 int impc_copy_to_host(impc_ctx ctx, void *dst, const void *src, int64_t bytes);
 
+/* Pipelined transfers: host <-> device copies of one batch overlapped with the solve of another.
+ * Pinned host memory (hipHostMalloc) for the asynchronous copies, extra streams and the ordering
+ * between them (waiter waits for the work queued on signaler so far), stream synchronisation. */
+int impc_host_alloc(impc_ctx ctx, int64_t bytes, void **out);
+int impc_host_free(impc_ctx ctx, void *ptr);
+int impc_stream_create(impc_ctx ctx, void **stream);
+int impc_stream_destroy(impc_ctx ctx, void *stream);
+int impc_stream_wait(impc_ctx ctx, void *waiter, void *signaler);
+int impc_stream_synchronize(impc_ctx ctx, void *stream);
+/* The per-QP values of a shared-structure batch (after impc_batch_set_values_shared, which fixes
+ * P, A and var_pos): Ax_var [B][nvar], q [B][n], l [B][m], u [B][m] and, when x_ws is not NULL,
+ * the warm start x [B][n] with zero duals -- queued on `stream` (NULL = the context's) with no
+ * host synchronisation and no validation (l <= u is the caller's).  The host arrays must stay
+ * valid until the stream has passed the copies (pinned memory overlaps them with solves); the
+ * caller orders the stream against solves of this batch (impc_stream_wait). */
+int impc_batch_set_values_async(impc_batch b, const double *Ax_var, const double *q, const double *l, const double *u,
+                                const double *x_ws, void *stream);
+/* Results (as impc_batch_get; any pointer may be NULL) copied on `stream`, not waited for. */
+int impc_batch_get_async(impc_batch b, double *x, double *y, impc_info *info, void *stream);
+
 /* Problem / analysis facts (for tests and roofline accounting). */
 typedef struct {
     int64_t n, m, nnzP, nnzA, batch, batch_stride;

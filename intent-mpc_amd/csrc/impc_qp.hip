@@ -478,10 +478,16 @@ struct impc_ctx_s {
     hipStream_t stream = nullptr;
     // the device clock of time limits and latencies: seconds per tick (hipDeviceAttributeWallClockRate)
     double tick_s = 1e-8;
-    // grouped launches: device copy of the entries (grow-only) and its host staging buffer
-    GroupEntry *d_group = nullptr;
-    int group_cap = 0;
-    std::vector<GroupEntry> h_group;
+    // grouped launches: device copies of the entry tables of the last few distinct groups (a
+    // pipeline alternates between batch sets), each with its host copy; reused while unchanged
+    struct GroupTable {
+        GroupEntry *d = nullptr;
+        int cap = 0;
+        std::vector<GroupEntry> h;
+        uint64_t used = 0;
+    };
+    std::vector<GroupTable> groups;
+    uint64_t group_clock = 0;
     // caller-stream bookkeeping (ctx_order_launch / ctx_note_launch / ctx_quiesce)
     hipEvent_t ev_order = nullptr;
     std::vector<hipEvent_t> ev_pool, ev_pending;
@@ -1248,7 +1254,8 @@ int impc_ctx_destroy(impc_ctx ctx) {
     for (auto &e : ctx->pool) (void)impc_batch_destroy(e.second);
     ctx->pool.clear();
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-    if (ctx->d_group) (void)hipFree(ctx->d_group);
+    for (auto &g : ctx->groups)
+        if (g.d) (void)hipFree(g.d);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
     for (hipEvent_t e : ctx->ev_pending) (void)hipEventDestroy(e);
     for (hipEvent_t e : ctx->timer_marks) (void)hipEventDestroy(e);
@@ -1590,6 +1597,43 @@ int impc_batch_warm_start(impc_batch b, const double *x, const double *y) {
     return IMPC_OK;
 }
 
+int impc_batch_set_values_async(impc_batch b, const double *Ax_var, const double *q, const double *l, const double *u,
+                                const double *x_ws, void *stream) {
+    if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
+    if (!b->shared || !b->d_Axv) return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "impc_batch_set_values_shared first");
+    if (!q || (b->m && (!l || !u)) || (b->nvar && !Ax_var)) return fail(IMPC_INVALID_ARGUMENT, "null value array");
+    HIP_OK(hipSetDevice(b->ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : b->ctx->stream;
+    const size_t B = (size_t)b->B;
+    auto h2d = [&](double *dst, const double *src, size_t len) -> hipError_t {
+        return len ? hipMemcpyAsync(dst, src, sizeof(double) * len, hipMemcpyHostToDevice, st) : hipSuccess;
+    };
+    HIP_OK(h2d(b->d_Axv, Ax_var, (size_t)b->nvar * B));
+    HIP_OK(h2d(b->in_q, q, (size_t)b->n * B));
+    HIP_OK(h2d(b->in_l, l, (size_t)b->m * B));
+    HIP_OK(h2d(b->in_u, u, (size_t)b->m * B));
+    if (x_ws) HIP_OK(h2d(b->in_xws, x_ws, (size_t)b->n * B));
+    b->has_ws = x_ws != nullptr;
+    b->ws_y = false;
+    if (x_ws) b->settings.warm_start = b->dst.warm_start = 1;
+    b->shared_expanded = false;
+    b->persist_valid = b->q_by_update = false;
+    b->values_set = true;
+    b->generic_dirty = true;
+    return IMPC_OK;
+}
+
+int impc_batch_get_async(impc_batch b, double *x, double *y, impc_info *info, void *stream) {
+    if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
+    HIP_OK(hipSetDevice(b->ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : b->ctx->stream;
+    const size_t B = (size_t)b->B;
+    if (x) HIP_OK(hipMemcpyAsync(x, b->d_xout, sizeof(double) * b->n * B, hipMemcpyDeviceToHost, st));
+    if (y && b->m) HIP_OK(hipMemcpyAsync(y, b->d_yout, sizeof(double) * b->m * B, hipMemcpyDeviceToHost, st));
+    if (info) HIP_OK(hipMemcpyAsync(info, b->d_info, sizeof(impc_info) * B, hipMemcpyDeviceToHost, st));
+    return IMPC_OK;
+}
+
 int impc_batch_warm_start_device(impc_batch b, const double *x, const double *y) {
     if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
     HIP_OK(hipSetDevice(b->ctx->device));
@@ -1705,28 +1749,42 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
     }
     for (const Launch &L : launches)
         if (L.lds > 160 * 1024 - 1024) return fail(IMPC_UNSUPPORTED, "grouped batches exceed the LDS of a CU");
-    // upload the entries only when they change (repeated solves of one group launch back to back);
-    // the device copy must not change under an in-flight kernel, so an update first waits for every
+    // the entry table: a cached device copy of these very entries (repeated solves of one group,
+    // or of the few groups a pipeline alternates between), else a fresh table -- uploaded on the
+    // launch stream; replacing a cached table that a launch in flight may read waits for every
     // launch on every stream this context has used
-    const bool same = ctx->h_group.size() == entries.size() &&
-                      std::memcmp(ctx->h_group.data(), entries.data(), sizeof(GroupEntry) * (size_t)count) == 0;
-    if (!same) {
-        IMPC_TRY(ctx_quiesce(ctx));
-        if (count > ctx->group_cap) {
-            if (ctx->d_group) HIP_OK(hipFree(ctx->d_group));
-            ctx->d_group = nullptr;
-            HIP_OK(hipMalloc((void **)&ctx->d_group, sizeof(GroupEntry) * (size_t)count));
-            ctx->group_cap = count;
-        }
-        IMPC_TRY(h2d_sync(ctx->stream, ctx->d_group, entries.data(), sizeof(GroupEntry) * (size_t)count));
-        ctx->h_group = entries;
-    }
+    constexpr size_t kGroupTables = 8;
+    const size_t ebytes = sizeof(GroupEntry) * (size_t)count;
+    impc_ctx_s::GroupTable *tab = nullptr;
+    for (auto &g : ctx->groups)
+        if (g.h.size() == entries.size() && std::memcmp(g.h.data(), entries.data(), ebytes) == 0) tab = &g;
     IMPC_TRY(ctx_order_launch(ctx, st));
+    if (!tab) {
+        if (ctx->groups.size() < kGroupTables) {
+            ctx->groups.emplace_back();
+            tab = &ctx->groups.back();
+        } else {
+            IMPC_TRY(ctx_quiesce(ctx));
+            tab = &*std::min_element(ctx->groups.begin(), ctx->groups.end(),
+                                     [](const impc_ctx_s::GroupTable &a, const impc_ctx_s::GroupTable &c) {
+                                         return a.used < c.used;
+                                     });
+        }
+        if (count > tab->cap) {
+            if (tab->d) HIP_OK(hipFree(tab->d));
+            tab->d = nullptr;
+            HIP_OK(hipMalloc((void **)&tab->d, ebytes));
+            tab->cap = count;
+        }
+        tab->h = entries;  // the host copy stays alive: the stream-ordered upload reads it
+        HIP_OK(hipMemcpyAsync(tab->d, tab->h.data(), ebytes, hipMemcpyHostToDevice, st));
+    }
+    tab->used = ++ctx->group_clock;
     if (b0->profile) HIP_OK(hipEventRecord(b0->ev[2], st));
     for (const Launch &L : launches) {
         if (L.total == 0) continue;
         HIP_OK(hipMemsetAsync(L.counter, 0, 256, st));
-        const GroupEntry *E = ctx->d_group + L.first;
+        const GroupEntry *E = tab->d + L.first;
         std::vector<impc_batch> lb((size_t)L.count);
         std::vector<int64_t> lf((size_t)L.count);
         for (int k = 0; k < L.count; k++) {
@@ -2059,6 +2117,54 @@ int impc_copy_to_device(impc_ctx ctx, void *dst, const void *src, int64_t bytes)
     IMPC_TRY(h2d_sync(ctx->stream, dst, src, (size_t)bytes));
     return IMPC_OK;
 }
+int impc_host_alloc(impc_ctx ctx, int64_t bytes, void **out) {
+    if (!ctx || !out || bytes < 0) return fail(IMPC_INVALID_ARGUMENT, "invalid argument");
+    *out = nullptr;
+    HIP_OK(hipSetDevice(ctx->device));
+    HIP_OK(hipHostMalloc(out, (size_t)std::max<int64_t>(bytes, 1), hipHostMallocDefault));
+    return IMPC_OK;
+}
+int impc_host_free(impc_ctx ctx, void *ptr) {
+    if (!ctx) return fail(IMPC_INVALID_ARGUMENT, "null context");
+    if (ptr) HIP_OK(hipHostFree(ptr));
+    return IMPC_OK;
+}
+int impc_stream_create(impc_ctx ctx, void **stream) {
+    if (!ctx || !stream) return fail(IMPC_INVALID_ARGUMENT, "invalid argument");
+    HIP_OK(hipSetDevice(ctx->device));
+    hipStream_t s = nullptr;
+    HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = (void *)s;
+    return IMPC_OK;
+}
+int impc_stream_destroy(impc_ctx ctx, void *stream) {
+    if (!ctx) return fail(IMPC_INVALID_ARGUMENT, "null context");
+    if (stream) {
+        HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+        HIP_OK(hipStreamDestroy((hipStream_t)stream));
+    }
+    return IMPC_OK;
+}
+int impc_stream_wait(impc_ctx ctx, void *waiter, void *signaler) {
+    if (!ctx) return fail(IMPC_INVALID_ARGUMENT, "null context");
+    HIP_OK(hipSetDevice(ctx->device));
+    hipStream_t w = waiter ? (hipStream_t)waiter : ctx->stream, s = signaler ? (hipStream_t)signaler : ctx->stream;
+    if (w == s) return IMPC_OK;
+    hipEvent_t e = nullptr;
+    HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    hipError_t err = hipEventRecord(e, s);
+    if (err == hipSuccess) err = hipStreamWaitEvent(w, e, 0);
+    (void)hipEventDestroy(e);  // released once the wait has been satisfied
+    if (err != hipSuccess) return fail(IMPC_DEVICE_ERROR, std::string("impc_stream_wait: ") + hipGetErrorString(err));
+    return IMPC_OK;
+}
+int impc_stream_synchronize(impc_ctx ctx, void *stream) {
+    if (!ctx) return fail(IMPC_INVALID_ARGUMENT, "null context");
+    HIP_OK(hipSetDevice(ctx->device));
+    HIP_OK(hipStreamSynchronize(stream ? (hipStream_t)stream : ctx->stream));
+    return IMPC_OK;
+}
+
 int impc_copy_to_host(impc_ctx ctx, void *dst, const void *src, int64_t bytes) {
     if (!ctx || (bytes > 0 && (!dst || !src)) || bytes < 0) return fail(IMPC_INVALID_ARGUMENT, "invalid argument");
     HIP_OK(hipSetDevice(ctx->device));

@@ -101,6 +101,14 @@ _sig("impc_batch_create", C.c_int, _P, C.c_int64, C.c_int64, _i64p, _i64p, _i64p
 _sig("impc_batch_destroy", C.c_int, _P)
 _sig("impc_batch_acquire", C.c_int, _P, C.c_int64, C.c_int64, _i64p, _i64p, _i64p, _i64p, C.c_int64, C.POINTER(_P))
 _sig("impc_batch_release", C.c_int, _P)
+_sig("impc_host_alloc", C.c_int, _P, C.c_int64, C.POINTER(_P))
+_sig("impc_host_free", C.c_int, _P, _P)
+_sig("impc_stream_create", C.c_int, _P, C.POINTER(_P))
+_sig("impc_stream_destroy", C.c_int, _P, _P)
+_sig("impc_stream_wait", C.c_int, _P, _P, _P)
+_sig("impc_stream_synchronize", C.c_int, _P, _P)
+_sig("impc_batch_set_values_async", C.c_int, _P, _P, _P, _P, _P, _P, _P)
+_sig("impc_batch_get_async", C.c_int, _P, _P, _P, _P, _P)
 _sig("impc_batch_set_settings", C.c_int, _P, C.POINTER(Settings))
 _sig("impc_batch_set_values", C.c_int, _P, _dp, _dp, _dp, _dp, _dp)
 _sig("impc_batch_set_values_device", C.c_int, _P, _P, _P, _P, _P, _P)
@@ -242,7 +250,8 @@ EXPORTED = [
     "impc_comm_max", "impc_ctx_timer_mark", "impc_ctx_timer_read", "impc_batch_set_time_limits",
     "impc_ctx_clock_rate", "impc_ctx_clock_check", "impc_batch_set_queue_order", "impc_batch_warm_start_device",
     "impc_batch_set_active", "impc_gather_rows_device", "impc_replan_commit_device", "impc_batch_acquire",
-    "impc_batch_release",
+    "impc_batch_release", "impc_host_alloc", "impc_host_free", "impc_stream_create", "impc_stream_destroy",
+    "impc_stream_wait", "impc_stream_synchronize", "impc_batch_set_values_async", "impc_batch_get_async",
 ]
 
 
@@ -374,6 +383,19 @@ class Batch:
         """impc_batch_warm_start_device: QP-major device arrays x [B][n] (y [B][m] or None = 0)."""
         _check(lib.impc_batch_warm_start_device(self.h, _P(x_ptr) if x_ptr else None, _P(y_ptr) if y_ptr else None),
                "impc_batch_warm_start_device")
+
+    def set_values_async(self, Ax_var, q, l, u, x_ws=None, stream=None):
+        """impc_batch_set_values_async: HostArray / pinned sources, queued on `stream` (a Stream)."""
+        ptr = lambda a: None if a is None else _P(a.ptr if isinstance(a, HostArray) else a.ctypes.data)  # noqa: E731
+        _check(lib.impc_batch_set_values_async(self.h, ptr(Ax_var), ptr(q), ptr(l), ptr(u), ptr(x_ws),
+                                               _P(stream.h) if stream is not None else None),
+               "impc_batch_set_values_async")
+
+    def get_async(self, x, y, info, stream=None):
+        """impc_batch_get_async into HostArrays (any may be None), queued on `stream`."""
+        ptr = lambda a: None if a is None else _P(a.ptr)  # noqa: E731
+        _check(lib.impc_batch_get_async(self.h, ptr(x), ptr(y), ptr(info), _P(stream.h) if stream is not None else None),
+               "impc_batch_get_async")
 
     def set_active(self, count):
         """impc_batch_set_active: the solves take the first `count` QPs."""
@@ -605,6 +627,54 @@ class MpcBuilder:
             self.close()
         except Exception:
             pass
+
+
+class HostArray:
+    """Pinned host memory of the library (impc_host_alloc) viewed as a numpy array: the source /
+    destination of asynchronous transfers (Batch.set_values_async / get_async)."""
+
+    def __init__(self, ctx, shape, dtype=np.float64):
+        self.ctx, self.shape, self.dtype = ctx, tuple(shape), np.dtype(dtype)
+        self.nbytes = int(np.prod(self.shape, dtype=np.int64)) * self.dtype.itemsize
+        p = _P()
+        _check(lib.impc_host_alloc(ctx.h, self.nbytes, C.byref(p)), "impc_host_alloc")
+        self.ptr = p.value
+        buf = (C.c_char * max(self.nbytes, 1)).from_address(self.ptr)
+        self.a = np.frombuffer(buf, self.dtype, count=int(np.prod(self.shape, dtype=np.int64))).reshape(self.shape)
+
+    def free(self):
+        if self.ptr:
+            self.a = None
+            lib.impc_host_free(self.ctx.h, _P(self.ptr))
+            self.ptr = None
+
+
+class Stream:
+    """An extra HIP stream of a context (impc_stream_create), for copy / compute pipelines."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+        p = _P()
+        _check(lib.impc_stream_create(ctx.h, C.byref(p)), "impc_stream_create")
+        self.h = p.value
+
+    def wait(self, other):
+        """This stream waits for the work queued on `other` (a Stream, or None = the context's)."""
+        _check(lib.impc_stream_wait(self.ctx.h, _P(self.h), _P(other.h) if other is not None else None),
+               "impc_stream_wait")
+
+    def synchronize(self):
+        _check(lib.impc_stream_synchronize(self.ctx.h, _P(self.h)), "impc_stream_synchronize")
+
+    def close(self):
+        if self.h:
+            lib.impc_stream_destroy(self.ctx.h, _P(self.h))
+            self.h = None
+
+
+def ctx_stream_wait(ctx, stream):
+    """The context's stream waits for the work queued on `stream` so far."""
+    _check(lib.impc_stream_wait(ctx.h, None, _P(stream.h)), "impc_stream_wait")
 
 
 class DeviceArray:
