@@ -20,6 +20,13 @@ Workloads (--workload):
       Sigma m (impc.distributed.shard_plan).  Strong scaling: the job is fixed, each rank runs one
       grouped launch over its ~42 pattern buckets per step, and each step ends with one RCCL
       all_gather of every QP's cost record (the 64-byte impc_info, read straight from HBM).
+  config5 (BASELINE.json configs[4]): 65,536 N=40 QPs (8192 instances x 8 hypotheses, 10(+1)
+      dynamic obstacles), split by instance across the ranks, as a receding window on persistent
+      workspaces: setup + first solve before the timed region, then every step is
+      osqp_update_lin_cost (the shifted reference) + osqp_update_bounds (the next x0) + the solve
+      resuming from the kept scaling, rho and iterates (impc_batch_update_*_device: each step's
+      values are built on the device beforehand by impc_mpc_build_values_device), and one RCCL
+      all_gather of the cost records (N > 1).
 
 Multi-GPU: one process per GPU.  `python bench.py --gpus N` without a torchrun environment
 starts `torch.distributed.run` with N processes itself (before touching the GPU) and exits with
@@ -243,8 +250,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=("config3", "config4"), default="config3")
-    ap.add_argument("--instances", type=int, default=8192, help="config3: planning instances per GPU (x8 hypotheses)")
+    ap.add_argument("--workload", choices=("config3", "config4", "config5"), default="config3")
+    ap.add_argument("--instances", type=int, default=8192,
+                    help="config3 / config5: planning instances of the job (x8 hypotheses)")
     ap.add_argument("--total-qps", type=int, default=262144, help="config4: QPs of the whole job")
     ap.add_argument("--cpu-sample", type=int, default=8192, help="QPs solved by the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16,
@@ -282,11 +290,12 @@ def main():
     dist = D.init("gloo", local_rank) if world > 1 else None
 
     settings = impc.default_settings(verbose=0)
-    strong = args.workload == "config4" or args.scaling == "strong"
+    strong = args.workload != "config3" or args.scaling == "strong"
     t_gen = time.time()
-    if args.workload == "config3":
-        buckets = scenarios.intent_config(N=20, K=8, instances=args.instances, hyps=8,
-                                          seed=3000 if strong else D.rank_seed(3000, rank))
+    if args.workload in ("config3", "config5"):
+        N_, K_, seed_ = (20, 8, 3000) if args.workload == "config3" else (40, 10, 5000)
+        buckets = scenarios.intent_config(N=N_, K=K_, instances=args.instances, hyps=8,
+                                          seed=seed_ if strong else D.rank_seed(seed_, rank))
         if strong:  # equal instance ranges (every instance carries the same 8 hypotheses)
             bounds = D.equal_instance_bounds(args.instances, args.shard_of or world)
             buckets = scenarios.slice_instances(buckets, int(bounds[rank]), int(bounds[rank + 1]))
@@ -319,12 +328,25 @@ def main():
         dist.all_reduce(t)
         counts = [int(c) for c in t]
     comm = D.make_comm(dist, ctx) if (world > 1 or args.workload == "config4") else None
+    receding = None
+    if args.workload == "config5":  # persistent workspaces: setup + first solve, untimed
+        for _, b in batches:
+            b.set_persistent(True)
+        impc.solve_group([b for _, b in batches]) if len(batches) > 1 else batches[0][1].solve()
+        ctx.synchronize()
+        receding = receding_values(impc, scenarios, ctx, bks, args.warmup + args.steps)
+        rstep = [0]
     max_qps = max(counts)
     recv = impc.DeviceArray(ctx, (world * max_qps,), impc.INFO_DTYPE) if comm is not None else None
     # strong scaling: the cost records of the step's QPs reach every rank inside the step
     gather_in_step = (args.workload == "config4" or (strong and world > 1)) and not args.no_allgather
 
     def launch():
+        if receding is not None:  # the next receding-window step's updates (values already on the device)
+            for (_, b), (q, l, u) in zip(batches, receding[rstep[0]]):
+                b.update_lin_cost_device(q.ptr)
+                b.update_bounds_device(l.ptr, u.ptr)
+            rstep[0] += 1
         if grouped:  # one persistent launch over all pattern buckets (impc_batch_solve_group)
             impc.solve_group([b for _, b in batches])
         else:
@@ -414,14 +436,21 @@ def main():
     traffic, traffic_src = measured_traffic(build_id, total_qps, kernel_name, values_mode, args.workload)
 
     e2e = e2e_serial = None
-    if args.e2e_steps > 0:
+    if args.e2e_steps > 0 and receding is None:
         e2e_serial = end_to_end(impc, ctx, batches, args, grouped)
         if grouped and not args.full_values and all(bk.get("x_ws") is not None for bk in bks):
             e2e = end_to_end_pipelined(impc, ctx, bks, settings, args, qw)
             e2e["frac_of_resident"] = e2e["qps_per_s"] / (total_qps * args.steps / elapsed) if world == 1 else None
 
     cpu = parity = None
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
+    if rank == 0 and world == 1 and args.cpu_sample > 0 and receding is not None:
+        cpu, ref = cpu_baseline_receding(impc, ctx, bks, settings, receding, min(args.cpu_sample, 128))
+        parity = parity_vs_oracle(results, ref)
+        parity["what"] = ("the last receding step's x, y, status, iterations for the CPU sample's QPs vs the oracle's "
+                          "persistent workspaces after the same setup + update sequence (parity unpinned against the "
+                          "real libosqp, DESIGN.md 3)")
+        args.cpu_all_cores = 0
+    elif rank == 0 and world == 1 and args.cpu_sample > 0:
         cpu, ref = cpu_baseline(bks, settings, args.cpu_sample, args.cpu_threads)
         parity = parity_vs_oracle(results, ref)
         if args.cpu_all_cores:
@@ -441,6 +470,15 @@ def main():
             "global_batch": global_batch, "batch_per_gpu": total_qps, "shard_qps": counts,
             "buckets": {str(bk["K"]): int(b.B) for bk, b in batches},
         }
+    elif args.workload == "config5":
+        config = {
+            "workload": ("configs[4]: 65536 N=40 QPs = 8192 instances x 8 intent hypotheses, 10(+1) dynamic obstacles, "
+                         "split by instance over the ranks, receding window on persistent workspaces (per step: "
+                         "update q + update l, u + solve from the kept scaling / rho / iterates), per-step RCCL "
+                         "all-gather of the cost records (N>1)"),
+            "global_batch": global_batch, "batch_per_gpu": total_qps, "shard_qps": counts,
+            "buckets": {str(bk["K"]): int(b.B) for bk, b in batches},
+        }
     else:
         config = {
             "workload": "configs[3]: 262144 mixed-K QPs (K ~ U{0..20}) sharded by Sigma m, per-step RCCL "
@@ -449,7 +487,7 @@ def main():
             "shard_sigma_m": share, "pattern_buckets": len(batches), "allgather": gathered,
         }
     config.update({
-        "horizon": 20,
+        "horizon": bks[0]["N"],
         "settings": "OSQP 0.6.2 defaults, adaptive_rho_interval auto->25, warm-started from previous plan",
         "parallelism": f"independent QPs, {world} rank(s)",
         "queue": ("longest-first (device-estimated key: warm-start violation + q_weight*||q||_inf, "
@@ -536,6 +574,89 @@ def select_candidates(impc, scenarios, ctx, buckets, batch_by_k, pd_params):
     picks = np.bincount(out["best_cand"][out["best_cand"] >= 0], minlength=C)
     return {"instances": int(I), "candidates": int(C), "ms_incl_transfers": 1000.0 * t,
             "picked_histogram": [int(v) for v in picks]}
+
+
+def receding_values(impc, scenarios, ctx, bks, steps):
+    """Config 5's receding window: for shift s = 1..steps, every QP's next values q, l, u (xRef
+    shifted s steps along the path, x0 = the previous plan's state s, the same linearisation points
+    and obstacles -- scenarios.receding_update's step), built on the device by the MPC builder.
+    Returns [step][bucket] = (q, l, u) device arrays."""
+    out = [[] for _ in range(steps)]
+    for bk in bks:
+        N, K = bk["N"], bk["K"]
+        d, inst = bk["instances"], bk["inst"]
+        xref, prev = d["xref"][inst], d["prev"][inst]
+        nb = inst.size
+        p, _ = impc.mpc_params(horizon=N)
+        L = bk["dyn_pos"].shape[2]
+        bld = impc.MpcBuilder(ctx, p, 0, K, L)
+        n, m, nnzP, nnzA = impc.mpc_dims(p, 0, K)
+        keep = [impc.DeviceArray(ctx, np.ascontiguousarray(a, np.float64)) for a in (prev, bk["dyn_pos"], bk["dyn_size"])]
+        Px, Ax = impc.DeviceArray(ctx, (nb, nnzP)), impc.DeviceArray(ctx, (nb, nnzA))
+        step = xref[:, -1, :] - xref[:, -2, :]
+        for s in range(1, steps + 1):
+            ext = xref[:, -1:, :] + step[:, None, :] * np.arange(1, s + 1)[None, :, None]
+            xr = np.concatenate([xref[:, s:], ext], axis=1)
+            tmp = [impc.DeviceArray(ctx, np.ascontiguousarray(a, np.float64))
+                   for a in (prev[:, s, 0:3], prev[:, s, 3:6], xr)]
+            q, l, u = impc.DeviceArray(ctx, (nb, n)), impc.DeviceArray(ctx, (nb, m)), impc.DeviceArray(ctx, (nb, m))
+            bld.build(nb, tmp[0].ptr, tmp[1].ptr, tmp[2].ptr, keep[0].ptr, None, None, None, keep[1].ptr, keep[2].ptr,
+                      Px.ptr, q.ptr, Ax.ptr, l.ptr, u.ptr)
+            ctx.synchronize()
+            for t in tmp:
+                t.free()
+            out[s - 1].append((q, l, u))
+        for a in keep + [Px, Ax]:
+            a.free()
+        bld.close()
+    return out
+
+
+def rows_to_host(impc, ctx, darr, k):
+    """The first k rows of a QP-major device array."""
+    row = darr.nbytes // darr.shape[0]
+    out = np.empty((k,) + tuple(darr.shape[1:]), darr.dtype)
+    impc._check(impc.lib.impc_copy_to_host(ctx.h, impc._P(out.ctypes.data), impc._P(darr.ptr), row * k),
+                "impc_copy_to_host")
+    return out
+
+
+def cpu_baseline_receding(impc, ctx, bks, settings, receding, sample):
+    """Config 5's CPU path: the oracle's persistent workspaces (osqp_setup, warm start, solve once,
+    then per receding step osqp_update_lin_cost + osqp_update_bounds + osqp_solve, the reference's
+    polyTrajSolver pattern) over a bounded sample -- the first QPs of each bucket, one thread; the
+    timed part is the update + solve steps.  Returns (line object, [(k, x, y, info) per bucket] of
+    the last step, for the parity check)."""
+    from oracle import osqp_oracle as ora
+    total = sum(bk["values"]["q"].shape[0] for bk in bks)
+    s = ora.settings_from(settings)
+    ref, t_all, n_all = [], 0.0, 0
+    for j, bk in enumerate(bks):
+        B = bk["values"]["q"].shape[0]
+        k = min(B, max(1, int(round(sample * B / total))))
+        v = bk["values"]
+        ups = [tuple(rows_to_host(impc, ctx, a, k) for a in step[j]) for step in receding]
+        xs, ys, infos = [], [], []
+        for i in range(k):
+            w = ora.Workspace(bk["pattern"], v["Px"][i], v["q"][i], v["Ax"][i], v["l"][i], v["u"][i], s)
+            w.warm_start(bk["x_ws"][i], np.zeros(int(bk["pattern"]["m"])))
+            w.solve()
+            t = time.perf_counter()
+            for q, l, u in ups:
+                w.update_lin_cost(q[i])
+                w.update_bounds(l[i], u[i])
+                x, y, info = w.solve()
+            t_all += time.perf_counter() - t
+            n_all += len(ups)
+            w.close()
+            xs.append(x)
+            ys.append(y)
+            infos.append(info)
+        ref.append((k, np.array(xs), np.array(ys), np.array(infos, dtype=infos[0].dtype)))
+    return {"value": n_all / t_all, "unit": "QP-solves/s", "cores": 1, "kind": "port",
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_info(),
+            "sample": f"{sum(r[0] for r in ref)} QPs of the workload (first of each bucket) x {len(receding)} receding "
+                      f"steps, oracle persistent workspaces (update q, update l/u, solve), one thread ({t_all:.1f} s)"}, ref
 
 
 def measured_traffic(build_id, qps, kernel, values_mode, workload):

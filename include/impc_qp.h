@@ -204,6 +204,11 @@ int impc_batch_device_results(impc_batch b, double **x, double **y, impc_info **
  * (equality / inequality / loose), and keep the iterates as the next warm start. */
 int impc_batch_update_lin_cost(impc_batch b, const double *q);
 int impc_batch_update_bounds(impc_batch b, const double *l, const double *u);
+/* The same from DEVICE arrays (q [B][n]; l, u [B][m]), stream-ordered on the context stream after
+ * every launch already issued, no host synchronisation and no l <= u check (the caller's; a
+ * receding-horizon loop builds the next step's values on the device). */
+int impc_batch_update_lin_cost_device(impc_batch b, const double *q);
+int impc_batch_update_bounds_device(impc_batch b, const double *l, const double *u);
 
 /* Kernel selection.  AUTO picks the one-QP-per-wavefront structured kernel when the pattern is
  * the stage-structured mpcPlanner QP and fits its register layout, else the

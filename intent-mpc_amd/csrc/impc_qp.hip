@@ -1917,6 +1917,63 @@ int impc_batch_update_bounds(impc_batch b, const double *l, const double *u) {
     return IMPC_OK;
 }
 
+int impc_batch_update_lin_cost_device(impc_batch b, const double *q) {
+    if (!b || !q) return fail(IMPC_INVALID_ARGUMENT, "null batch or q");
+    HIP_OK(hipSetDevice(b->ctx->device));
+    hipStream_t st = b->ctx->stream;
+    const size_t bytes = sizeof(double) * (size_t)(b->n * b->B);
+    if (use_structured(b)) {
+        if (!b->persist_on || !b->persist_valid)
+            return fail(IMPC_WORKSPACE_NOT_INIT_ERROR,
+                        "structured kernel: impc_batch_set_persistent(b, 1) and one solve before updates");
+        IMPC_TRY(ctx_order_after_all(b->ctx, st));
+        HIP_OK(hipMemcpyAsync(b->in_q, q, bytes, hipMemcpyDeviceToDevice, st));
+        b->q_by_update = true;
+        b->generic_dirty = true;
+        return IMPC_OK;
+    }
+    if (!b->generic_setup_done || b->generic_dirty)
+        return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "setup has not run on current data");
+    IMPC_TRY(ctx_order_after_all(b->ctx, st));
+    HIP_OK(hipMemcpyAsync(b->in_q, q, bytes, hipMemcpyDeviceToDevice, st));
+    IMPC_TRY(interleave(b, b->in_q, const_cast<double *>(b->dwk.q), b->n, st));
+    hipLaunchKernelGGL(k_update_q, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk, b->dst, b->B);
+    HIP_OK(hipGetLastError());
+    return IMPC_OK;
+}
+
+int impc_batch_update_bounds_device(impc_batch b, const double *l, const double *u) {
+    if (!b || (b->m && (!l || !u))) return fail(IMPC_INVALID_ARGUMENT, "null batch or bounds");
+    HIP_OK(hipSetDevice(b->ctx->device));
+    hipStream_t st = b->ctx->stream;
+    const size_t bytes = sizeof(double) * (size_t)(b->m * b->B);
+    if (use_structured(b)) {
+        if (!b->persist_on || !b->persist_valid)
+            return fail(IMPC_WORKSPACE_NOT_INIT_ERROR,
+                        "structured kernel: impc_batch_set_persistent(b, 1) and one solve before updates");
+        IMPC_TRY(ctx_order_after_all(b->ctx, st));
+        if (bytes) {
+            HIP_OK(hipMemcpyAsync(b->in_l, l, bytes, hipMemcpyDeviceToDevice, st));
+            HIP_OK(hipMemcpyAsync(b->in_u, u, bytes, hipMemcpyDeviceToDevice, st));
+        }
+        b->generic_dirty = true;
+        return IMPC_OK;
+    }
+    if (!b->generic_setup_done || b->generic_dirty)
+        return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "setup has not run on current data");
+    IMPC_TRY(ctx_order_after_all(b->ctx, st));
+    if (bytes) {
+        HIP_OK(hipMemcpyAsync(b->in_l, l, bytes, hipMemcpyDeviceToDevice, st));
+        HIP_OK(hipMemcpyAsync(b->in_u, u, bytes, hipMemcpyDeviceToDevice, st));
+    }
+    IMPC_TRY(interleave(b, b->in_l, const_cast<double *>(b->dwk.l), b->m, st));
+    IMPC_TRY(interleave(b, b->in_u, const_cast<double *>(b->dwk.u), b->m, st));
+    hipLaunchKernelGGL(k_update_bounds, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk, b->dst,
+                       b->B);
+    HIP_OK(hipGetLastError());
+    return IMPC_OK;
+}
+
 int impc_batch_get_stats(impc_batch b, impc_batch_stats *out) {
     if (!b || !out) return fail(IMPC_INVALID_ARGUMENT, "null argument");
     std::memset(out, 0, sizeof(*out));

@@ -125,6 +125,8 @@ _sig("impc_batch_get", C.c_int, _P, _dp, _dp, C.c_void_p)
 _sig("impc_batch_device_results", C.c_int, _P, C.POINTER(_P), C.POINTER(_P), C.POINTER(_P))
 _sig("impc_batch_update_lin_cost", C.c_int, _P, _dp)
 _sig("impc_batch_update_bounds", C.c_int, _P, _dp, _dp)
+_sig("impc_batch_update_lin_cost_device", C.c_int, _P, _P)
+_sig("impc_batch_update_bounds_device", C.c_int, _P, _P, _P)
 _sig("impc_batch_get_stats", C.c_int, _P, C.POINTER(Stats))
 _sig("impc_batch_get_perm", C.c_int, _P, _i64p)
 _sig("impc_batch_set_profiling", C.c_int, _P, C.c_int)
@@ -252,6 +254,7 @@ EXPORTED = [
     "impc_batch_set_active", "impc_gather_rows_device", "impc_replan_commit_device", "impc_batch_acquire",
     "impc_batch_release", "impc_host_alloc", "impc_host_free", "impc_stream_create", "impc_stream_destroy",
     "impc_stream_wait", "impc_stream_synchronize", "impc_batch_set_values_async", "impc_batch_get_async",
+    "impc_batch_update_lin_cost_device", "impc_batch_update_bounds_device",
 ]
 
 
@@ -457,6 +460,14 @@ class Batch:
             raise ValueError(f"update_bounds: l / u have {la.size} / {ua.size} values, expected B*m = "
                              f"{self.B * self.m}")
         _check(lib.impc_batch_update_bounds(self.h, _d(la), _d(ua)), "impc_batch_update_bounds")
+
+    def update_lin_cost_device(self, q_ptr):
+        """impc_batch_update_lin_cost_device: q [B][n] in device memory (address)."""
+        _check(lib.impc_batch_update_lin_cost_device(self.h, _P(q_ptr)), "impc_batch_update_lin_cost_device")
+
+    def update_bounds_device(self, l_ptr, u_ptr):
+        """impc_batch_update_bounds_device: l, u [B][m] in device memory (addresses)."""
+        _check(lib.impc_batch_update_bounds_device(self.h, _P(l_ptr), _P(u_ptr)), "impc_batch_update_bounds_device")
 
     def stats(self):
         s = Stats()

@@ -96,6 +96,39 @@ def test_config5_receding_window_persistent(ctx):
                 compare(one, (ref[0][None], ref[1][None], np.array([ref[2]], dtype=ref[2].dtype)))
 
 
+def test_config5_device_updates_equal_host_updates(ctx):
+    """bench.py --workload config5's step: the receding values built on the device and applied by
+    impc_batch_update_*_device give bit for bit the solves of the host-array updates."""
+    cfg = scenarios.intent_config(N=40, K=10, instances=2, hyps=8, seed=5200)
+    s = impc.default_settings(verbose=0)
+    for kk, bk in sorted(cfg.items()):
+        v = bk["values"]
+        v2 = scenarios.receding_update(bk, shift=1)
+        res = []
+        for dev in (False, True):
+            b = _batch(ctx, bk, s)
+            keep = []
+            try:
+                b.set_persistent(True)
+                b.solve()
+                if dev:
+                    keep = [impc.DeviceArray(ctx, np.ascontiguousarray(v2[k])) for k in ("q", "l", "u")]
+                    b.update_lin_cost_device(keep[0].ptr)
+                    b.update_bounds_device(keep[1].ptr, keep[2].ptr)
+                else:
+                    b.update_lin_cost(v2["q"])
+                    b.update_bounds(v2["l"], v2["u"])
+                b.solve()
+                res.append(b.get())
+            finally:
+                b.close()
+                for d in keep:
+                    d.free()
+        np.testing.assert_array_equal(res[0][0], res[1][0])
+        np.testing.assert_array_equal(res[0][2]["iter"], res[1][2]["iter"])
+        assert np.array_equal(v2["Px"], v["Px"])
+
+
 def test_groups_on_two_caller_streams(ctx):
     """Two grouped launches on two caller streams, the second replacing the context's group-entry
     table while the first may still run (impc_qp.h: caller streams are ordered against every
