@@ -116,7 +116,7 @@ int impc_repeat_rows_device(impc_ctx ctx, const void *src, int64_t rows, int64_t
                             void *dst, void *stream);
 
 /* Row gather on the device: dst row r = src row idx[r], r < count (idx a DEVICE int64 array; rows
- * of row_bytes bytes, a multiple of 8).  The batched replan compacts the planning instances that
+ * of row_bytes bytes, a multiple of 4).  The batched replan compacts the planning instances that
  * take one makePlanWithPred branch with it.  Asynchronous on `stream`. */
 int impc_gather_rows_device(impc_ctx ctx, const void *src, int64_t row_bytes, const int64_t *idx, int64_t count,
                             void *dst, void *stream);

@@ -84,9 +84,10 @@ __global__ void k_repeat_rows(const double *__restrict__ src, int64_t rows, int6
         dst[t] = src[r * words + w];
     }
 }
-// dst row r = src row idx[r]
-__global__ void k_gather_rows(const double *__restrict__ src, int64_t words, const int64_t *__restrict__ idx,
-                              int64_t count, double *__restrict__ dst) {
+// dst row r = src row idx[r] (T: 8- or 4-byte words)
+template <class T>
+__global__ void k_gather_rows(const T *__restrict__ src, int64_t words, const int64_t *__restrict__ idx, int64_t count,
+                              T *__restrict__ dst) {
     const int64_t n = count * words;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
         const int64_t w = t % words, r = t / words;
@@ -97,16 +98,21 @@ __global__ void k_gather_rows(const double *__restrict__ src, int64_t words, con
 
 extern "C" int impc_gather_rows_device(impc_ctx ctx, const void *src, int64_t row_bytes, const int64_t *idx,
                                        int64_t count, void *dst, void *stream) {
-    if (!ctx || count < 0 || row_bytes < 0 || (row_bytes & 7) || (count && row_bytes && (!src || !dst || !idx)))
-        return fail(IMPC_INVALID_ARGUMENT, "invalid row-gather arguments (row_bytes a multiple of 8)");
+    if (!ctx || count < 0 || row_bytes < 0 || (row_bytes & 3) || (count && row_bytes && (!src || !dst || !idx)))
+        return fail(IMPC_INVALID_ARGUMENT, "invalid row-gather arguments (row_bytes a multiple of 4)");
     if (!count || !row_bytes) return IMPC_OK;
     HIP_OK(hipSetDevice(ctx->device));
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
     IMPC_TRY(ctx_order_launch(ctx, st));
-    const int64_t n = count * (row_bytes / 8);
+    const bool w8 = (row_bytes & 7) == 0;
+    const int64_t words = row_bytes / (w8 ? 8 : 4), n = count * words;
     const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)ctx->num_cu * 8);
-    hipLaunchKernelGGL(impc_reftraj::k_gather_rows, dim3(blocks), dim3(256), 0, st, (const double *)src,
-                       row_bytes / 8, idx, count, (double *)dst);
+    if (w8)
+        hipLaunchKernelGGL(impc_reftraj::k_gather_rows<double>, dim3(blocks), dim3(256), 0, st, (const double *)src,
+                           words, idx, count, (double *)dst);
+    else
+        hipLaunchKernelGGL(impc_reftraj::k_gather_rows<uint32_t>, dim3(blocks), dim3(256), 0, st,
+                           (const uint32_t *)src, words, idx, count, (uint32_t *)dst);
     HIP_OK(hipGetLastError());
     return ctx_note_launch(ctx, st);
 }
