@@ -134,7 +134,8 @@ int impc_batch_destroy(impc_batch b);
  * impc_batch_create leaves (default settings, no values, no warm start, no time limits, FIFO
  * queue, every QP active, persistent workspace off, profiling off).  impc_batch_release returns it
  * to the pool: the next acquire's uploads are stream-ordered after anything still reading it.
- * impc_ctx_destroy frees the pool.  The OsqpEigen front end's Solver (one per solveTraj call,
+ * impc_ctx_destroy frees the pool (impc_batch_destroy of a released batch takes it out of the
+ * pool first).  The OsqpEigen front end's Solver (one per solveTraj call,
  * mpcPlanner.cpp:436 / :527) lives on it. */
 int impc_batch_acquire(impc_ctx ctx, int64_t n, int64_t m, const int64_t *Pp, const int64_t *Pi, const int64_t *Ap,
                        const int64_t *Ai, int64_t batch, impc_batch *out);

@@ -1251,8 +1251,9 @@ int impc_ctx_destroy(impc_ctx ctx) {
     if (!ctx) return IMPC_OK;
     (void)hipSetDevice(ctx->device);
     (void)ctx_quiesce(ctx);
-    for (auto &e : ctx->pool) (void)impc_batch_destroy(e.second);
+    auto pool = std::move(ctx->pool);  // (impc_batch_destroy looks the batch up in ctx->pool)
     ctx->pool.clear();
+    for (auto &e : pool) (void)impc_batch_destroy(e.second);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     for (auto &g : ctx->groups)
         if (g.d) (void)hipFree(g.d);
@@ -1337,6 +1338,13 @@ int impc_batch_destroy(impc_batch b) {
     if (b->ctx) {
         (void)hipSetDevice(b->ctx->device);
         (void)ctx_quiesce(b->ctx);
+        // a released batch destroyed by its holder leaves the pool (no second destroy at ctx_destroy)
+        auto &pool = b->ctx->pool;
+        for (size_t k = 0; k < pool.size(); k++)
+            if (pool[k].second == b) {
+                pool.erase(pool.begin() + (std::ptrdiff_t)k);
+                break;
+            }
     }
     for (hipEvent_t e : b->ev)
         if (e) (void)hipEventDestroy(e);

@@ -201,5 +201,6 @@ def test_workspace_pool_reuses_and_resets(ctx):
     assert (info2["iter"] > 7).all() and (info2["status_val"] == 1).all()
     assert impc.lib.impc_batch_acquire(ctx.h, pat["n"], pat["m"], *[ip(a) for a in arrs], 1, C.byref(h3)) == 0
     assert h3.value != h2.value  # other capacity: a new batch
+    b.h = None  # released below: the pool owns it (Batch.__del__ must not destroy it)
     for h in (h2, h3):
         assert impc.lib.impc_batch_release(h) == 0
