@@ -263,7 +263,10 @@ int impc_batch_get_stats(impc_batch b, impc_batch_stats *out);
 /* Kernel timing with HIP events recorded on the solve stream around k_setup, k_solve and the
  * output transposes (profiling on: events are recorded by every subsequent setup/solve). */
 int impc_batch_set_profiling(impc_batch b, int on);
-/* Durations (ms) of the last profiled setup / solve-kernel / output-transpose launches. */
+/* Durations (ms) of the last profiled setup / solve-kernel / output-transpose launches.  For the
+ * structured kernel solve_ms spans the whole solve call on its stream: with the longest-first queue
+ * (impc_batch_set_queue_order) that includes the queue-key kernel and the radix sort (~0.7 ms at
+ * 65,536 QPs) before the solver kernel; the per-QP latencies (impc_batch_get_qp_latency) do not. */
 int impc_batch_get_timings(impc_batch b, double *setup_ms, double *solve_ms, double *output_ms);
 
 /* Persistent workspace (structured kernel; OSQP's workspace kept between osqp_solve calls, as a

@@ -950,7 +950,8 @@ int queue_order(impc_batch *bs, const int64_t *firsts, int count, int64_t total,
     bool any = false;
     for (int k = 0; k < count; k++) any = any || bs[k]->queue_mode == IMPC_QUEUE_LONGEST_FIRST;
     if (!any || total < 2) return IMPC_OK;
-    if (total > (int64_t)UINT32_MAX) return fail(IMPC_UNSUPPORTED, "queue order: too many QPs in one launch");
+    // the radix sort takes an int item count
+    if (total > (int64_t)INT32_MAX) return fail(IMPC_UNSUPPORTED, "queue order: too many QPs in one launch");
     impc_batch h = bs[0];
     size_t tmp = 0;
     HIP_OK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, (const double *)nullptr, (double *)nullptr,

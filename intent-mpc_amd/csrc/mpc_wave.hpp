@@ -1396,7 +1396,11 @@ struct WaveQP {
         // time_limit clock: from the start of the QP's setup (load, scaling, factorisation), as
         // OSQP 0.6.2 counts setup_time + solve time on a first run (every solveTraj call is one);
         // the profiling record (qpt) starts at the same tick, so a QP stopped by its limit always
-        // shows a recorded latency of at least that limit
+        // shows a recorded latency of at least that limit.  A persistent-workspace resume (OSQP's
+        // non-first run) counts from the same tick: OSQP then counts update_time + solve time, and
+        // here the update work (the scaling replay, the row types, the refactorisation) runs at the
+        // start of the resumed solve -- one difference: OSQP refactors on osqp_update_bounds only
+        // when a row changes type, the resume always does (its time counts against the limit)
         const uint64_t t0 = device_clock();
         rw = (int)(b % (NL / 64));  // spread the serial recursions of co-resident QPs over SIMDs
 #if defined(__HIP_DEVICE_COMPILE__)
