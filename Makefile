@@ -31,6 +31,7 @@ PROFLIB := $(LIBDIR)/libimpc_qp_prof.so
 ORACLE  := $(ORADIR)/libosqp_oracle.so
 HARNESS := $(HARNDIR)/libimpc_core_cpu.so
 EMU     := $(HARNDIR)/libwave_emu.so
+EMU64   := $(HARNDIR)/libwave_emu64.so
 SHIMT   := $(HARNDIR)/shim_test
 REPLANX := $(HARNDIR)/replan_example
 
@@ -38,7 +39,7 @@ REPLANX := $(HARNDIR)/replan_example
 all: lib oracle harness
 lib: $(LIB)
 oracle: $(ORACLE)
-harness: $(HARNESS) $(EMU) $(SHIMT) $(REPLANX)
+harness: $(HARNESS) $(EMU) $(EMU64) $(SHIMT) $(REPLANX)
 
 $(LIBDIR)/impc_qp.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symbolic.hpp $(CSRC)/mpc_wave.hpp \
 		$(CSRC)/mpc_structure.hpp $(CSRC)/select.hpp $(CSRC)/mpc_build.hpp $(CSRC)/mpc_qp_internal.hpp \
@@ -91,6 +92,13 @@ $(EMU): $(ROOT)/tests/native/wave_emu.cpp $(CSRC)/mpc_wave.hpp $(CSRC)/admm_core
 		$(CSRC)/mpc_structure.hpp
 	@mkdir -p $(HARNDIR)
 	$(HIPCC) -x hip --offload-host-only -std=c++20 -O2 -fPIC -shared -ffp-contract=off \
+		$(ROOT)/tests/native/wave_emu.cpp -x c++ $(CSRC)/mpc_structure.cpp -o $@
+
+# the one-QP-per-wavefront team shape (64 lanes, four variables per lane) in the same emulation
+$(EMU64): $(ROOT)/tests/native/wave_emu.cpp $(CSRC)/mpc_wave.hpp $(CSRC)/admm_core.hpp $(CSRC)/mpc_structure.cpp \
+		$(CSRC)/mpc_structure.hpp
+	@mkdir -p $(HARNDIR)
+	$(HIPCC) -x hip --offload-host-only -std=c++20 -O2 -fPIC -shared -ffp-contract=off -DEMU_NL=64 \
 		$(ROOT)/tests/native/wave_emu.cpp -x c++ $(CSRC)/mpc_structure.cpp -o $@
 
 # OsqpEigen shim driver (test-only Eigen stand-in; links the product library)

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/impc_qp.h"
@@ -70,8 +71,18 @@ constexpr int kTile = 64;   // transpose tile edge
 #ifndef IMPC_WAVES_PER_SIMD
 #define IMPC_WAVES_PER_SIMD 2
 #endif
+// general-row slots per lane of the instantiated kernels (mg <= kTeam * GS), and of the two-tier
+// products instances
+#ifndef IMPC_GS_MAX
+#define IMPC_GS_MAX 4
+#endif
+#ifndef IMPC_TIER_GS_MAX
+#define IMPC_TIER_GS_MAX 3
+#endif
 constexpr int kTeam = IMPC_TEAM;   // lanes per QP (IMPC_TEAM / 64 wavefronts)
 constexpr int kWaveVS = IMPC_VS;   // variable slots per lane (n <= kTeam * kWaveVS)
+constexpr int kGsMax = IMPC_GS_MAX, kTierGsMax = IMPC_TIER_GS_MAX;
+static_assert(kGsMax >= 2 && kGsMax <= 8 && kTierGsMax >= 2 && kTierGsMax <= kGsMax, "general-row slot range");
 // long-horizon shape (e.g. N = 40, n = 515): three variable slots per lane, one wave per SIMD
 // (the per-QP LDS then allows one team per CU anyway)
 constexpr int kWaveVSLong = 3;
@@ -631,10 +642,14 @@ struct impc_batch_s {
     hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     bool ev_setup = false, ev_solve = false;
     // small batches: pinned host staging of the inputs, warm start and results (one DMA each way
-    // instead of a pageable copy + synchronisation per array), regions [inputs][x ws][y ws][x][y][info]
+    // instead of a pageable copy + synchronisation per array), regions [inputs][x ws][y ws][x][y][info].
+    // impc_batch_set_values / _warm_start only fill the staging (in_dirty / ws_dirty); the first call
+    // that needs them on the device queues one DMA for both (flush_staged)
     double *h_stage = nullptr;
-    hipEvent_t ev_in = nullptr, ev_ws = nullptr;  // the last staged input / warm-start DMA
-    bool in_pending = false, ws_pending = false;
+    hipEvent_t ev_in = nullptr;  // the last staged DMA (the staging is rewritten only after it)
+    bool in_pending = false;
+    bool in_dirty = false, ws_dirty = false;
+    size_t ws_len = 0;  // doubles of the staged warm start (x, or x and y)
     uint64_t pool_hash = 0;
 };
 
@@ -994,6 +1009,33 @@ int queue_order(impc_batch *bs, const int64_t *firsts, int count, int64_t total,
     return IMPC_OK;
 }
 
+// runtime (VS, GS, TIER) -> the instantiated kernel class: f(VS, GS, TIER) as integral constants
+template <int V, int G, bool TR, class F>
+int shape_call(F &&f) {
+    return f(std::integral_constant<int, V>{}, std::integral_constant<int, G>{}, std::integral_constant<bool, TR>{});
+}
+template <int V, bool TR, class F>
+int with_gs(int gs, F &&f) {
+    constexpr int gmax = TR ? kTierGsMax : (V == kWaveVS ? kGsMax : 4);
+    switch (gs) {
+        case 2: return shape_call<V, 2, TR>(f);
+        case 3: return shape_call<V, 3, TR>(f);
+        case 4: if constexpr (gmax >= 4) return shape_call<V, 4, TR>(f); break;
+        case 5: if constexpr (gmax >= 5) return shape_call<V, 5, TR>(f); break;
+        case 6: if constexpr (gmax >= 6) return shape_call<V, 6, TR>(f); break;
+        case 7: if constexpr (gmax >= 7) return shape_call<V, 7, TR>(f); break;
+        case 8: if constexpr (gmax >= 8) return shape_call<V, 8, TR>(f); break;
+        default: break;
+    }
+    return fail(IMPC_UNSUPPORTED, "no structured kernel for this size");
+}
+template <class F>
+int with_shape(int vs, int gs, bool tier, F &&f) {
+    if (vs == kWaveVS) return tier ? with_gs<kWaveVS, true>(gs, f) : with_gs<kWaveVS, false>(gs, f);
+    if (vs == kWaveVSLong && !tier) return with_gs<kWaveVSLong, false>(gs, f);
+    return fail(IMPC_UNSUPPORTED, "no structured kernel for this size");
+}
+
 // After a structured solve of a persistent batch: its workspace holds the scaled iterates, and an
 // explicit warm start has been consumed (OSQP applies osqp_warm_start once).
 void structured_solved(impc_batch b) {
@@ -1017,16 +1059,9 @@ int structured_solve(impc_batch b, hipStream_t st) {
     const uint32_t *ord = nullptr;
     const int64_t first0 = 0;
     IMPC_TRY(queue_order(&b, &first0, 1, b->Bact, st, &ord));
-    int rc;
-    switch (b->vs * 8 + b->gs) {
-        case kWaveVS * 8 + 2: rc = launch_wave<kWaveVS, 2>(b, st, io, ord); break;
-        case kWaveVS * 8 + 3: rc = launch_wave<kWaveVS, 3>(b, st, io, ord); break;
-        case kWaveVS * 8 + 4: rc = launch_wave<kWaveVS, 4>(b, st, io, ord); break;
-        case kWaveVSLong * 8 + 2: rc = launch_wave<kWaveVSLong, 2>(b, st, io, ord); break;
-        case kWaveVSLong * 8 + 3: rc = launch_wave<kWaveVSLong, 3>(b, st, io, ord); break;
-        case kWaveVSLong * 8 + 4: rc = launch_wave<kWaveVSLong, 4>(b, st, io, ord); break;
-        default: return fail(IMPC_UNSUPPORTED, "no structured kernel for this size");
-    }
+    const int rc = with_shape(b->vs, b->gs, false, [&](auto vs, auto gs, auto) {
+        return launch_wave<decltype(vs)::value, decltype(gs)::value>(b, st, io, ord);
+    });
     if (rc) return rc;
     structured_solved(b);
     if (b->profile) {
@@ -1060,12 +1095,12 @@ int launch_group(impc_ctx ctx, hipStream_t st, const GroupEntry *entries, int co
 
 // dynamic LDS bytes of the structured kernel for a shape (team VS, GS) and pattern (CG, n)
 size_t wave_lds_bytes(int vs, int gs, const impc::WaveTables &T) {
-    auto sz = [&](auto ld) { return sizeof(double) * (size_t)decltype(ld)::size(T); };
-    if (vs == kWaveVS)
-        return gs == 2 ? sz(impc::WaveLds<kTeam, kWaveVS, 2>{}) : gs == 3 ? sz(impc::WaveLds<kTeam, kWaveVS, 3>{})
-                                                                          : sz(impc::WaveLds<kTeam, kWaveVS, 4>{});
-    return gs == 2 ? sz(impc::WaveLds<kTeam, kWaveVSLong, 2>{}) : gs == 3 ? sz(impc::WaveLds<kTeam, kWaveVSLong, 3>{})
-                                                                          : sz(impc::WaveLds<kTeam, kWaveVSLong, 4>{});
+    size_t bytes = 0;
+    (void)with_shape(vs, gs, false, [&](auto v, auto g, auto) {
+        bytes = sizeof(double) * (size_t)impc::WaveLds<kTeam, decltype(v)::value, decltype(g)::value>::size(T);
+        return IMPC_OK;
+    });
+    return bytes;
 }
 
 int prepare_structured(impc_batch b) {
@@ -1077,7 +1112,10 @@ int prepare_structured(impc_batch b) {
     }
     b->vs = b->ms->n <= kTeam * kWaveVS ? kWaveVS : kWaveVSLong;
     const int mg = b->ms->mg;
-    b->gs = mg <= 2 * kTeam ? 2 : mg <= 3 * kTeam ? 3 : mg <= 4 * kTeam ? 4 : 0;
+    {
+        const int g = std::max(2, (mg + kTeam - 1) / kTeam);  // general-row slots per lane
+        b->gs = g <= (b->vs == kWaveVS ? kGsMax : 4) ? g : 0;
+    }
     const impc::MpcStructure &s = *b->ms;
     impc::WaveTables &t = b->wt;
     t.n = s.n;
@@ -1093,7 +1131,7 @@ int prepare_structured(impc_batch b) {
     t.HS = 0;
     t.T1r = impc::WaveLds<kTeam, kWaveVS, 2>::cg4(s.CG);
     // (two-tier instances: the one-variable-per-lane shape with 2 or 3 general-row slots)
-    if (b->gs && b->vs == kWaveVS && b->gs <= 3) {
+    if (b->gs && b->vs == kWaveVS && b->gs <= kTierGsMax) {
         const int per_cu = std::max(1, (4 * IMPC_WAVES_PER_SIMD) / (kTeam / 64));
         const size_t budget = (160 * 1024 - 1024) / (size_t)per_cu;
         if (wave_lds_bytes(b->vs, b->gs, t) > budget) {
@@ -1127,8 +1165,8 @@ int prepare_structured(impc_batch b) {
     for (size_t k = 0; k < arrs.size(); k++) *dst_ptrs[k] = base + offs[k];
     // per-QP HBM scratch for the scaling vectors: long-horizon shape only (the default shape keeps
     // them in LDS, mpc_wave.hpp WaveLds::ONCHIP)
-    const size_t scal_bytes =
-        b->vs == kWaveVS ? 0 : sizeof(double) * (size_t)b->B * (size_t)(2 * s.n + s.mg);
+    const bool onchip = b->vs == kWaveVS && impc::WaveLds<kTeam, kWaveVS, 2>::ONCHIP;
+    const size_t scal_bytes = onchip ? 0 : sizeof(double) * (size_t)b->B * (size_t)(2 * s.n + s.mg);
     if (scal_bytes) HIP_OK(hipMalloc((void **)&b->d_scal, scal_bytes));
     HIP_OK(hipMalloc((void **)&b->d_counter, 256));
     b->device_bytes += (int64_t)(scal_bytes + h.size() * 4 + 256);
@@ -1149,7 +1187,29 @@ int stage_ensure(impc_batch b) {
     if (b->h_stage) return IMPC_OK;
     HIP_OK(hipHostMalloc((void **)&b->h_stage, 8 * stage_len(b), hipHostMallocDefault));
     HIP_OK(hipEventCreateWithFlags(&b->ev_in, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&b->ev_ws, hipEventDisableTiming));
+    return IMPC_OK;
+}
+// before the host rewrites the staging: the last DMA from it has completed
+int stage_wait(impc_batch b) {
+    if (b->in_pending) HIP_OK(hipEventSynchronize(b->ev_in));
+    b->in_pending = false;
+    return IMPC_OK;
+}
+// the staged inputs and / or warm start to the device: one DMA on the context stream, after every
+// launch (on any stream) that may still read the arrays it replaces.  The device regions
+// [inputs][x ws][y ws] are contiguous in the staging's order, so both go in one copy.  Called by
+// every entry point that reads or rewrites the device inputs.
+int flush_staged(impc_batch b) {
+    if (!b->in_dirty && !b->ws_dirty) return IMPC_OK;
+    HIP_OK(hipSetDevice(b->ctx->device));
+    hipStream_t st = b->ctx->stream;
+    IMPC_TRY(ctx_order_after_all(b->ctx, st));
+    const size_t in_len = stage_in_len(b);
+    const size_t off = b->in_dirty ? 0 : in_len, end = b->ws_dirty ? in_len + b->ws_len : in_len;
+    HIP_OK(hipMemcpyAsync(b->in_Px + off, b->h_stage + off, sizeof(double) * (end - off), hipMemcpyHostToDevice, st));
+    HIP_OK(hipEventRecord(b->ev_in, st));
+    b->in_pending = true;
+    b->in_dirty = b->ws_dirty = false;
     return IMPC_OK;
 }
 
@@ -1168,6 +1228,7 @@ void reset_batch(impc_batch b) {
     b->shared = b->shared_expanded = false;
     b->generic_dirty = true;
     b->generic_setup_done = b->generic_first_run = false;
+    b->in_dirty = b->ws_dirty = false;
 }
 
 uint64_t pattern_hash(int64_t n, int64_t m, int64_t batch, const int64_t *Pp, const int64_t *Pi, const int64_t *Ap,
@@ -1322,10 +1383,13 @@ int impc_batch_create(impc_ctx ctx, int64_t n, int64_t m, const int64_t *Pp, con
     p += b->n * B;
     b->in_yws = p;
     IMPC_TRY(fill0_sync(ctx->stream, b->d_in, in_bytes));
-    if (hipMalloc((void **)&b->d_xout, sizeof(double) * (size_t)(std::max<int64_t>(n, 1) * B)) != hipSuccess ||
-        hipMalloc((void **)&b->d_yout, sizeof(double) * (size_t)(std::max<int64_t>(m, 1) * B)) != hipSuccess ||
-        hipMalloc((void **)&b->d_info, sizeof(impc_info) * (size_t)B) != hipSuccess)
+    // results [x][y][info] in one allocation, so a small batch's results come back in one DMA
+    // (impc_batch_get; the staging's result regions have the same order)
+    const size_t xo_len = (size_t)n * (size_t)B, yo_len = (size_t)std::max<int64_t>(m, 1) * (size_t)B;
+    if (hipMalloc((void **)&b->d_xout, sizeof(double) * (xo_len + yo_len) + sizeof(impc_info) * (size_t)B) != hipSuccess)
         return fail(IMPC_MEM_ALLOC_ERROR, "hipMalloc(results) failed");
+    b->d_yout = b->d_xout + xo_len;
+    b->d_info = (impc_info *)(b->d_yout + yo_len);
     IMPC_TRY(fill0_sync(ctx->stream, b->d_info, sizeof(impc_info) * (size_t)B));
     b->device_bytes = (int64_t)(in_bytes + sizeof(double) * (n + m) * B + sizeof(impc_info) * B);
     int rc = prepare_structured(b.get());
@@ -1349,10 +1413,9 @@ int impc_batch_destroy(impc_batch b) {
     }
     for (hipEvent_t e : b->ev)
         if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {b->ev_in, b->ev_ws})
-        if (e) (void)hipEventDestroy(e);
+    if (b->ev_in) (void)hipEventDestroy(b->ev_in);
     if (b->h_stage) (void)hipHostFree(b->h_stage);
-    void *ptrs[] = {b->d_in,     b->d_xout,  b->d_yout,  b->d_info,  b->d_tables, b->d_scal, b->d_counter,
+    void *ptrs[] = {b->d_in,     b->d_xout,  b->d_tables, b->d_scal, b->d_counter,
                     b->d_sym,    b->d_work,  b->d_sec,   b->d_shPx,  b->d_shAx,   b->d_Axv,  b->d_vmap,
                     b->d_qpt,    b->d_persist, b->d_tlim, b->d_csr, b->d_qscr};
     for (void *p : ptrs)
@@ -1446,7 +1509,7 @@ int impc_batch_set_values(impc_batch b, const double *Px, const double *q, const
         // are contiguous in that order), one DMA queued after every launch that may still read
         // the inputs -- no host synchronisation
         IMPC_TRY(stage_ensure(b));
-        if (b->in_pending) HIP_OK(hipEventSynchronize(b->ev_in));
+        IMPC_TRY(stage_wait(b));
         double *s = b->h_stage;
         const size_t len[5] = {(size_t)b->nnzP * B, (size_t)b->n * B, (size_t)b->nnzA * B, (size_t)b->m * B,
                                (size_t)b->m * B};
@@ -1455,11 +1518,7 @@ int impc_batch_set_values(impc_batch b, const double *Px, const double *q, const
             if (len[k]) std::memcpy(s, src[k], sizeof(double) * len[k]);
             s += len[k];
         }
-        hipStream_t st = b->ctx->stream;
-        IMPC_TRY(ctx_order_after_all(b->ctx, st));
-        HIP_OK(hipMemcpyAsync(b->in_Px, b->h_stage, sizeof(double) * stage_in_len(b), hipMemcpyHostToDevice, st));
-        HIP_OK(hipEventRecord(b->ev_in, st));
-        b->in_pending = true;
+        b->in_dirty = true;  // uploaded with the warm start by the next call that needs them (flush_staged)
         b->shared = false;
         b->persist_valid = b->q_by_update = false;
         b->values_set = true;
@@ -1504,6 +1563,7 @@ int impc_batch_set_values_shared(impc_batch b, const double *Px, const double *A
     HIP_OK(hipSetDevice(b->ctx->device));
     hipStream_t st = b->ctx->stream;
     IMPC_TRY(ctx_quiesce(b->ctx));  // no solve in flight on any stream reads the arrays replaced below
+    b->in_dirty = false;            // staged inputs of impc_batch_set_values are superseded
     if (!b->d_shPx) {
         HIP_OK(hipMalloc((void **)&b->d_shPx, sizeof(double) * std::max<int64_t>(b->nnzP, 1)));
         HIP_OK(hipMalloc((void **)&b->d_shAx, sizeof(double) * std::max<int64_t>(b->nnzA, 1)));
@@ -1541,6 +1601,7 @@ int impc_batch_set_values_device(impc_batch b, const double *Px, const double *q
         return fail(IMPC_INVALID_ARGUMENT, "null value array");
     HIP_OK(hipSetDevice(b->ctx->device));
     IMPC_TRY(ctx_quiesce(b->ctx));  // the copies below are ordered on the context stream only
+    b->in_dirty = false;            // staged inputs of impc_batch_set_values are superseded
     hipStream_t st = b->ctx->stream;
     const size_t B = (size_t)b->B;
     if (b->nnzP) HIP_OK(hipMemcpyAsync(b->in_Px, Px, sizeof(double) * b->nnzP * B, hipMemcpyDeviceToDevice, st));
@@ -1568,16 +1629,12 @@ int impc_batch_warm_start(impc_batch b, const double *x, const double *y) {
     const size_t B = (size_t)b->B;
     if (stage_ok(b)) {  // x (and y) through the pinned staging, stream-ordered, one DMA
         IMPC_TRY(stage_ensure(b));
-        if (b->ws_pending) HIP_OK(hipEventSynchronize(b->ev_ws));
+        IMPC_TRY(stage_wait(b));
         double *s = stage_xws(b);
         std::memcpy(s, x, sizeof(double) * b->n * B);
-        const size_t len = (size_t)b->n * B + (b->m && y ? (size_t)b->m * B : 0);
-        if (b->m && y) std::memcpy(s + (size_t)b->n * B, y, sizeof(double) * b->m * B);
-        hipStream_t st = b->ctx->stream;
-        IMPC_TRY(ctx_order_after_all(b->ctx, st));
-        HIP_OK(hipMemcpyAsync(b->in_xws, s, sizeof(double) * len, hipMemcpyHostToDevice, st));  // in_yws follows in_xws
-        HIP_OK(hipEventRecord(b->ev_ws, st));
-        b->ws_pending = true;
+        if (b->m && y) std::memcpy(s + (size_t)b->n * B, y, sizeof(double) * b->m * B);  // in_yws follows in_xws
+        b->ws_len = (size_t)b->n * B + (b->m && y ? (size_t)b->m * B : 0);
+        b->ws_dirty = true;  // uploaded by the next call that needs it (flush_staged)
     } else {
         IMPC_TRY(ctx_quiesce(b->ctx));  // no solve in flight on any stream reads the arrays replaced below
         IMPC_TRY(h2d_sync(b->ctx->stream, b->in_xws, x, sizeof(double) * b->n * B));
@@ -1591,6 +1648,7 @@ int impc_batch_warm_start(impc_batch b, const double *x, const double *y) {
     b->dst.warm_start = 1;
     if (!use_structured(b) && b->generic_setup_done && !b->generic_dirty) {
         // a set-up generic workspace takes the warm start in place, keeping scaling, rho and factor
+        IMPC_TRY(flush_staged(b));
         hipStream_t st = b->ctx->stream;
         int rc = interleave(b, b->in_xws, const_cast<double *>(b->dwk.xws), b->n, st);
         if (!rc && !b->ws_y && b->m) rc = fill0_sync(st, b->in_yws, sizeof(double) * b->m * b->B);
@@ -1617,6 +1675,10 @@ int impc_batch_set_values_async(impc_batch b, const double *Ax_var, const double
     auto h2d = [&](double *dst, const double *src, size_t len) -> hipError_t {
         return len ? hipMemcpyAsync(dst, src, sizeof(double) * len, hipMemcpyHostToDevice, st) : hipSuccess;
     };
+    // staged uploads these copies supersede are dropped (a DMA of them on the context stream would
+    // not be ordered with this stream's copies)
+    b->in_dirty = false;
+    if (x_ws) b->ws_dirty = false;
     HIP_OK(h2d(b->d_Axv, Ax_var, (size_t)b->nvar * B));
     HIP_OK(h2d(b->in_q, q, (size_t)b->n * B));
     HIP_OK(h2d(b->in_l, l, (size_t)b->m * B));
@@ -1651,6 +1713,7 @@ int impc_batch_warm_start_device(impc_batch b, const double *x, const double *y)
     // queued after every launch on every stream this context has used: none of them still reads
     // the warm-start arrays when the copies land
     IMPC_TRY(ctx_order_after_all(b->ctx, st));
+    b->ws_dirty = false;  // a staged host warm start is superseded
     const size_t B = (size_t)b->B;
     HIP_OK(hipMemcpyAsync(b->in_xws, x, sizeof(double) * b->n * B, hipMemcpyDeviceToDevice, st));
     if (b->m && y) HIP_OK(hipMemcpyAsync(b->in_yws, y, sizeof(double) * b->m * B, hipMemcpyDeviceToDevice, st));
@@ -1688,6 +1751,7 @@ int impc_batch_setup(impc_batch b, void *stream) {
     if (!b->values_set) return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "values not set");
     HIP_OK(hipSetDevice(b->ctx->device));
     if (use_structured(b)) return IMPC_OK;  // the wave kernel runs setup and solve per QP in one launch
+    IMPC_TRY(flush_staged(b));
     hipStream_t st = pick(b, stream);
     IMPC_TRY(ctx_order_launch(b->ctx, st));
     IMPC_TRY(generic_setup(b, st));
@@ -1698,6 +1762,7 @@ int impc_batch_solve(impc_batch b, void *stream) {
     if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
     if (!b->values_set) return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "values not set");
     HIP_OK(hipSetDevice(b->ctx->device));
+    IMPC_TRY(flush_staged(b));
     hipStream_t st = pick(b, stream);
     IMPC_TRY(ctx_order_launch(b->ctx, st));
     IMPC_TRY(use_structured(b) ? structured_solve(b, st) : generic_solve(b, st));
@@ -1716,6 +1781,7 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
         if (!use_structured(b) || b->vs != b0->vs)
             return fail(IMPC_UNSUPPORTED, "grouped solves need structured batches of one team shape");
     }
+    for (int k = 0; k < count; k++) IMPC_TRY(flush_staged(bs[k]));
     // One persistent launch per kernel class (general-row slots per lane, GS): a bucket never runs
     // in a wider instance than it needs (more registers, spills) and each launch's LDS is sized by
     // its own batches, so mixed obstacle counts (config 4, K = 0..21) keep the narrow kernel at two
@@ -1802,18 +1868,10 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
         }
         const uint32_t *ord = nullptr;
         IMPC_TRY(queue_order(lb.data(), lf.data(), L.count, L.total, st, &ord));
-        int rc;
-        switch (b0->vs * 8 + L.gs + (L.tier ? 64 : 0)) {
-            case 64 + kWaveVS * 8 + 2: rc = launch_group<kWaveVS, 2, true>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord); break;
-            case 64 + kWaveVS * 8 + 3: rc = launch_group<kWaveVS, 3, true>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord); break;
-            case kWaveVS * 8 + 2: rc = launch_group<kWaveVS, 2>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord); break;
-            case kWaveVS * 8 + 3: rc = launch_group<kWaveVS, 3>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord); break;
-            case kWaveVS * 8 + 4: rc = launch_group<kWaveVS, 4>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord); break;
-            case kWaveVSLong * 8 + 2: rc = launch_group<kWaveVSLong, 2>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord); break;
-            case kWaveVSLong * 8 + 3: rc = launch_group<kWaveVSLong, 3>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord); break;
-            case kWaveVSLong * 8 + 4: rc = launch_group<kWaveVSLong, 4>(ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord); break;
-            default: return fail(IMPC_UNSUPPORTED, "no structured kernel for this size");
-        }
+        const int rc = with_shape(b0->vs, L.gs, L.tier, [&](auto vs, auto gs, auto tr) {
+            return launch_group<decltype(vs)::value, decltype(gs)::value, decltype(tr)::value>(
+                ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord);
+        });
         if (rc) return rc;
     }
     IMPC_TRY(ctx_note_launch(ctx, st));
@@ -1836,9 +1894,14 @@ int impc_batch_get(impc_batch b, double *x, double *y, impc_info *info) {
         double *sx = stage_xout(b), *sy = sx + (size_t)b->B * b->n;
         impc_info *si = (impc_info *)(sy + (size_t)b->B * b->m);
         const size_t B = (size_t)b->B;
-        if (x) HIP_OK(hipMemcpyAsync(sx, b->d_xout, sizeof(double) * b->n * B, hipMemcpyDeviceToHost, st));
-        if (y && b->m) HIP_OK(hipMemcpyAsync(sy, b->d_yout, sizeof(double) * b->m * B, hipMemcpyDeviceToHost, st));
-        if (info) HIP_OK(hipMemcpyAsync(si, b->d_info, sizeof(impc_info) * B, hipMemcpyDeviceToHost, st));
+        if (x && y && info && b->m) {  // the device regions [x][y][info] are contiguous as in the staging
+            HIP_OK(hipMemcpyAsync(sx, b->d_xout, sizeof(double) * (b->n + b->m) * B + sizeof(impc_info) * B,
+                                  hipMemcpyDeviceToHost, st));
+        } else {
+            if (x) HIP_OK(hipMemcpyAsync(sx, b->d_xout, sizeof(double) * b->n * B, hipMemcpyDeviceToHost, st));
+            if (y && b->m) HIP_OK(hipMemcpyAsync(sy, b->d_yout, sizeof(double) * b->m * B, hipMemcpyDeviceToHost, st));
+            if (info) HIP_OK(hipMemcpyAsync(si, b->d_info, sizeof(impc_info) * B, hipMemcpyDeviceToHost, st));
+        }
         IMPC_TRY(ctx_quiesce(b->ctx));
         if (x) std::memcpy(x, sx, sizeof(double) * b->n * B);
         if (y && b->m) std::memcpy(y, sy, sizeof(double) * b->m * B);
@@ -1871,6 +1934,7 @@ static int upload_interleaved(impc_batch b, const double *host, double *qp_major
 
 int impc_batch_update_lin_cost(impc_batch b, const double *q) {
     if (!b || !q) return fail(IMPC_INVALID_ARGUMENT, "null batch or q");
+    IMPC_TRY(flush_staged(b));  // the staged values go first, the update overwrites q after them
     if (use_structured(b)) {  // the next structured solve resumes the workspace with this q
         if (!b->persist_on || !b->persist_valid)
             return fail(IMPC_WORKSPACE_NOT_INIT_ERROR,
@@ -1896,6 +1960,7 @@ int impc_batch_update_lin_cost(impc_batch b, const double *q) {
 
 int impc_batch_update_bounds(impc_batch b, const double *l, const double *u) {
     if (!b || (b->m && (!l || !u))) return fail(IMPC_INVALID_ARGUMENT, "null batch or bounds");
+    IMPC_TRY(flush_staged(b));
     if (use_structured(b)) {  // the next structured solve resumes the workspace with these bounds
         if (!b->persist_on || !b->persist_valid)
             return fail(IMPC_WORKSPACE_NOT_INIT_ERROR,
@@ -1929,6 +1994,7 @@ int impc_batch_update_bounds(impc_batch b, const double *l, const double *u) {
 int impc_batch_update_lin_cost_device(impc_batch b, const double *q) {
     if (!b || !q) return fail(IMPC_INVALID_ARGUMENT, "null batch or q");
     HIP_OK(hipSetDevice(b->ctx->device));
+    IMPC_TRY(flush_staged(b));
     hipStream_t st = b->ctx->stream;
     const size_t bytes = sizeof(double) * (size_t)(b->n * b->B);
     if (use_structured(b)) {
@@ -1954,6 +2020,7 @@ int impc_batch_update_lin_cost_device(impc_batch b, const double *q) {
 int impc_batch_update_bounds_device(impc_batch b, const double *l, const double *u) {
     if (!b || (b->m && (!l || !u))) return fail(IMPC_INVALID_ARGUMENT, "null batch or bounds");
     HIP_OK(hipSetDevice(b->ctx->device));
+    IMPC_TRY(flush_staged(b));
     hipStream_t st = b->ctx->stream;
     const size_t bytes = sizeof(double) * (size_t)(b->m * b->B);
     if (use_structured(b)) {

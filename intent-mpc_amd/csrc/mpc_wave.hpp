@@ -157,7 +157,7 @@ struct WaveLds {
     static constexpr int WMAX = (NMAX + 5) / 13 - 1;       // max control stages
     // stage count whose recursions are fully unrolled (the reference's default horizon N = 20
     // for the one-variable-per-lane shape, N = 40 for the long-horizon shape)
-    static constexpr int WSPEC = VS == 1 ? 19 : 39;
+    static constexpr int WSPEC = NMAX <= 256 ? 19 : 39;
     // exchange vector length: zero tail past NMAX, and room for the factorisation scratch
     // (the sweeps' two-steps-ahead prefetches read at most 13 (W + 4) + 8 past the start), and
     // room for the factorisation's dense stage scratch (FA .. DIAGX below)
@@ -661,14 +661,16 @@ struct WaveQP {
             // (exactly symmetric).
             {
                 double *src = A, *dst = Li;
-                const int gi = L / 13, gc = L % 13;
-                const bool act = L < 169 && gi < sz && gc < sz;
                 // two pivots per step (2x2 block pivot Q = P^-1, P = S[J][J], J = {j, j+1}):
                 //   D[J][J] = Q, D[J][c] = Q S[J][c], D[i][J] = -S[i][J] Q,
                 //   D[i][c] = S[i][c] - (S[i][J] Q) S[J][c]; a non-PD pivot block flags failure
                 for (int j = 0; j < sz; j += 2) {
                     const bool two = j + 1 < sz, last = j + (two ? 2 : 1) >= sz;
-                    if (act) {
+                    // element (gi, gc) of the 13 x 13 block per lane (a team of fewer than 169 lanes
+                    // takes several)
+                    for (int el = L; el < 169; el += NL) {
+                        const int gi = el / 13, gc = el % 13;
+                        if (gi >= sz || gc >= sz) continue;
                         const int i = last && gc > gi ? gc : gi, c = last && gc > gi ? gi : gc;
                         double v;
                         if (two) {

@@ -10,6 +10,7 @@ from oracle import osqp_oracle as ora
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HARNESS_PATH = os.path.join(ROOT, "tests", "native", "build", "libimpc_core_cpu.so")
 EMU_PATH = os.path.join(ROOT, "tests", "native", "build", "libwave_emu.so")
+EMU64_PATH = os.path.join(ROOT, "tests", "native", "build", "libwave_emu64.so")  # one QP per wavefront
 
 # BASELINE.json north_star: primal within 1e-5 relative of the reference solver.
 PRIMAL_RTOL = 1e-5
@@ -75,9 +76,9 @@ def harness(cfg, settings):
 _E = {}
 
 
-def emulate(cfg, settings):
-    """Test-only CPU emulation of the structured wave kernel (mpc_wave.hpp, 256 lanes as threads)."""
-    path = EMU_PATH
+def emulate(cfg, settings, path=EMU_PATH):
+    """Test-only CPU emulation of the structured wave kernel (mpc_wave.hpp, 256 lanes as threads;
+    path=EMU64_PATH: the 64-lane team shape)."""
     if path not in _E:
         _E[path] = C.CDLL(path)
         _E[path].emu_wave_solve_batch.restype = C.c_int

@@ -4,7 +4,9 @@
 // running its NL lanes as NL threads that meet at a barrier wherever the GPU wave synchronises
 // (LDS exchange, readlane broadcast, wave reductions).  This lets the structured solver be
 // checked against the oracle in the GPU-less container.  Never linked into libimpc_qp.so.
+#include <algorithm>
 #include <barrier>
+#include <utility>
 #include <cstring>
 #include <thread>
 #include <limits>
@@ -15,15 +17,23 @@
 
 namespace {
 
-constexpr int NL = 256;  // the product team shape (impc_qp.hip IMPC_TEAM / IMPC_VS)
+// the team shape (impc_qp.hip IMPC_TEAM): 256 lanes (the product: one variable per lane, or three
+// for the long horizon), or 64 (EMU_NL=64: one QP per wavefront, four variables per lane)
+#ifndef EMU_NL
+#define EMU_NL 256
+#endif
+constexpr int NL = EMU_NL;
+static_assert(NL == 256 || NL == 64, "emulated team shapes");
 
 struct EmuShared {
     std::barrier<> bar{NL};
-    std::barrier<> wbar[NL / 64] = {std::barrier<>{64}, std::barrier<>{64}, std::barrier<>{64}, std::barrier<>{64}};
+    std::barrier<> wbar[NL / 64];
     double scratch[2][NL];
     double wscratch[2][NL];  // wave-level exchanges (bcast / shfl / 8-lane sums), per-wave regions
+    EmuShared() : EmuShared(std::make_index_sequence<NL / 64>{}) {}
+    template <size_t... I>
+    EmuShared(std::index_sequence<I...>) : wbar{((void)I, std::barrier<>{64})...} {}
 };
-static_assert(NL == 256, "wbar initialiser assumes 4 wavefronts");
 
 struct EmuWave {
     int l;
@@ -133,6 +143,34 @@ void run(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSetti
         tier ? run_w<VS, GS, 0, true>(T, io, st) : run_w<VS, GS, 0, false>(T, io, st);
 }
 
+// the product's shapes for the team size (impc_qp.hip kWaveVS / kWaveVSLong / kGsMax)
+template <int N>
+int dispatch(const impc::MpcStructure &ms, const impc::WaveTables &T, const impc::WaveIO &io,
+             const impc::DevSettings &st) {
+    if constexpr (N == 64) {  // one QP per wavefront: four variable slots, up to six general-row slots
+        if (ms.n > 4 * N || ms.mg > 6 * N) return 2;
+        const int gs = std::max(2, (ms.mg + N - 1) / N);
+        if (gs == 2) run<4, 2>(T, io, st);
+        else if (gs == 3) run<4, 3>(T, io, st);
+        else if (gs == 4) run<4, 4>(T, io, st);
+        else if (gs == 5) run<4, 5>(T, io, st);
+        else run<4, 6>(T, io, st);
+    } else {
+        if (ms.n > 3 * N || ms.mg > 4 * N) return 2;
+        const int gs = ms.mg <= 2 * N ? 2 : ms.mg <= 3 * N ? 3 : 4;
+        if (ms.n <= N) {
+            if (gs == 2) run<1, 2>(T, io, st);
+            else if (gs == 3) run<1, 3>(T, io, st);
+            else run<1, 4>(T, io, st);
+        } else {
+            if (gs == 2) run<3, 2>(T, io, st);
+            else if (gs == 3) run<3, 3>(T, io, st);
+            else run<3, 4>(T, io, st);
+        }
+    }
+    return 0;
+}
+
 }  // namespace
 
 extern "C" int emu_wave_solve_batch(int64_t n, int64_t m, const int64_t *Pp, const int64_t *Pi, const int64_t *Ap,
@@ -148,6 +186,7 @@ extern "C" int emu_wave_solve_batch(int64_t n, int64_t m, const int64_t *Pp, con
     // the emulation takes the two-tier products layout whenever the pattern has heavy columns (the
     // product uses it where one tier would cost occupancy), so both gathers are covered on the CPU
     if (ms.HS == 0) T.T1r = impc::WaveLds<NL, 1, 2>::cg4(ms.CG);
+    // per-QP scratch of the scaling vectors (shapes without them in LDS)
     std::vector<double> zx((size_t)B * n, 0.0), zy((size_t)B * m, 0.0), scal((size_t)B * (2 * n + ms.mg), 0.0);
     impc::WaveIO io{B, Px, q, Ax, l, u, xws ? xws : zx.data(), yws ? yws : zy.data(), xws ? 1 : 0,
                     xo, yo, scal.data(), info};
@@ -169,16 +208,6 @@ extern "C" int emu_wave_solve_batch(int64_t n, int64_t m, const int64_t *Pp, con
     st.scaled_termination = (int32_t)s->scaled_termination;
     st.check_termination = (int32_t)s->check_termination;
     st.warm_start = (int32_t)s->warm_start;
-    if (ms.n > 3 * NL || ms.CG > impc::WaveLds<NL, 1, 2>::CGM || ms.mg > 4 * NL) return 2;
-    const int gs = ms.mg <= 2 * NL ? 2 : ms.mg <= 3 * NL ? 3 : 4;
-    if (ms.n <= NL) {  // the product's shapes (impc_qp.hip kWaveVS / kWaveVSLong)
-        if (gs == 2) run<1, 2>(T, io, st);
-        else if (gs == 3) run<1, 3>(T, io, st);
-        else run<1, 4>(T, io, st);
-    } else {
-        if (gs == 2) run<3, 2>(T, io, st);
-        else if (gs == 3) run<3, 3>(T, io, st);
-        else run<3, 4>(T, io, st);
-    }
-    return 0;
+    if (ms.CG > impc::WaveLds<NL, 1, 2>::CGM) return 2;
+    return dispatch<NL>(ms, T, io, st);
 }

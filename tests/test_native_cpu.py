@@ -14,7 +14,7 @@ import pytest
 import impc
 from impc import scenarios
 
-from helpers import compare, emulate, harness, oracle, take
+from helpers import EMU64_PATH, compare, emulate, harness, oracle, take
 
 S25 = dict(verbose=0, adaptive_rho_interval=25)
 
@@ -98,3 +98,20 @@ def test_structured_emulation_default_horizon_batch(rho):
         compare(res, ref)
         if rho < 0.1:
             assert ref[2]["rho_updates"].max() >= 1
+
+
+@pytest.mark.parametrize("name", ["config3_K8", "config3_K9", "config2"])
+def test_structured_emulation_wavefront_team(name):
+    """The one-QP-per-wavefront team shape (64 lanes, four variable slots and up to six
+    general-row slots per lane, D / E and the check deltas off LDS) against the oracle: the same
+    kernel body at NL = 64 (mpc_wave.hpp, Gauss-Jordan with several elements per lane)."""
+    s = impc.default_settings(**S25)
+    cfg = take(CFG[name], 2)
+    compare(emulate(cfg, s, EMU64_PATH), oracle(cfg, s))
+
+
+@pytest.mark.parametrize("N", [3, 19])
+def test_structured_emulation_wavefront_team_horizons(N):
+    cfg = scenarios.static_config(N=N, K=4, batch=1, identical=False, seed=1900 + N)
+    s = impc.default_settings(**S25)
+    compare(emulate(cfg, s, EMU64_PATH), oracle(cfg, s))
