@@ -257,6 +257,9 @@ typedef struct {
     int64_t device_bytes;
     int64_t kernel;          /* IMPC_KERNEL_GENERIC or IMPC_KERNEL_STRUCTURED for the next solve */
     int64_t structured_ok;   /* 1 if the pattern qualifies for the structured kernel */
+    /* structured team shape (0 when structured_ok is 0): lanes per QP (64: one QP per wavefront,
+     * 256: one QP per 4-wavefront workgroup), variable and general-row slots per lane */
+    int64_t team_lanes, var_slots, row_slots;
 } impc_batch_stats;
 int impc_batch_get_stats(impc_batch b, impc_batch_stats *out);
 

@@ -61,31 +61,26 @@ int fail(int code, const std::string &msg) {
 
 constexpr int kBlock = 64;  // generic path: one wavefront per workgroup, one QP per lane
 constexpr int kTile = 64;   // transpose tile edge
-// structured path team shape (compile-time; see DESIGN.md for the measured choice)
-#ifndef IMPC_TEAM
-#define IMPC_TEAM 256
+// Structured path team shapes, keyed by the variable slots per lane VS:
+//   VS = 1  team shape: one QP per 256-lane workgroup (one variable per lane), two teams per CU
+//           (n <= 256: the reference's default horizon N = 20)
+//   VS = 3  long shape: 256 lanes, three variables per lane, one team per CU (n <= 768)
+//   VS = 4  wavefront shape (built only with IMPC_WAVEFRONT=1: measured slower):
+//           one QP per 64-lane wavefront (four variables and up to six general rows per lane, D / E
+//           and the check deltas off LDS), one wavefront per SIMD, four QPs per CU
+#ifndef IMPC_WAVEFRONT
+#define IMPC_WAVEFRONT 0
 #endif
-#ifndef IMPC_VS
-#define IMPC_VS 1
-#endif
-#ifndef IMPC_WAVES_PER_SIMD
-#define IMPC_WAVES_PER_SIMD 2
-#endif
-// general-row slots per lane of the instantiated kernels (mg <= kTeam * GS), and of the two-tier
-// products instances
-#ifndef IMPC_GS_MAX
-#define IMPC_GS_MAX 4
-#endif
-#ifndef IMPC_TIER_GS_MAX
-#define IMPC_TIER_GS_MAX 3
-#endif
-constexpr int kTeam = IMPC_TEAM;   // lanes per QP (IMPC_TEAM / 64 wavefronts)
-constexpr int kWaveVS = IMPC_VS;   // variable slots per lane (n <= kTeam * kWaveVS)
-constexpr int kGsMax = IMPC_GS_MAX, kTierGsMax = IMPC_TIER_GS_MAX;
-static_assert(kGsMax >= 2 && kGsMax <= 8 && kTierGsMax >= 2 && kTierGsMax <= kGsMax, "general-row slot range");
-// long-horizon shape (e.g. N = 40, n = 515): three variable slots per lane, one wave per SIMD
-// (the per-QP LDS then allows one team per CU anyway)
-constexpr int kWaveVSLong = 3;
+constexpr int kWaveVS = 1, kWaveVSLong = 3, kWaveVSFront = 4;
+template <int VS>
+struct Shape {
+    static constexpr int NL = VS == kWaveVSFront ? 64 : 256;  // lanes per QP
+    static constexpr int WPS = VS == kWaveVS ? 2 : 1;         // waves per SIMD (launch bound: registers)
+    static constexpr int GMAX = VS == kWaveVSFront ? 6 : 4;   // general-row slots per lane
+    // the two-tier products instances (mpc_wave.hpp WaveLds): general-row slot counts that have them
+    static constexpr int TIER_GMAX = VS == kWaveVSFront ? 6 : VS == kWaveVS ? 3 : 1;
+    static constexpr int PER_CU = 4 * WPS / (NL / 64);        // resident QPs per CU by waves
+};
 
 // ------------------------------------------------------------------ layout transposes
 // dst[e * S + b] = src[b * len + e]; 64x64 tile through LDS so both sides are coalesced.
@@ -227,9 +222,19 @@ template <int NL>
 struct GpuTeam {
     double *red;  // >= NL/64 doubles of LDS
     __device__ int lane() const { return (int)threadIdx.x; }
-    __device__ void sync() { __syncthreads(); }
+    // A one-wavefront team (NL = 64) needs no workgroup barrier: a wavefront's LDS operations
+    // execute in issue order, so a read issued after a write sees it; only code motion across the
+    // exchange point is ruled out (wavefront-scope fence, no wait for outstanding LDS operations)
+    __device__ static void wave_sync() {
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    __device__ void sync() {
+        if constexpr (NL == 64) wave_sync();
+        else __syncthreads();
+    }
     // barrier of the ADMM iteration's LDS exchanges (an LDS-only wait was measured slower)
-    __device__ void lsync() { __syncthreads(); }
+    __device__ void lsync() { sync(); }
     __device__ double bcast(double v, int src) {
         int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
         int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
@@ -420,26 +425,6 @@ struct GpuTeam {
         return r;
     }
 };
-
-template <int NL, int VS, int GS, int WPS, int WF>
-__global__ __launch_bounds__(NL, WPS) void k_mpc_wave(impc::WaveTables T, impc::WaveIO io, impc::DevSettings st,
-                                                      unsigned *counter, const uint32_t *__restrict__ ord) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    using LD = impc::WaveLds<NL, VS, GS>;
-    GpuTeam<NL> wv{smem + LD::RED_OFF};
-    __shared__ unsigned next;
-    impc::WaveQP<GpuTeam<NL>, NL, VS, GS, WF>::load_tables(wv, T, smem);
-    for (;;) {
-        if (threadIdx.x == 0) next = atomicAdd(counter, 1u);
-        __syncthreads();
-        const unsigned pos = next;
-        __syncthreads();
-        if ((int64_t)pos >= io.B) break;
-        const unsigned b = ord ? ord[pos] : pos;  // queue order (impc_batch_set_queue_order)
-        impc::WaveQP<GpuTeam<NL>, NL, VS, GS, WF> qp(wv, T, io, st, smem);
-        qp.solve((int64_t)b);
-    }
-}
 
 // One batch of a grouped launch (impc_batch_solve_group): its tables, I/O, settings and the
 // index of its first QP in the group's work queue.
@@ -720,6 +705,9 @@ impc::WaveIO wave_io(impc_batch b) {
                     b->in_l,     b->in_u,   b->in_xws, b->in_yws, b->has_ws ? (b->ws_y ? 1 : 2) : 0, b->d_xout, b->d_yout,
                     b->d_scal,   b->d_info};
     if (b->profile && b->d_qpt) io.qpt = b->d_qpt;
+#ifdef IMPC_SECTION_PROF
+    io.sec = b->d_sec;
+#endif
     if (b->tlim_on) io.tlim = b->d_tlim;
     if (b->persist_on && b->d_persist) {
         io.persist = b->d_persist;
@@ -904,34 +892,14 @@ int ensure_lds_attr(K kernel, size_t lds) {
 // resident workgroups per CU: the waves-per-SIMD budget of the shape, and LDS
 template <int VS>
 int64_t resident_groups(int num_cu, size_t lds, int64_t work) {
-    constexpr int WPS = VS == kWaveVS ? IMPC_WAVES_PER_SIMD : 1;
-    const int by_waves = std::max(1, (4 * WPS) / (kTeam / 64));
-    const int per_cu = std::max<int>(1, std::min<int>(by_waves, (int)((160 * 1024 - 1024) / lds)));
+    const int per_cu = std::max<int>(1, std::min<int>(Shape<VS>::PER_CU, (int)((160 * 1024 - 1024) / lds)));
     return std::min<int64_t>(work, (int64_t)num_cu * per_cu);
 }
 
-// ---- structured path
-template <int VS, int GS, int WF>
-int launch_wave_w(impc_batch b, hipStream_t st, const impc::WaveIO &io, const uint32_t *ord) {
-    constexpr int WPS = VS == kWaveVS ? IMPC_WAVES_PER_SIMD : 1;
-    using LD = impc::WaveLds<kTeam, VS, GS>;
-    const size_t lds = sizeof(double) * (size_t)LD::size(b->wt);  // products sized by the pattern
-    if (int rc = ensure_lds_attr(k_mpc_wave<kTeam, VS, GS, WPS, WF>, lds)) return rc;
-    const int64_t groups = resident_groups<VS>(b->ctx->num_cu, lds, b->Bact);
-    hipLaunchKernelGGL((k_mpc_wave<kTeam, VS, GS, WPS, WF>), dim3((unsigned)groups), dim3(kTeam), lds, st, b->wt, io,
-                       b->dst, b->d_counter, ord);
-    HIP_OK(hipGetLastError());
-    return IMPC_OK;
-}
 // the default-horizon instance (compile-time W) takes the batch when its W is the shape's WSPEC
 bool spec_ok(impc_batch b) {
-    const int ws = b->vs == kWaveVS ? impc::WaveLds<kTeam, kWaveVS, 2>::WSPEC : impc::WaveLds<kTeam, kWaveVSLong, 2>::WSPEC;
+    const int ws = b->vs == kWaveVSLong ? impc::WaveLds<256, kWaveVSLong, 2>::WSPEC : impc::WaveLds<256, kWaveVS, 2>::WSPEC;
     return b->ms->W == ws;
-}
-template <int VS, int GS>
-int launch_wave(impc_batch b, hipStream_t st, const impc::WaveIO &io, const uint32_t *ord) {
-    constexpr int WS = impc::WaveLds<kTeam, VS, GS>::WSPEC;
-    return spec_ok(b) ? launch_wave_w<VS, GS, WS>(b, st, io, ord) : launch_wave_w<VS, GS, 0>(b, st, io, ord);
 }
 
 // ---- work-queue order (impc_batch_set_queue_order, csrc/queue.hpp)
@@ -1016,23 +984,28 @@ int shape_call(F &&f) {
 }
 template <int V, bool TR, class F>
 int with_gs(int gs, F &&f) {
-    constexpr int gmax = TR ? kTierGsMax : (V == kWaveVS ? kGsMax : 4);
+    constexpr int gmax = TR ? Shape<V>::TIER_GMAX : Shape<V>::GMAX;
     switch (gs) {
-        case 2: return shape_call<V, 2, TR>(f);
-        case 3: return shape_call<V, 3, TR>(f);
+        case 2: if constexpr (gmax >= 2) return shape_call<V, 2, TR>(f); break;
+        case 3: if constexpr (gmax >= 3) return shape_call<V, 3, TR>(f); break;
         case 4: if constexpr (gmax >= 4) return shape_call<V, 4, TR>(f); break;
         case 5: if constexpr (gmax >= 5) return shape_call<V, 5, TR>(f); break;
         case 6: if constexpr (gmax >= 6) return shape_call<V, 6, TR>(f); break;
-        case 7: if constexpr (gmax >= 7) return shape_call<V, 7, TR>(f); break;
-        case 8: if constexpr (gmax >= 8) return shape_call<V, 8, TR>(f); break;
         default: break;
     }
     return fail(IMPC_UNSUPPORTED, "no structured kernel for this size");
 }
 template <class F>
 int with_shape(int vs, int gs, bool tier, F &&f) {
-    if (vs == kWaveVS) return tier ? with_gs<kWaveVS, true>(gs, f) : with_gs<kWaveVS, false>(gs, f);
-    if (vs == kWaveVSLong && !tier) return with_gs<kWaveVSLong, false>(gs, f);
+    switch (vs) {
+        case kWaveVSFront:
+            if constexpr (IMPC_WAVEFRONT != 0)
+                return tier ? with_gs<kWaveVSFront, true>(gs, f) : with_gs<kWaveVSFront, false>(gs, f);
+            break;
+        case kWaveVS: return tier ? with_gs<kWaveVS, true>(gs, f) : with_gs<kWaveVS, false>(gs, f);
+        case kWaveVSLong: return tier ? with_gs<kWaveVSLong, true>(gs, f) : with_gs<kWaveVSLong, false>(gs, f);
+        default: break;
+    }
     return fail(IMPC_UNSUPPORTED, "no structured kernel for this size");
 }
 
@@ -1044,43 +1017,26 @@ void structured_solved(impc_batch b) {
     b->has_ws = false;
 }
 
+// One batch's structured solve: a grouped launch of one entry (the entry table is cached, so
+// repeated solves of a batch upload nothing)
 int structured_solve(impc_batch b, hipStream_t st) {
-    if (b->tier) return impc_batch_solve_group(&b, 1, st);  // the two-tier instances are grouped ones
-    impc::WaveIO io = wave_io(b);
-    HIP_OK(hipMemsetAsync(b->d_counter, 0, 256, st));
 #ifdef IMPC_SECTION_PROF
     if (!b->d_sec) {
         HIP_OK(hipMalloc((void **)&b->d_sec, sizeof(unsigned long long) * impc::kSecCount));
         HIP_OK(hipMemsetAsync(b->d_sec, 0, sizeof(unsigned long long) * impc::kSecCount, st));
     }
-    io.sec = b->d_sec;
 #endif
-    if (b->profile) HIP_OK(hipEventRecord(b->ev[2], st));
-    const uint32_t *ord = nullptr;
-    const int64_t first0 = 0;
-    IMPC_TRY(queue_order(&b, &first0, 1, b->Bact, st, &ord));
-    const int rc = with_shape(b->vs, b->gs, false, [&](auto vs, auto gs, auto) {
-        return launch_wave<decltype(vs)::value, decltype(gs)::value>(b, st, io, ord);
-    });
-    if (rc) return rc;
-    structured_solved(b);
-    if (b->profile) {
-        HIP_OK(hipEventRecord(b->ev[3], st));
-        HIP_OK(hipEventRecord(b->ev[4], st));
-        b->ev_solve = true;
-        b->ev_setup = false;
-    }
-    return IMPC_OK;
+    return impc_batch_solve_group(&b, 1, st);
 }
 
 template <int VS, int GS, int WF, bool TIER>
 int launch_group_w(impc_ctx ctx, hipStream_t st, const GroupEntry *entries, int count, int64_t total, size_t lds,
                    unsigned *counter, const uint32_t *ord) {
-    constexpr int WPS = VS == kWaveVS ? IMPC_WAVES_PER_SIMD : 1;
-    if (int rc = ensure_lds_attr(k_mpc_wave_group<kTeam, VS, GS, WPS, WF, TIER>, lds)) return rc;
+    using S = Shape<VS>;
+    if (int rc = ensure_lds_attr(k_mpc_wave_group<S::NL, VS, GS, S::WPS, WF, TIER>, lds)) return rc;
     const int64_t groups = resident_groups<VS>(ctx->num_cu, lds, total);
-    hipLaunchKernelGGL((k_mpc_wave_group<kTeam, VS, GS, WPS, WF, TIER>), dim3((unsigned)groups), dim3(kTeam), lds, st,
-                       entries, count, total, counter, ord);
+    hipLaunchKernelGGL((k_mpc_wave_group<S::NL, VS, GS, S::WPS, WF, TIER>), dim3((unsigned)groups), dim3(S::NL), lds,
+                       st, entries, count, total, counter, ord);
     HIP_OK(hipGetLastError());
     return IMPC_OK;
 }
@@ -1088,34 +1044,34 @@ int launch_group_w(impc_ctx ctx, hipStream_t st, const GroupEntry *entries, int 
 template <int VS, int GS, bool TIER = false>
 int launch_group(impc_ctx ctx, hipStream_t st, const GroupEntry *entries, int count, int64_t total, size_t lds,
                  unsigned *counter, bool spec, const uint32_t *ord) {
-    constexpr int WS = impc::WaveLds<kTeam, VS, GS>::WSPEC;
+    constexpr int WS = impc::WaveLds<Shape<VS>::NL, VS, GS>::WSPEC;
     return spec ? launch_group_w<VS, GS, WS, TIER>(ctx, st, entries, count, total, lds, counter, ord)
                 : launch_group_w<VS, GS, 0, TIER>(ctx, st, entries, count, total, lds, counter, ord);
 }
 
-// dynamic LDS bytes of the structured kernel for a shape (team VS, GS) and pattern (CG, n)
+// dynamic LDS bytes of the structured kernel for a shape (team VS, GS) and pattern (CG, n); 0 if
+// the shape has no kernel for GS
 size_t wave_lds_bytes(int vs, int gs, const impc::WaveTables &T) {
     size_t bytes = 0;
     (void)with_shape(vs, gs, false, [&](auto v, auto g, auto) {
-        bytes = sizeof(double) * (size_t)impc::WaveLds<kTeam, decltype(v)::value, decltype(g)::value>::size(T);
+        constexpr int V = decltype(v)::value;
+        bytes = sizeof(double) * (size_t)impc::WaveLds<Shape<V>::NL, V, decltype(g)::value>::size(T);
         return IMPC_OK;
     });
     return bytes;
 }
 
-int prepare_structured(impc_batch b) {
-    b->ms.reset(new impc::MpcStructure());
-    std::string why = b->ms->analyse(b->n, b->m, b->Pp.data(), b->Pi.data(), b->Ap.data(), b->Ai.data());
-    if (!why.empty() || b->ms->n > kTeam * kWaveVSLong || b->ms->CG > impc::WaveLds<kTeam, kWaveVS, 2>::CGM) {
-        b->structured_ok = false;
-        return IMPC_OK;
-    }
-    b->vs = b->ms->n <= kTeam * kWaveVS ? kWaveVS : kWaveVSLong;
-    const int mg = b->ms->mg;
-    {
-        const int g = std::max(2, (mg + kTeam - 1) / kTeam);  // general-row slots per lane
-        b->gs = g <= (b->vs == kWaveVS ? kGsMax : 4) ? g : 0;
-    }
+// A library built with the wavefront shape uses it unless IMPC_WAVEFRONT_SHAPE=0 is in the
+// environment when the batch is created (A/B in one process).
+bool wavefront_shape_on() {
+    const char *e = std::getenv("IMPC_WAVEFRONT_SHAPE");
+    return IMPC_WAVEFRONT != 0 && !(e && e[0] == '0');
+}
+
+// Shape selection: (when built) the wavefront shape if the pattern fits it with four QPs per CU,
+// else the team shape (n <= 256), else the long shape.  Sets b->vs, b->gs, b->tier and the tables' layout
+// fields; false if no structured shape takes the pattern.
+bool choose_shape(impc_batch b) {
     const impc::MpcStructure &s = *b->ms;
     impc::WaveTables &t = b->wt;
     t.n = s.n;
@@ -1126,24 +1082,43 @@ int prepare_structured(impc_batch b) {
     t.CG = s.CG;
     t.nnzP = s.nnzP;
     t.nnzA = s.nnzA;
-    // products layout (mpc_wave.hpp WaveLds): one tier unless it would cost the shape a resident
-    // team per CU, then the heavy columns' overflow in a second tier
-    t.HS = 0;
-    t.T1r = impc::WaveLds<kTeam, kWaveVS, 2>::cg4(s.CG);
-    // (two-tier instances: the one-variable-per-lane shape with 2 or 3 general-row slots)
-    if (b->gs && b->vs == kWaveVS && b->gs <= kTierGsMax) {
-        const int per_cu = std::max(1, (4 * IMPC_WAVES_PER_SIMD) / (kTeam / 64));
+    auto fit = [&](int vs, int nl, int gmax, int tier_gmax, int per_cu, bool need_full) -> bool {
+        if (s.n > nl * vs) return false;
+        const int g = std::max(2, (s.mg + nl - 1) / nl);  // general-row slots per lane
+        if (g > gmax) return false;
         const size_t budget = (160 * 1024 - 1024) / (size_t)per_cu;
-        if (wave_lds_bytes(b->vs, b->gs, t) > budget) {
+        // products layout (mpc_wave.hpp WaveLds): one tier unless it would cost the shape a resident
+        // team per CU, then the heavy columns' overflow in a second tier
+        t.HS = 0;
+        t.T1r = impc::WaveLds<256, kWaveVS, 2>::cg4(s.CG);
+        if (g <= tier_gmax && wave_lds_bytes(vs, g, t) > budget) {
             t.HS = s.HS;
             t.T1r = impc::kProdTier1;
         }
-    }
-    b->tier = t.T1r < impc::WaveLds<kTeam, kWaveVS, 2>::cg4(s.CG);
-    if (!b->gs || wave_lds_bytes(b->vs, b->gs, t) > 160 * 1024 - 1024) {
+        const size_t lds = wave_lds_bytes(vs, g, t);
+        if (!lds || lds > (need_full ? budget : (size_t)(160 * 1024 - 1024))) return false;
+        b->vs = vs;
+        b->gs = g;
+        b->tier = t.T1r < impc::WaveLds<256, kWaveVS, 2>::cg4(s.CG);
+        return true;
+    };
+    using F = Shape<kWaveVSFront>;
+    using T1 = Shape<kWaveVS>;
+    using L = Shape<kWaveVSLong>;
+    if (wavefront_shape_on() && fit(kWaveVSFront, F::NL, F::GMAX, F::TIER_GMAX, F::PER_CU, true)) return true;
+    if (fit(kWaveVS, T1::NL, T1::GMAX, T1::TIER_GMAX, T1::PER_CU, false)) return true;
+    return fit(kWaveVSLong, L::NL, L::GMAX, L::TIER_GMAX, L::PER_CU, false);
+}
+
+int prepare_structured(impc_batch b) {
+    b->ms.reset(new impc::MpcStructure());
+    std::string why = b->ms->analyse(b->n, b->m, b->Pp.data(), b->Pi.data(), b->Ap.data(), b->Ai.data());
+    if (!why.empty() || b->ms->CG > impc::WaveLds<256, kWaveVS, 2>::CGM || !choose_shape(b)) {
         b->structured_ok = false;  // the generic kernel takes it
         return IMPC_OK;
     }
+    const impc::MpcStructure &s = *b->ms;
+    impc::WaveTables &t = b->wt;
     std::vector<const std::vector<int32_t> *> arrs = {&s.var_orig, &s.var_pdiag, &s.var_boxrow, &s.var_boxpos,
                                                       &s.gen_row,  &s.gen_col,   &s.gen_pos,    &s.colg,
                                                       &s.term_ptr, &s.term,      &s.col_hid};
@@ -1163,9 +1138,9 @@ int prepare_structured(impc_batch b) {
                                   &t.gen_col,  &t.gen_pos,   &t.colg,       &t.term_ptr,   &t.term,
                                   &t.col_hid};
     for (size_t k = 0; k < arrs.size(); k++) *dst_ptrs[k] = base + offs[k];
-    // per-QP HBM scratch for the scaling vectors: long-horizon shape only (the default shape keeps
+    // per-QP HBM scratch for the scaling vectors: the wavefront and long shapes (the team shape keeps
     // them in LDS, mpc_wave.hpp WaveLds::ONCHIP)
-    const bool onchip = b->vs == kWaveVS && impc::WaveLds<kTeam, kWaveVS, 2>::ONCHIP;
+    const bool onchip = b->vs == kWaveVS && impc::WaveLds<256, kWaveVS, 2>::ONCHIP;
     const size_t scal_bytes = onchip ? 0 : sizeof(double) * (size_t)b->B * (size_t)(2 * s.n + s.mg);
     if (scal_bytes) HIP_OK(hipMalloc((void **)&b->d_scal, scal_bytes));
     HIP_OK(hipMalloc((void **)&b->d_counter, 256));
@@ -1778,21 +1753,21 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
         impc_batch b = bs[k];
         if (!b || b->ctx != ctx) return fail(IMPC_INVALID_ARGUMENT, "group batches must share a context");
         if (!b->values_set) return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "values not set");
-        if (!use_structured(b) || b->vs != b0->vs)
-            return fail(IMPC_UNSUPPORTED, "grouped solves need structured batches of one team shape");
+        if (!use_structured(b)) return fail(IMPC_UNSUPPORTED, "grouped solves need structured batches");
     }
     for (int k = 0; k < count; k++) IMPC_TRY(flush_staged(bs[k]));
-    // One persistent launch per kernel class (general-row slots per lane, GS): a bucket never runs
-    // in a wider instance than it needs (more registers, spills) and each launch's LDS is sized by
-    // its own batches, so mixed obstacle counts (config 4, K = 0..21) keep the narrow kernel at two
-    // QPs per CU for most buckets.  Classes run back to back on the stream, entries contiguous.
+    // One persistent launch per kernel class (team shape VS, general-row slots per lane GS, products
+    // tiers): a bucket never runs in a wider instance than it needs (more registers, spills) and each
+    // launch's LDS is sized by its own batches, so mixed obstacle counts (config 4, K = 0..21) keep
+    // the narrow kernels for most buckets.  Classes run back to back on the stream, entries contiguous.
     std::vector<int> order((size_t)count);
     for (int k = 0; k < count; k++) order[(size_t)k] = k;
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+        if (bs[x]->vs != bs[y]->vs) return bs[x]->vs > bs[y]->vs;  // wavefront shape first
         return bs[x]->gs != bs[y]->gs ? bs[x]->gs < bs[y]->gs : (int)bs[x]->tier < (int)bs[y]->tier;
     });
     struct Launch {
-        int gs;
+        int vs, gs;
         bool tier;
         int first, count;
         int64_t total;
@@ -1807,8 +1782,9 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
     std::memset((void *)entries.data(), 0, sizeof(GroupEntry) * (size_t)count);  // comparable bytes
     for (int p = 0; p < count; p++) {
         impc_batch b = bs[order[(size_t)p]];
-        if (launches.empty() || launches.back().gs != b->gs || launches.back().tier != b->tier)
-            launches.push_back(Launch{b->gs, b->tier, p, 0, 0, 0, true, b->d_counter});
+        if (launches.empty() || launches.back().vs != b->vs || launches.back().gs != b->gs ||
+            launches.back().tier != b->tier)
+            launches.push_back(Launch{b->vs, b->gs, b->tier, p, 0, 0, 0, true, b->d_counter});
         Launch &L = launches.back();
         L.count++;
         L.lds = std::max(L.lds, wave_lds_bytes(b->vs, b->gs, b->wt));
@@ -1868,7 +1844,7 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
         }
         const uint32_t *ord = nullptr;
         IMPC_TRY(queue_order(lb.data(), lf.data(), L.count, L.total, st, &ord));
-        const int rc = with_shape(b0->vs, L.gs, L.tier, [&](auto vs, auto gs, auto tr) {
+        const int rc = with_shape(L.vs, L.gs, L.tier, [&](auto vs, auto gs, auto tr) {
             return launch_group<decltype(vs)::value, decltype(gs)::value, decltype(tr)::value>(
                 ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord);
         });
@@ -2068,6 +2044,11 @@ int impc_batch_get_stats(impc_batch b, impc_batch_stats *out) {
     out->device_bytes = b->device_bytes;
     out->kernel = use_structured(b) ? IMPC_KERNEL_STRUCTURED : IMPC_KERNEL_GENERIC;
     out->structured_ok = b->structured_ok ? 1 : 0;
+    if (b->structured_ok) {
+        out->team_lanes = b->vs == kWaveVSFront ? Shape<kWaveVSFront>::NL : Shape<kWaveVS>::NL;
+        out->var_slots = b->vs;
+        out->row_slots = b->gs;
+    }
     return IMPC_OK;
 }
 

@@ -59,7 +59,7 @@ INFO_DTYPE = np.dtype([("iter", np.int64), ("status_val", np.int64), ("rho_updat
 class Stats(C.Structure):
     _fields_ = [(k, C.c_int64) for k in ("n", "m", "nnzP", "nnzA", "batch", "batch_stride", "nnzL", "nnzLcol",
                                          "n_terms", "bandwidth", "device_bytes", "kernel",
-                                         "structured_ok")]
+                                         "structured_ok", "team_lanes", "var_slots", "row_slots")]
 
 
 class MpcParams(C.Structure):

@@ -43,7 +43,7 @@ def test_struct_layouts_match_headers():
     # impc_settings: 22 8-byte fields (OSQPSettings mirror); impc_info: 8 fields
     assert C.sizeof(impc.Settings) == 22 * 8
     assert C.sizeof(impc.Info) == 8 * 8 and impc.INFO_DTYPE.itemsize == 64
-    assert C.sizeof(impc.Stats) == 13 * 8
+    assert C.sizeof(impc.Stats) == 16 * 8  # 13 facts + the structured team shape (lanes, var / row slots)
 
 
 def test_default_settings_are_osqp_defaults():
