@@ -64,15 +64,6 @@ namespace impc {
 // history / store captures, (c, S)-carried sweeps, off-chip scaling vectors, Cholesky / 1x1-pivot
 // stage inverses.  What is left is the measured-best form of each phase.
 
-// Round-4 experiment (off until measured): the S1 phase folded into the forward sweep.  The
-// recursion a_{k+1} = t_{k+1} - F_k a_k with t_{k+1} = r_{k+1}[:8] - G_k[:, 8:] r_k[8:] is
-// a_{k+1} = r_{k+1}[:8] - (G_k[:, :8] a_k + G_k[:, 8:] r_k[8:]): the lanes of the sweep's 8x8 grid
-// whose reduction index is < 5 add G_k[out][8 + in] r_k[8 + in] to their product (an FMA, the term
-// formed off the chain), so the S1 phase and its barrier go away.  One-variable-per-lane shape.
-#ifndef IMPC_S1FOLD
-#define IMPC_S1FOLD 0
-#endif
-
 // Scheduling hint for the parallel phases' LDS reads: under the kernel's register pressure the
 // machine scheduler otherwise issues them one ds_read2 at a time, each followed by its own
 // lgkmcnt wait (S3 = 7 serialised LDS round trips); this asks for the phase's reads first, then
@@ -177,10 +168,7 @@ struct WaveLds {
     static constexpr int VEC_N = 2 * NMAX + NL * GS;
     static constexpr int SCL_OFF = GSLOT_OFF + NL * GS;           // D, E (scaling)
     static constexpr int DLT_OFF = SCL_OFF + (ONCHIP ? VEC_N : 0);  // dx, dy (check iterations)
-    // S1 folded into the forward sweep (IMPC_S1FOLD): G_k[:, 8:] per stage in the sweep's lane layout
-    static constexpr bool S1F = VS == 1 && IMPC_S1FOLD;
-    static constexpr int GX_OFF = DLT_OFF + (ONCHIP ? VEC_N : 0);   // [WMAX][64]
-    static constexpr int P_OFF = GX_OFF + (S1F ? WMAX * 64 : 0);    // products, column-slot layout (size below)
+    static constexpr int P_OFF = DLT_OFF + (ONCHIP ? VEC_N : 0);  // products, column-slot layout (size below)
     static constexpr int CGM = 24;                          // max general entries per column
     // products region: entry t < T1r of column v at t * stride(n) + v (stride = n rounded up to
     // 64, plus a pad), so a column's gather is independent, conflict-free reads.  When that one
@@ -239,15 +227,6 @@ IMPC_WF int row_type(double l, double u) {  // set_rho_vec (auxil.h:34)
     if ((l < -kInf * kMinScaling) && (u > kInf * kMinScaling)) return -1;
     if (u - l < kRhoTol) return 1;
     return 0;
-}
-
-// a * b rounded on its own (never contracted into a following add), so the symmetric
-// cross-lane sums that consume it give bitwise-identical results in every lane of a group
-IMPC_WF double prod_nc(double a, double b) {
-    // contract(off) drops the multiply's contraction flag, so it never fuses into the add that
-    // consumes it (an empty volatile asm would do the same but also pin the instruction order)
-#pragma clang fp contract(off)
-    return a * b;
 }
 
 // WF: the stage count W fixed at compile time (LD::WSPEC, the default horizon: every stage loop
@@ -735,9 +714,6 @@ struct WaveQP {
                     // recursion layout: lane (i,j) of step k reads F_k[j][i] when the column index
                     // sits on i (k even), F_k[i][j] otherwise
                     Fm[64 * k + 8 * i + j] = !(k & 1) ? G[13 * j + i] : G[13 * i + j];
-                    if constexpr (LD::S1F)  // G_k[out][8 + in], in = the reduction index (< 5, else 0)
-                        lds[LD::GX_OFF + 64 * k + 8 * i + j] =
-                            !(k & 1) ? (i < 5 ? G[13 * j + 8 + i] : 0.0) : (j < 5 ? G[13 * i + 8 + j] : 0.0);
                 }
                 _Pragma("unroll") for (int s = 0; s < VS; s++) {
                     if (!vok[s]) continue;
@@ -760,12 +736,14 @@ struct WaveQP {
         return bad;
     }
 
-    // One step of a stage recursion on the 8x8 lane grid: returns c - R(F v), R the strided
-    // (STRIDE) or contiguous 8-lane sum.
+    // One step of a stage recursion on the 8x8 lane grid: returns c - F v as R(c / 8 - f v), R the
+    // strided (STRIDE) or contiguous 8-lane sum.  The sweeps' inputs c come pre-scaled by 1/8
+    // (exact: S1 stores t / 8, S3 the state part of e / 8), so the subtraction rides in the
+    // product's FMA: one instruction and one dependent operation less per step on the serial chain.
     template <bool STRIDE>
-    IMPC_WF double rstep(double f, double c, double v) {
-        const double p = prod_nc(f, v);
-        return c - (STRIDE ? wv.sum_stride8(p) : wv.sum_contig8(p));
+    IMPC_WF double rstep(double f, double c8, double v) {
+        const double p = __builtin_fma(-f, v, c8);
+        return STRIDE ? wv.sum_stride8(p) : wv.sum_contig8(p);
     }
 
     // Sweeps with a compile-time step count WC (= WSPEC) are fully unrolled: every LDS wait is
@@ -814,7 +792,7 @@ struct WaveQP {
     IMPC_WF void fwd_sweep(const double *tb, double *rb, int W) {
         const double *Fm = lds + LD::F_OFF;
         const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;  // opaque: see lane_o
-        double a = tb[i];
+        double a = 8.0 * tb[i];  // a_0 = t_0 (tb holds t / 8)
         // (F, t) of the next even / odd step, loaded two steps ahead (reads past the last stage
         // stay inside the LDS buffers and are never used)
         double fe = Fm[l], te = tb[13 + j], fo = Fm[64 + l], to = tb[26 + i];
@@ -856,67 +834,6 @@ struct WaveQP {
         }
     }
 
-    // S2 body with S1 folded in (IMPC_S1FOLD): a_0 = r_0[:8]; a_{k+1} = r_{k+1}[:8] -
-    // R(F_k a_k + Gx_k r_k[8:]), Gx_k the zero-padded G_k[:, 8:] block of the lane layout; in place in
-    // rb (each stage's [:8] overwritten by a only after its last read).  WC as fwd_sweep.
-    template <bool STRIDE>
-    IMPC_WF double rstep_w(double f, double c, double v, double w) {
-        const double p = __builtin_fma(f, v, w);
-        return c - (STRIDE ? wv.sum_stride8(p) : wv.sum_contig8(p));
-    }
-    template <int WC>
-    IMPC_WF void fwd_sweep_fold(double *rb, int W) {
-        const double *Fm = lds + LD::F_OFF, *Gx = lds + LD::GX_OFF;
-        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;
-        double a = rb[i];
-        // (F, Gx, r_{k+1}[out], r_k[8 + in]) of the next even / odd step, loaded two steps ahead
-        double fe = Fm[l], ge = Gx[l], ce = rb[13 + j], re = rb[8 + i];
-        double fo = Fm[64 + l], go = Gx[64 + l], co = rb[26 + i], ro = rb[13 + 8 + j];
-        if constexpr (WC > 0) {
-            double c0[CQ], c1[CQ];
-            _Pragma("unroll") for (int q = 0; q < CQ; q++) c0[q] = c1[q] = 0.0;
-            _Pragma("unroll") for (int k = 0; k < WC; k += 2) {
-                const double f0 = fe, g0 = ge, t0 = ce, r0 = re;
-                fe = Fm[64 * (k + 2) + l];
-                ge = Gx[64 * (k + 2) + l];
-                ce = rb[13 * (k + 3) + j];
-                re = rb[13 * (k + 2) + 8 + i];
-                a = rstep_w<true>(f0, t0, a, prod_nc(g0, r0));
-                capm<true>(c0, a, k, i);
-                if (k + 1 < WC) {
-                    const double f1 = fo, g1 = go, t1 = co, r1 = ro;
-                    fo = Fm[64 * (k + 3) + l];
-                    go = Gx[64 * (k + 3) + l];
-                    co = rb[13 * (k + 4) + i];
-                    ro = rb[13 * (k + 3) + 8 + j];
-                    a = rstep_w<false>(f1, t1, a, prod_nc(g1, r1));
-                    capm<false>(c1, a, k + 1, j);
-                }
-            }
-            cap_store<true>(c0, c1, rb, WC, true, i, j);
-        } else {
-            double *junk = lds + LD::JUNK_OFF + lo;
-            const bool wri = j == 0, wrj = i == 0;
-            for (int k = 0; k < W; k += 2) {
-                const double f0 = fe, g0 = ge, t0 = ce, r0 = re;
-                fe = Fm[64 * (k + 2) + l];
-                ge = Gx[64 * (k + 2) + l];
-                ce = rb[13 * (k + 3) + j];
-                re = rb[13 * (k + 2) + 8 + i];
-                a = rstep_w<true>(f0, t0, a, prod_nc(g0, r0));
-                *(wrj ? rb + 13 * (k + 1) + j : junk) = a;
-                if (k + 1 >= W) break;
-                const double f1 = fo, g1 = go, t1 = co, r1 = ro;
-                fo = Fm[64 * (k + 3) + l];
-                go = Gx[64 * (k + 3) + l];
-                co = rb[13 * (k + 4) + i];
-                ro = rb[13 * (k + 3) + 8 + j];
-                a = rstep_w<false>(f1, t1, a, prod_nc(g1, r1));
-                *(wri ? rb + 13 * (k + 2) + i : junk) = a;
-            }
-        }
-    }
-
     // S4 body for a first step k = W-1 of parity ODD: steps alternate strided (odd k) and
     // contiguous (even k) reductions; x_k sits at index j (odd k) / i (even k).  WC as above.
     template <bool ODD, int WC>
@@ -924,8 +841,8 @@ struct WaveQP {
         const double *Fm = lds + LD::F_OFF;
         const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;
         if constexpr (WC > 0) W = WC;
-        // x_W: W = (W-1)+1 has the opposite parity of the first step
-        double x = eb[13 * W + (ODD ? i : j)];
+        // x_W = e_W: W = (W-1)+1 has the opposite parity of the first step (eb holds e[:8] / 8)
+        double x = 8.0 * eb[13 * W + (ODD ? i : j)];
         const int k1 = W - 2 > 0 ? W - 2 : 0;
         double fa = Fm[64 * (W - 1) + l], ea = eb[13 * (W - 1) + (ODD ? j : i)];
         double fb = Fm[64 * k1 + l], ebv = eb[13 * k1 + (ODD ? i : j)];
@@ -999,7 +916,7 @@ struct WaveQP {
             wv.lsync();
         }
         IMPC_SEC(kSecRhs);
-        if (!LD::S1F) IMPC_REP(kSecS1) {
+        IMPC_REP(kSecS1) {
             // S1: t_k = r_k[:8] - G_{k-1}[:, 8:] r_{k-1}[8:]  (every lane, without branches: a
             // stage-0 or empty slot has zero coupling coefficients, a control lane's t lands in a
             // slot nothing reads)
@@ -1013,7 +930,7 @@ struct WaveQP {
                 _Pragma("unroll") for (int cc = 0; cc < 5; cc++) rv[cc] = rp[cc];
                 IMPC_LOADS_FIRST(5, 12);
                 _Pragma("unroll") for (int cc = 0; cc < 5; cc++) t -= cp[s][cc] * rv[cc];
-                tb[v] = t;
+                tb[v] = 0.125 * t;  // the forward sweep's input, pre-scaled (rstep)
             }
             wv.lsync();
         }
@@ -1026,21 +943,12 @@ struct WaveQP {
             // DPP), all in the VALU, with no transpose.  The next F and t are loaded two steps ahead.
             // One wavefront of the team (rw) runs it -- the others go straight to the barrier and
             // leave their SIMD's issue slots to the co-resident team.
-            if constexpr (LD::S1F) {
-                if ((L >> 6) == rw) {
-                    if (W == LD::WSPEC)
-                        fwd_sweep_fold<LD::WSPEC>(rb, W);
-                    else
-                        fwd_sweep_fold<0>(rb, W);
-                }
-            } else {
-                if (L < 8) rb[L] = tb[L];
-                if ((L >> 6) == rw) {
-                    if (W == LD::WSPEC)
-                        fwd_sweep<LD::WSPEC>(tb, rb, W);
-                    else
-                        fwd_sweep<0>(tb, rb, W);
-                }
+            if (L < 8) rb[L] = 8.0 * tb[L];
+            if ((L >> 6) == rw) {
+                if (W == LD::WSPEC)
+                    fwd_sweep<LD::WSPEC>(tb, rb, W);
+                else
+                    fwd_sweep<0>(tb, rb, W);
             }
             wv.lsync();
         }
@@ -1054,7 +962,8 @@ struct WaveQP {
                 IMPC_LOADS_FIRST(7, 20);
                 double e = 0.0;
                 _Pragma("unroll") for (int cc = 0; cc < 13; cc++) e += ainv[s][cc] * rv[cc];
-                eb[NL * s + L] = e;
+                // the state part pre-scaled for the backward sweep (rstep); S5 reads the controls' e
+                eb[NL * s + L] = vr_[s] < 8 ? 0.125 * e : e;
             }
             wv.lsync();
         }
@@ -1062,7 +971,7 @@ struct WaveQP {
         IMPC_REP(kSecBwd) {
             // S4: backward 8-dim recursion x_k[:8] = e_k[:8] - F_k' x_{k+1}[:8] on the same grid and
             // stored layout: even steps reduce over j (contiguous), odd steps over i (strided).
-            if (L < 8) xb[13 * W + L] = eb[13 * W + L];
+            if (L < 8) xb[13 * W + L] = 8.0 * eb[13 * W + L];
             if ((L >> 6) == rw) {
                 if (W == LD::WSPEC)
                     bwd_sweep<((LD::WSPEC - 1) & 1) != 0, LD::WSPEC>(eb, xb, W);
