@@ -310,81 +310,77 @@ struct GpuTeam {
     // round across wavefronts
     __device__ double max(double v) {
         double mv[1] = {v};
-        max_n(mv);
+        reduce<1, 0>(mv, nullptr);
         return mv[0];
     }
-    // K team maxima at once: DPP / permlane exchanges inside each wavefront (max is
-    // order-independent, so any pairing that covers the wave will do), one LDS round across
-    // wavefronts instead of K (a termination check reduces 14 norms)
+    // K team maxima at once (one LDS round across wavefronts)
     template <int K>
     __device__ void max_n(double (&v)[K]) {
-        static_assert(K * (NL / 64) <= 64, "team reduction scratch (WaveLds RED_OFF) holds 64 doubles");
-        auto mx = [](double a, double b) { return b > a ? b : a; };
-        _Pragma("unroll") for (int k = 0; k < K; k++) {
-            double t = v[k];
-            t = mx(t, dpp<0xB1>(t));   // quad_perm [1,0,3,2]
-            t = mx(t, dpp<0x4E>(t));   // quad_perm [2,3,0,1]
-            t = mx(t, dpp<0x141>(t));  // row_half_mirror
-            t = mx(t, dpp<0x128>(t));  // row_ror:8
-            const int lo = __double2loint(t), hi = __double2hiint(t);
-            auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-            auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-            t = mx(__hiloint2double(rh[0], rl[0]), __hiloint2double(rh[1], rl[1]));
-            const int lo2 = __double2loint(t), hi2 = __double2hiint(t);
-            auto ql = __builtin_amdgcn_permlane32_swap(lo2, lo2, false, false);
-            auto qh = __builtin_amdgcn_permlane32_swap(hi2, hi2, false, false);
-            v[k] = mx(__hiloint2double(qh[0], ql[0]), __hiloint2double(qh[1], ql[1]));
-            // one value at a time: interleaving all K exchange chains would need ~2K extra VGPRs
-            // at a point where the whole per-QP state is live (measured: spills)
-            asm volatile("" : "+v"(v[k]));
-        }
-        if (NL == 64) return;
-        if ((threadIdx.x & 63) == 0)
-            _Pragma("unroll") for (int k = 0; k < K; k++) red[(threadIdx.x >> 6) * K + k] = v[k];
-        __syncthreads();
-        _Pragma("unroll") for (int k = 0; k < K; k++) {
-            double r = red[k];
-            for (int w = 1; w < NL / 64; w++) r = red[w * K + k] > r ? red[w * K + k] : r;
-            v[k] = r;
-        }
-        __syncthreads();
+        reduce<K, 0>(v, nullptr);
     }
-    // KM maxima and KS sums at once, each bitwise the value max() / sum() gives, over one LDS round
-    // (the infeasibility tests' first stages: one team exchange instead of four)
     template <int KM, int KS>
     __device__ void max_sum_n(double (&mx)[KM], double (&sm)[KS]) {
-        static_assert((KM + KS) * (NL / 64) <= 64, "team reduction scratch (WaveLds RED_OFF) holds 64 doubles");
-        auto mxf = [](double a, double b) { return b > a ? b : a; };
-        _Pragma("unroll") for (int k = 0; k < KM; k++) {
-            double t = mx[k];
-            t = mxf(t, dpp<0xB1>(t));
-            t = mxf(t, dpp<0x4E>(t));
-            t = mxf(t, dpp<0x141>(t));
-            t = mxf(t, dpp<0x128>(t));
-            const int lo = __double2loint(t), hi = __double2hiint(t);
-            auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-            auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-            t = mxf(__hiloint2double(rh[0], rl[0]), __hiloint2double(rh[1], rl[1]));
-            const int lo2 = __double2loint(t), hi2 = __double2hiint(t);
-            auto ql = __builtin_amdgcn_permlane32_swap(lo2, lo2, false, false);
-            auto qh = __builtin_amdgcn_permlane32_swap(hi2, hi2, false, false);
-            mx[k] = mxf(__hiloint2double(qh[0], ql[0]), __hiloint2double(qh[1], ql[1]));
+        reduce<KM, KS>(mx, sm);
+    }
+    // the 64-bit permlane swaps (V_PERMLANE32_SWAP / V_PERMLANE16_SWAP on both halves): lanes of the
+    // lower 32 (even 16-lane row) end with x from their partner l + 32 (l + 16) in y, the upper
+    // (odd) ones with y from their partner in x -- so max(x, y) is, in every lane, the pair's
+    // maximum of x (lower / even lanes) or of y (upper / odd lanes)
+    template <bool P32>
+    __device__ static void swap64(double &x, double &y) {
+        const int xl = __double2loint(x), xh = __double2hiint(x), yl = __double2loint(y), yh = __double2hiint(y);
+        auto rl = P32 ? __builtin_amdgcn_permlane32_swap(xl, yl, false, false)
+                      : __builtin_amdgcn_permlane16_swap(xl, yl, false, false);
+        auto rh = P32 ? __builtin_amdgcn_permlane32_swap(xh, yh, false, false)
+                      : __builtin_amdgcn_permlane16_swap(xh, yh, false, false);
+        x = __hiloint2double(rh[0], rl[0]);
+        y = __hiloint2double(rh[1], rl[1]);
+    }
+    // KM team maxima and KS team sums at once, each bitwise the value max() / sum() gives, over one
+    // LDS round.  Maxima: reduce-scatter inside the wavefront -- the permlane32 swap pairs value k
+    // with value k + K1 (lower 32 lanes keep the first K1 values, upper 32 the rest), the permlane16
+    // swap halves each half again per 16-lane row, then DPP butterflies inside the rows over the K2
+    // values left: every lane of row r ends with values (r >> 1) K1 + (r & 1) K2 + k (max is exact,
+    // so the order does not matter; 3 instructions per value and level instead of 30 per value
+    // for a full butterfly of each).  Sums: the xor butterfly of wave_sum, wavefronts added in order.
+    template <int KM, int KS>
+    __device__ void reduce(double (&mx)[KM], double *sm) {
+        constexpr int K1 = (KM + 1) / 2, K2 = (K1 + 1) / 2, KT = KM + KS;
+        static_assert(KT * (NL / 64) <= impc::kRedLen, "team reduction scratch (WaveLds RED_OFF)");
+        auto vmax = [](double a, double b) { return b > a ? b : a; };
+        double h[K1], q[K2];
+        _Pragma("unroll") for (int k = 0; k < K1; k++) {
+            double x = mx[k], y = k + K1 < KM ? mx[k + K1] : mx[k];
+            swap64<true>(x, y);
+            h[k] = vmax(x, y);
+        }
+        _Pragma("unroll") for (int k = 0; k < K2; k++) {
+            double x = h[k], y = k + K2 < K1 ? h[k + K2] : h[k];
+            swap64<false>(x, y);
+            double t = vmax(x, y);
+            t = vmax(t, dpp<0xB1>(t));   // quad_perm [1,0,3,2]
+            t = vmax(t, dpp<0x4E>(t));   // quad_perm [2,3,0,1]
+            t = vmax(t, dpp<0x141>(t));  // row_half_mirror
+            q[k] = vmax(t, dpp<0x128>(t));  // row_ror:8
         }
         _Pragma("unroll") for (int k = 0; k < KS; k++) sm[k] = wave_sum(sm[k]);
-        if (NL == 64) return;
-        if ((threadIdx.x & 63) == 0) {
-            _Pragma("unroll") for (int k = 0; k < KM; k++) red[(threadIdx.x >> 6) * (KM + KS) + k] = mx[k];
-            _Pragma("unroll") for (int k = 0; k < KS; k++) red[(threadIdx.x >> 6) * (KM + KS) + KM + k] = sm[k];
+        const int w = (int)threadIdx.x >> 6, row = ((int)threadIdx.x >> 4) & 3;
+        if ((threadIdx.x & 15) == 0) {
+            _Pragma("unroll") for (int k = 0; k < K2; k++) {
+                const int sub = (row & 1) * K2 + k, idx = (row >> 1) * K1 + sub;
+                if (sub < K1 && idx < KM) red[w * KT + idx] = q[k];
+            }
         }
+        if ((threadIdx.x & 63) == 0) _Pragma("unroll") for (int k = 0; k < KS; k++) red[w * KT + KM + k] = sm[k];
         __syncthreads();
         _Pragma("unroll") for (int k = 0; k < KM; k++) {
             double r = red[k];
-            for (int w = 1; w < NL / 64; w++) r = red[w * (KM + KS) + k] > r ? red[w * (KM + KS) + k] : r;
+            for (int u = 1; u < NL / 64; u++) r = vmax(r, red[u * KT + k]);
             mx[k] = r;
         }
         _Pragma("unroll") for (int k = 0; k < KS; k++) {
             double r = red[KM + k];
-            for (int w = 1; w < NL / 64; w++) r = r + red[w * (KM + KS) + KM + k];
+            for (int u = 1; u < NL / 64; u++) r = r + red[u * KT + KM + k];
             sm[k] = r;
         }
         __syncthreads();

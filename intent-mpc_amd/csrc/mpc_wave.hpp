@@ -141,6 +141,9 @@ enum {
 #define IMPC_SEC_START() ((void)0)
 #endif
 
+// team reduction scratch (WaveLds RED_OFF): values x wavefronts of one team reduction
+constexpr int kRedLen = 128;
+
 // LDS doubles per wave for (VS, GS)
 template <int NL, int VS, int GS>
 struct WaveLds {
@@ -158,8 +161,8 @@ struct WaveLds {
     static constexpr int T_OFF = R_OFF + NP;                // tbuf
     static constexpr int E_OFF = T_OFF + NP;                // ebuf
     static constexpr int X_OFF = E_OFF + NP;                // xbuf
-    static constexpr int RED_OFF = X_OFF + NP;              // team reduction scratch
-    static constexpr int JUNK_OFF = RED_OFF + 64;           // per-lane discard slots [NL]
+    static constexpr int RED_OFF = X_OFF + NP;              // team reduction scratch [kRedLen]
+    static constexpr int JUNK_OFF = RED_OFF + kRedLen;      // per-lane discard slots [NL]
     static constexpr int GSLOT_OFF = JUNK_OFF + NL;         // int16 [4 NL GS]: general entry -> product slot
     // One-variable-per-lane shape: the Ruiz scaling vectors D, E and the ADMM deltas of the
     // termination checks live here (the long-horizon shape keeps them in HBM / registers: its LDS
@@ -1052,6 +1055,9 @@ struct WaveQP {
     // ------------------------------------------------------------ update_info + checks
     struct Info {
         double pri_res, dua_res, pri_norm_u, dua_norm_u, pri_norm_s, dua_norm_s, pri_plain, dua_plain;
+        // the infeasibility tests' first stages (is_primal_infeasible: ||E P(dy)||, u'P(dy)_+ +
+        // l'P(dy)_-; is_dual_infeasible: ||D dx||, q'dx), reduced with the norms above
+        double pinf_nrm, pinf_lhs, dinf_nrm, dinf_qdx;
     };
 
     IMPC_WF void load_scal(int64_t b, double D[VS], double Eb[VS], double Eg[GS]) {
@@ -1115,10 +1121,20 @@ struct WaveQP {
             px_u = dmax(px_u, fabs(di * px));
         }
         {
-            double r[14] = {pr_u, z_u, ax_u, pr_p, z_p, ax_p, dr_u, q_u, aty_u, px_u, dr_p, q_p, aty_p, px_p};
-            wv.max_n(r);  // one team reduction for all 14 norms
+            // the infeasibility tests' lane-local parts too (the check needs them whenever it does
+            // not terminate): one team reduction for 16 maxima and 2 sums
+            double pn, pl, dn, dq;
+            pinf_partials(Eb, Eg, pn, pl);
+            dinf_partials(D, dn, dq);
+            double r[16] = {pr_u, z_u, ax_u, pr_p, z_p, ax_p, dr_u, q_u, aty_u, px_u, dr_p, q_p, aty_p, px_p, pn, dn};
+            double sm[2] = {pl, dq};
+            wv.max_sum_n(r, sm);
             pr_u = r[0], z_u = r[1], ax_u = r[2], pr_p = r[3], z_p = r[4], ax_p = r[5], dr_u = r[6];
             q_u = r[7], aty_u = r[8], px_u = r[9], dr_p = r[10], q_p = r[11], aty_p = r[12], px_p = r[13];
+            inf.pinf_nrm = r[14];
+            inf.dinf_nrm = r[15];
+            inf.pinf_lhs = sm[0];
+            inf.dinf_qdx = sm[1];
         }
         inf.pri_plain = pr_p;
         inf.dua_plain = dr_p;
@@ -1135,33 +1151,30 @@ struct WaveQP {
             inf.pri_norm_u = inf.pri_norm_s;
             inf.dua_norm_u = inf.dua_norm_s;
         }
-        wv.sync();
+        // (no barrier: the reduction's last one already follows every read of the exchange
+        // buffers above)
     }
 
-    // is_primal_infeasible (projects dy in place), lane-local part: the projected dy, ||E dy||_inf
-    // and u' max(dy, 0) + l' min(dy, 0)
+    // is_primal_infeasible's projection of dy onto the normal cone of the bounds (OSQP projects
+    // delta_y in place; the next ADMM step overwrites it, so only the test's second stage sees it)
+    IMPC_WF static double pinf_proj(double d, double l, double u) {
+        if (u > kInf * kMinScaling) return (l < -kInf * kMinScaling) ? 0.0 : dmin(d, 0.0);
+        if (l < -kInf * kMinScaling) return dmax(d, 0.0);
+        return d;
+    }
+    // is_primal_infeasible, lane-local part: ||E P(dy)||_inf and u' max(P(dy), 0) + l' min(P(dy), 0)
     IMPC_WF void pinf_partials(const double Eb[VS], const double Eg[GS], double &nrm_o, double &lhs_o) {
         const bool unsc = st.scaling > 0 && !st.scaled_termination;
         double nrm = 0.0, lhs = 0.0;
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (!vok[s]) continue;
-            double d = dyb(s);
-            if (ub[s] > kInf * kMinScaling)
-                d = (lb[s] < -kInf * kMinScaling) ? 0.0 : dmin(d, 0.0);
-            else if (lb[s] < -kInf * kMinScaling)
-                d = dmax(d, 0.0);
-            dyb(s) = d;
+            const double d = pinf_proj(dyb(s), lb[s], ub[s]);
             nrm = dmax(nrm, fabs(unsc ? Eb[s] * d : d));
             lhs += ub[s] * dmax(d, 0) + lb[s] * dmin(d, 0);
         }
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
             if (!gok[s]) continue;
-            double d = dyg(s);
-            if (ug[s] > kInf * kMinScaling)
-                d = (lg[s] < -kInf * kMinScaling) ? 0.0 : dmin(d, 0.0);
-            else if (lg[s] < -kInf * kMinScaling)
-                d = dmax(d, 0.0);
-            dyg(s) = d;
+            const double d = pinf_proj(dyg(s), lg[s], ug[s]);
             nrm = dmax(nrm, fabs(unsc ? Eg[s] * d : d));
             lhs += ug[s] * dmax(d, 0) + lg[s] * dmin(d, 0);
         }
@@ -1175,14 +1188,16 @@ struct WaveQP {
         if (nrm > kDivTol && lhs < eps * nrm) {
             double *pb = pbuf();
             _Pragma("unroll") for (int s = 0; s < GS; s++) {
-                if (gok[s])
-                    _Pragma("unroll") for (int e = 0; e < 4; e++) pb[gdst(s, e)] = a[s][e] * dyg(s);
+                if (gok[s]) {
+                    const double d = pinf_proj(dyg(s), lg[s], ug[s]);
+                    _Pragma("unroll") for (int e = 0; e < 4; e++) pb[gdst(s, e)] = a[s][e] * d;
+                }
             }
             wv.sync();
             double mx = 0.0;
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
                 if (!vok[s]) continue;
-                double t = ab[s] * dyb(s) + col_gather(NL * s + L, hid_[s]);
+                double t = ab[s] * pinf_proj(dyb(s), lb[s], ub[s]) + col_gather(NL * s + L, hid_[s]);
                 if (unsc) t = (1. / D[s]) * t;
                 mx = dmax(mx, fabs(t));
             }
@@ -1263,19 +1278,12 @@ struct WaveQP {
             eps_dinf *= 10;
         }
         int prim_ok = 0, dual_ok = 0, prim_inf = 0, dual_inf = 0;
-        // the same tests as below, the two infeasibility tests' first-stage norms and sums reduced
-        // over the team in one exchange (bitwise the values of the separate reductions)
         const bool ptest = T.m != 0 && !(inf.pri_res < eps_abs + eps_rel * inf.pri_norm_u);
         prim_ok = !ptest;
         dual_ok = inf.dua_res < eps_abs + eps_rel * inf.dua_norm_u;
-        if (ptest || !dual_ok) {
-            double mx[2] = {0.0, 0.0}, sm[2] = {0.0, 0.0};
-            if (ptest) pinf_partials(Eb, Eg, mx[0], sm[0]);
-            if (!dual_ok) dinf_partials(D, mx[1], sm[1]);
-            wv.max_sum_n(mx, sm);
-            if (ptest) prim_inf = pinf_stage2(eps_pinf, mx[0], sm[0], D);
-            if (!dual_ok) dual_inf = dinf_stage2(eps_dinf, mx[1], sm[1], D, Eb, Eg);
-        }
+        // the first stages' norms and sums were reduced with the residual norms (update_info)
+        if (ptest) prim_inf = pinf_stage2(eps_pinf, inf.pinf_nrm, inf.pinf_lhs, D);
+        if (!dual_ok) dual_inf = dinf_stage2(eps_dinf, inf.dinf_nrm, inf.dinf_qdx, D, Eb, Eg);
         if (prim_ok && dual_ok) {
             status = approximate ? IMPC_SOLVED_INACCURATE : IMPC_SOLVED;
             return 1;
@@ -1488,9 +1496,12 @@ struct WaveQP {
                 IMPC_SEC_START();
                 double D[VS], Eb[VS], Eg[GS];
                 load_scal(b, D, Eb, Eg);
-                update_info(inf, D, Eb, Eg);
+                int done = 0;
+                IMPC_REP(kSecChecks) {  // (phase-cost experiments only: the check is idempotent)
+                    update_info(inf, D, Eb, Eg);
+                    done = check_termination(inf, 0, status, obj, D, Eb, Eg);
+                }
                 info_iter = iter;
-                int done = check_termination(inf, 0, status, obj, D, Eb, Eg);
                 write_v_products();
                 IMPC_SEC(kSecChecks);
                 if (done) break;
