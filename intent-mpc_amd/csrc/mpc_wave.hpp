@@ -56,6 +56,10 @@ namespace impc {
 #define IMPC_DUP -1
 #endif
 #define IMPC_REP(X) for (int rep_ = 0; rep_ < (IMPC_DUP == (X) ? 2 : 1); rep_++)
+// Branch counters of the CPU emulation's instrumented builds (tools only; nothing in the product)
+#ifndef IMPC_COUNT
+#define IMPC_COUNT(X) ((void)0)
+#endif
 
 // Variants measured slower and removed in round 4 (their numbers stay in profiles/r0*/exp/README.md,
 // their code in git history): the twisted two-ended elimination, pair-blocked and chunked stage
@@ -946,7 +950,7 @@ struct WaveQP {
             // DPP), all in the VALU, with no transpose.  The next F and t are loaded two steps ahead.
             // One wavefront of the team (rw) runs it -- the others go straight to the barrier and
             // leave their SIMD's issue slots to the co-resident team.
-            if (L < 8) rb[L] = 8.0 * tb[L];
+            // (a_0 = t_0 = r_0[:8] is already in rb: stage 0 has no coupling, so S1 left it as is)
             if ((L >> 6) == rw) {
                 if (W == LD::WSPEC)
                     fwd_sweep<LD::WSPEC>(tb, rb, W);
@@ -1056,8 +1060,9 @@ struct WaveQP {
     struct Info {
         double pri_res, dua_res, pri_norm_u, dua_norm_u, pri_norm_s, dua_norm_s, pri_plain, dua_plain;
         // the infeasibility tests' first stages (is_primal_infeasible: ||E P(dy)||, u'P(dy)_+ +
-        // l'P(dy)_-; is_dual_infeasible: ||D dx||, q'dx), reduced with the norms above
-        double pinf_nrm, pinf_lhs, dinf_nrm, dinf_qdx;
+        // l'P(dy)_-; is_dual_infeasible: ||D dx||, q'dx, and its ||D^-1 P dx||), reduced with the
+        // norms above
+        double pinf_nrm, pinf_lhs, dinf_nrm, dinf_qdx, dinf_pdx;
     };
 
     IMPC_WF void load_scal(int64_t b, double D[VS], double Eb[VS], double Eg[GS]) {
@@ -1123,16 +1128,17 @@ struct WaveQP {
         {
             // the infeasibility tests' lane-local parts too (the check needs them whenever it does
             // not terminate): one team reduction for 16 maxima and 2 sums
-            double pn, pl, dn, dq;
+            double pn, pl, dn, dq, dp;
             pinf_partials(Eb, Eg, pn, pl);
-            dinf_partials(D, dn, dq);
-            double r[16] = {pr_u, z_u, ax_u, pr_p, z_p, ax_p, dr_u, q_u, aty_u, px_u, dr_p, q_p, aty_p, px_p, pn, dn};
+            dinf_partials(D, dn, dq, dp);
+            double r[17] = {pr_u, z_u, ax_u, pr_p, z_p, ax_p, dr_u, q_u, aty_u, px_u, dr_p, q_p, aty_p, px_p, pn, dn, dp};
             double sm[2] = {pl, dq};
             wv.max_sum_n(r, sm);
             pr_u = r[0], z_u = r[1], ax_u = r[2], pr_p = r[3], z_p = r[4], ax_p = r[5], dr_u = r[6];
             q_u = r[7], aty_u = r[8], px_u = r[9], dr_p = r[10], q_p = r[11], aty_p = r[12], px_p = r[13];
             inf.pinf_nrm = r[14];
             inf.dinf_nrm = r[15];
+            inf.dinf_pdx = r[16];
             inf.pinf_lhs = sm[0];
             inf.dinf_qdx = sm[1];
         }
@@ -1186,6 +1192,7 @@ struct WaveQP {
         const bool unsc = st.scaling > 0 && !st.scaled_termination;
         int res = 0;
         if (nrm > kDivTol && lhs < eps * nrm) {
+            IMPC_COUNT(0);
             double *pb = pbuf();
             _Pragma("unroll") for (int s = 0; s < GS; s++) {
                 if (gok[s]) {
@@ -1208,33 +1215,30 @@ struct WaveQP {
         return res;
     }
 
-    // is_dual_infeasible, lane-local part: ||D dx||_inf and q' dx
-    IMPC_WF void dinf_partials(const double D[VS], double &nrm_o, double &qdx_o) {
+    // is_dual_infeasible, lane-local part: ||D dx||_inf, q' dx and ||D^-1 P dx||_inf
+    IMPC_WF void dinf_partials(const double D[VS], double &nrm_o, double &qdx_o, double &pdx_o) {
         const bool unsc = st.scaling > 0 && !st.scaled_termination;
-        double nrm = 0.0, qdx = 0.0;
+        double nrm = 0.0, qdx = 0.0, pdx = 0.0;
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (!vok[s]) continue;
             nrm = dmax(nrm, fabs(unsc ? D[s] * dxv(s) : dxv(s)));
             qdx += q[s] * dxv(s);
+            double pv = pd[s] * dxv(s);
+            if (unsc) pv = (1. / D[s]) * pv;
+            pdx = dmax(pdx, fabs(pv));
         }
         nrm_o = nrm;
         qdx_o = qdx;
+        pdx_o = pdx;
     }
-    IMPC_WF int dinf_stage2(double eps, double nrm, double qdx, const double D[VS], const double Eb[VS],
-                            const double Eg[GS]) {
+    IMPC_WF int dinf_stage2(double eps, double nrm, double qdx, double mx, const double Eb[VS], const double Eg[GS]) {
         const bool unsc = st.scaling > 0 && !st.scaled_termination;
         const double cs = unsc ? c : 1.0;
         int res = 0;
         if (nrm > kDivTol && qdx < cs * eps * nrm) {
-            double mx = 0.0;
-            _Pragma("unroll") for (int s = 0; s < VS; s++) {
-                if (!vok[s]) continue;
-                double pv = pd[s] * dxv(s);
-                if (unsc) pv = (1. / D[s]) * pv;
-                mx = dmax(mx, fabs(pv));
-            }
-            mx = wv.max(mx);
+            IMPC_COUNT(1);
             if (mx < cs * eps * nrm) {
+                IMPC_COUNT(2);
                 double *xb = xbuf();
                 _Pragma("unroll") for (int s = 0; s < VS; s++)
                     if (vok[s]) xb[NL * s + L] = dxv(s);
@@ -1282,8 +1286,11 @@ struct WaveQP {
         prim_ok = !ptest;
         dual_ok = inf.dua_res < eps_abs + eps_rel * inf.dua_norm_u;
         // the first stages' norms and sums were reduced with the residual norms (update_info)
+        IMPC_COUNT(3);
+        if (ptest) IMPC_COUNT(4);
+        if (!dual_ok) IMPC_COUNT(5);
         if (ptest) prim_inf = pinf_stage2(eps_pinf, inf.pinf_nrm, inf.pinf_lhs, D);
-        if (!dual_ok) dual_inf = dinf_stage2(eps_dinf, inf.dinf_nrm, inf.dinf_qdx, D, Eb, Eg);
+        if (!dual_ok) dual_inf = dinf_stage2(eps_dinf, inf.dinf_nrm, inf.dinf_qdx, inf.dinf_pdx, Eb, Eg);
         if (prim_ok && dual_ok) {
             status = approximate ? IMPC_SOLVED_INACCURATE : IMPC_SOLVED;
             return 1;

@@ -61,3 +61,6 @@ timeout -k 10 500 python3 -u tools/bench_configs.py --steps 3 > $O/configs_s3.js
 cat $O/configs_s3.jsonl | cut -c1-200
 timeout -k 10 300 python3 -u tools/replan_bench.py > $O/replan_device.json 2> $O/replan.err || { tail -20 $O/replan.err; exit 1; }
 cat $O/replan_device.json
+echo "== small-batch latency"
+timeout -k 10 300 python3 -u tools/latency_ab.py > $O/latency.jsonl 2> $O/latency.err || { tail -20 $O/latency.err; exit 1; }
+cut -c1-160 $O/latency.jsonl
