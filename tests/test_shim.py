@@ -204,3 +204,48 @@ def test_workspace_pool_reuses_and_resets(ctx):
     b.h = None  # released below: the pool owns it (Batch.__del__ must not destroy it)
     for h in (h2, h3):
         assert impc.lib.impc_batch_release(h) == 0
+
+
+@pytest.mark.gpu
+def test_staged_values_results_subsets_and_update_order(ctx):
+    """The small-batch staging: values and warm start staged and uploaded in one DMA
+    by the solve, results back in one DMA; a partial impc_batch_get (x only, info only, y only)
+    returns what the full one does, and values staged after a solve replace the solved ones."""
+    import ctypes as C
+    import impc
+    from impc import scenarios
+    cfg = scenarios.intent_config(N=20, K=8, instances=1, hyps=4, seed=77)[8]
+    pat, v = cfg["pattern"], cfg["values"]
+    B, n, m = v["q"].shape[0], int(pat["n"]), int(pat["m"])
+    b = impc.Batch(ctx, n, m, pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], B)
+    try:
+        b.set_settings(impc.default_settings(verbose=0))
+        b.set_values(v["Px"], v["q"], v["Ax"], v["l"], v["u"])
+        b.warm_start(cfg["x_ws"])
+        b.solve()
+        x, y, info = b.get()
+        xs, ys = np.empty((B, n)), np.empty((B, m))
+        inf_s = np.empty(B, dtype=impc.INFO_DTYPE)
+        d = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+        assert impc.lib.impc_batch_get(b.h, d(xs), None, None) == 0
+        assert impc.lib.impc_batch_get(b.h, None, d(ys), None) == 0
+        assert impc.lib.impc_batch_get(b.h, None, None, d(inf_s)) == 0
+        assert np.array_equal(xs, x) and np.array_equal(ys, y)
+        assert np.array_equal(inf_s["iter"], info["iter"]) and np.array_equal(inf_s["status_val"], info["status_val"])
+        # re-staged values (another cost) after a solve: the next solve sees them, not the old ones
+        q2 = np.ascontiguousarray(v["q"] * 0.5)
+        b.set_values(v["Px"], q2, v["Ax"], v["l"], v["u"])
+        b.warm_start(cfg["x_ws"])
+        b.solve()
+        x2, _, info2 = b.get()
+        ref = oracle_solve(dict(cfg, values=dict(v, q=q2)))
+        assert np.array_equal(info2["iter"], ref[2]["iter"])
+        assert np.max(np.abs(x2 - ref[0])) <= 1e-5 * max(1.0, np.max(np.abs(ref[0])))
+    finally:
+        b.close()
+
+
+def oracle_solve(cfg):
+    from helpers import oracle
+    import impc
+    return oracle(cfg, impc.default_settings(verbose=0))
