@@ -226,10 +226,10 @@ def test_staged_values_results_subsets_and_update_order(ctx):
         x, y, info = b.get()
         xs, ys = np.empty((B, n)), np.empty((B, m))
         inf_s = np.empty(B, dtype=impc.INFO_DTYPE)
-        d = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
-        assert impc.lib.impc_batch_get(b.h, d(xs), None, None) == 0
-        assert impc.lib.impc_batch_get(b.h, None, d(ys), None) == 0
-        assert impc.lib.impc_batch_get(b.h, None, None, d(inf_s)) == 0
+        dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+        assert impc.lib.impc_batch_get(b.h, dp(xs), None, None) == 0
+        assert impc.lib.impc_batch_get(b.h, None, dp(ys), None) == 0
+        assert impc.lib.impc_batch_get(b.h, None, None, inf_s.ctypes.data_as(C.c_void_p)) == 0
         assert np.array_equal(xs, x) and np.array_equal(ys, y)
         assert np.array_equal(inf_s["iter"], info["iter"]) and np.array_equal(inf_s["status_val"], info["status_val"])
         # re-staged values (another cost) after a solve: the next solve sees them, not the old ones
