@@ -233,6 +233,8 @@ struct GpuTeam {
         if constexpr (NL == 64) wave_sync();
         else __syncthreads();
     }
+    // exchange point inside the caller's wavefront only (the long horizon's chunk operators)
+    __device__ static void wsync() { wave_sync(); }
     // barrier of the ADMM iteration's LDS exchanges (an LDS-only wait was measured slower)
     __device__ void lsync() { sync(); }
     __device__ double bcast(double v, int src) {

@@ -55,6 +55,9 @@ namespace impc {
 #ifndef IMPC_DUP
 #define IMPC_DUP -1
 #endif
+#ifndef IMPC_CHDUP
+#define IMPC_CHDUP 0
+#endif
 #define IMPC_REP(X) for (int rep_ = 0; rep_ < (IMPC_DUP == (X) ? 2 : 1); rep_++)
 // Branch counters of the CPU emulation's instrumented builds (tools only; nothing in the product)
 #ifndef IMPC_COUNT
@@ -326,6 +329,20 @@ struct WaveQP {
     IMPC_WF double *ebuf() { return lds + LD::E_OFF; }
     IMPC_WF double *xbuf() { return lds + LD::X_OFF; }
     IMPC_WF double *pbuf() { return lds + LD::P_OFF; }
+
+    // Chunked stage recursions of the long horizon (the W = 39 instance of the three-slot shape).
+    // That shape runs one team per CU, so the three wavefronts that wait out a serial sweep leave
+    // their SIMDs idle.  Each 39-step sweep runs as four chunks of <= 10 steps, one per wavefront,
+    // in two rounds: wave 0 runs the first chunk from the true start while waves 1 and 2 run theirs
+    // from zero for the chunk-end values only; after a barrier each of waves 1..3 forms its chunk's
+    // true start from those ends and the chunk operators (products of the chunk's -F_k, or -F_k^T
+    // backward, built with the factorisation: a_{o+10} = a^_{o+10} + P a_o) in one 8-lane reduction
+    // and runs its chunk again.  Dependent chain per sweep: 39 steps -> 20 steps and one reduction.
+    // Operators and ends live in the F region's tail (blocks >= 42, never read at W = 39).
+    static constexpr bool CHUNK = WF == 39 && NL == 256;
+    static constexpr int CH_OFF = LD::F_OFF + 64 * 42;
+    enum { kChFP1 = 0, kChFP2 = 64, kChFP21 = 128, kChBT1 = 192, kChBT2 = 256, kChBT21 = 320, kChEnd = 384 };
+    static_assert(!CHUNK || CH_OFF + kChEnd + 32 <= LD::R_OFF, "chunk operators do not fit the F region");
 
     // zero the exchange vectors (their tails are the zero slots read by padded entries)
     IMPC_WF void clear_exchange() {
@@ -736,11 +753,50 @@ struct WaveQP {
         _Pragma("unroll") for (int s = 0; s < VS; s++)
             if (vok[s] && vs_[s] == 0 && vr_[s] < 8)
                 _Pragma("unroll") for (int j = 0; j < 8; j++) cp[s][j] = 0.0;
+        if constexpr (CHUNK) chunk_ops();
         bad = (int)wv.max((double)bad);  // set by lane 0 only: team-wide, so every wavefront agrees
         clear_exchange();
         zero_products();  // the (4g + e) factorisation scratch shared the products region
         (void)n;
         return bad;
+    }
+
+    // F_k[r][c] from the recursion layout (factorize stores even stages' blocks transposed)
+    IMPC_WF static double f_el(const double *Fm, int k, int r, int c) {
+        return !(k & 1) ? Fm[64 * k + 8 * c + r] : Fm[64 * k + 8 * r + c];
+    }
+
+    // The chunk operators (CHUNK): wave 0 / 1 the forward chunks 1 / 2 (steps 10..19 / 20..29,
+    // P <- -F_k P with k ascending), wave 2 / 3 the backward chunks 1 / 2 (steps 20..29 / 10..19,
+    // P <- -F_k^T P with k descending); lane (i, j) holds P[i][j].  Then the two-chunk operators of
+    // the last chunk's start, P2 P1, forward and backward.
+    IMPC_WF void chunk_ops() {
+        const double *Fm = F();
+        double *C = lds + CH_OFF;
+        const int w = L >> 6, l = L & 63, i = l >> 3, j = l & 7;
+        const bool fwd = w < 2;
+        const int o = (w == 0 || w == 3) ? 10 : 20;
+        double *P = C + (fwd ? kChFP1 + 64 * w : kChBT1 + 64 * (w - 2));
+        P[l] = i == j ? 1.0 : 0.0;
+        wv.wsync();
+        for (int s = 0; s < 10; s++) {
+            const int k = fwd ? o + s : o + 9 - s;
+            double pc[8];
+            _Pragma("unroll") for (int m = 0; m < 8; m++) pc[m] = P[8 * m + j];
+            double v = 0.0;
+            _Pragma("unroll") for (int m = 0; m < 8; m++) v -= (fwd ? f_el(Fm, k, i, m) : f_el(Fm, k, m, i)) * pc[m];
+            wv.wsync();
+            P[l] = v;
+            wv.wsync();
+        }
+        wv.sync();
+        if (w == 0 || w == 2) {
+            const double *P1 = C + (w == 0 ? kChFP1 : kChBT1), *P2 = C + (w == 0 ? kChFP2 : kChBT2);
+            double v = 0.0;
+            _Pragma("unroll") for (int m = 0; m < 8; m++) v += P2[8 * i + m] * P1[8 * m + j];
+            C[(w == 0 ? kChFP21 : kChBT21) + l] = v;
+        }
+        wv.sync();
     }
 
     // One step of a stage recursion on the 8x8 lane grid: returns c - F v as R(c / 8 - f v), R the
@@ -794,6 +850,37 @@ struct WaveQP {
         }
     }
 
+    // Forward steps o .. o + WC - 1 (o even) from a_o = a at index i, fully unrolled: the results
+    // a_{o+1} .. a_{o+WC} stored to rb when CAP, the last one returned (every lane (i, j) holds
+    // a_{o+WC}[i] or [j] by its parity).
+    template <int WC, bool CAP>
+    IMPC_WF double fwd_run(const double *tb, double *rb, int o, double a) {
+        const double *Fm = lds + LD::F_OFF + 64 * o;
+        tb += 13 * o;
+        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;  // opaque: see lane_o
+        // (F, t) of the next even / odd step, loaded two steps ahead (reads past the last stage
+        // stay inside the LDS buffers and are never used)
+        double fe = Fm[l], te = tb[13 + j], fo = Fm[64 + l], to = tb[26 + i];
+        double c0[CQ], c1[CQ];
+        _Pragma("unroll") for (int q = 0; q < CQ; q++) c0[q] = c1[q] = 0.0;
+        _Pragma("unroll") for (int k = 0; k < WC; k += 2) {
+            const double f0 = fe, t0 = te;
+            fe = Fm[64 * (k + 2) + l];
+            te = tb[13 * (k + 3) + j];
+            a = rstep<true>(f0, t0, a);
+            if constexpr (CAP) capm<true>(c0, a, k, i);
+            if (k + 1 < WC) {
+                const double f1 = fo, t1 = to;
+                fo = Fm[64 * (k + 3) + l];
+                to = tb[13 * (k + 4) + i];
+                a = rstep<false>(f1, t1, a);
+                if constexpr (CAP) capm<false>(c1, a, k + 1, j);
+            }
+        }
+        if constexpr (CAP) cap_store<true>(c0, c1, rb + 13 * o, WC, true, i, j);
+        return a;
+    }
+
     // S2 body: a_{k+1} = t_{k+1} - F_k a_k for k = 0..W-1 (WC = W, or 0 for a runtime W).
     template <int WC>
     IMPC_WF void fwd_sweep(const double *tb, double *rb, int W) {
@@ -839,6 +926,38 @@ struct WaveQP {
                 *(wri ? rb + 13 * (k + 2) + i : junk) = a;
             }
         }
+    }
+
+    // Backward steps o + WC - 1 .. o (o even, the first of parity ODD) from x_{o+WC} = x, fully
+    // unrolled: x_{o+WC-1} .. x_o stored to xb when CAP, x_o returned.
+    template <bool ODD, int WC, bool CAP>
+    IMPC_WF double bwd_run(const double *eb, double *xb, int o, double x) {
+        const double *Fm = lds + LD::F_OFF + 64 * o;
+        eb += 13 * o;
+        const int lo = lane_o(), l = lo & 63, i = l >> 3, j = l & 7;
+        constexpr int k1 = WC - 2 > 0 ? WC - 2 : 0;
+        double fa = Fm[64 * (WC - 1) + l], ea = eb[13 * (WC - 1) + (ODD ? j : i)];
+        double fb = Fm[64 * k1 + l], ebv = eb[13 * k1 + (ODD ? i : j)];
+        double c0[CQ], c1[CQ];
+        _Pragma("unroll") for (int q = 0; q < CQ; q++) c0[q] = c1[q] = 0.0;
+        _Pragma("unroll") for (int m = 0; m < WC; m += 2) {
+            const int k = WC - 1 - m;
+            const int k2 = k - 2 > 0 ? k - 2 : 0, k3 = k - 3 > 0 ? k - 3 : 0;
+            const double f0 = fa, e0 = ea;
+            fa = Fm[64 * k2 + l];
+            ea = eb[13 * k2 + (ODD ? j : i)];
+            x = rstep<ODD>(f0, e0, x);
+            if constexpr (CAP) capm<ODD>(c0, x, m, ODD ? i : j);
+            if (m + 1 < WC) {
+                const double f1 = fb, e1 = ebv;
+                fb = Fm[64 * k3 + l];
+                ebv = eb[13 * k3 + (ODD ? i : j)];
+                x = rstep<!ODD>(f1, e1, x);
+                if constexpr (CAP) capm<!ODD>(c1, x, m + 1, ODD ? j : i);
+            }
+        }
+        if constexpr (CAP) cap_store<ODD>(c0, c1, xb + 13 * o, WC, false, i, j);
+        return x;
     }
 
     // S4 body for a first step k = W-1 of parity ODD: steps alternate strided (odd k) and
@@ -890,6 +1009,66 @@ struct WaveQP {
                 x = rstep<!ODD>(f1, e1, x);
                 *(ODD ? (wri ? xb + 13 * (k - 1) + i : junk) : (wrj ? xb + 13 * (k - 1) + j : junk)) = x;
             }
+        }
+    }
+
+    // S2 in chunks (CHUNK; see CH_OFF): steps 0..9 / 10..19 / 20..29 / 30..38 on waves 0..3.
+    // a_20 = a^_20 + P1 a_10, a_30 = a^_30 + P2 a^_20 + P2 P1 a_10 (a^: the chunk run from zero).
+    IMPC_WF void fwd_chunked(const double *tb, double *rb) {
+        const double *C = lds + CH_OFF;
+        double *ends = lds + CH_OFF + kChEnd;
+        const int w = L >> 6, l = lane_o() & 63, i = l >> 3, j = l & 7;
+        for (int rep_ = 0; rep_ < (IMPC_CHDUP == 1 ? 2 : 1); rep_++)
+        if (w == 0) {
+            (void)fwd_run<10, true>(tb, rb, 0, 8.0 * tb[i]);  // a_0 = t_0 (tb holds t / 8)
+        } else if (w == 1) {
+            const double e = fwd_run<10, false>(tb, rb, 10, 0.0);
+            if (j == 0) ends[i] = e;
+        } else if (w == 2) {
+            const double e = fwd_run<10, false>(tb, rb, 20, 0.0);
+            if (j == 0) ends[8 + i] = e;
+        }
+        wv.lsync();
+        for (int rep_ = 0; rep_ < (IMPC_CHDUP == 2 ? 2 : 1); rep_++)
+        if (w == 1) {
+            (void)fwd_run<10, true>(tb, rb, 10, rb[130 + i]);
+        } else if (w == 2) {
+            const double a = wv.sum_contig8(__builtin_fma(C[kChFP1 + l], rb[130 + j], 0.125 * ends[i]));
+            (void)fwd_run<10, true>(tb, rb, 20, a);
+        } else if (w == 3) {
+            const double p = __builtin_fma(C[kChFP2 + l], ends[j],
+                                           __builtin_fma(C[kChFP21 + l], rb[130 + j], 0.125 * ends[8 + i]));
+            (void)fwd_run<9, true>(tb, rb, 30, wv.sum_contig8(p));
+        }
+    }
+
+    // S4 in chunks: steps 38..30 / 29..20 / 19..10 / 9..0 on waves 0..3, from x_39 / x_30 / x_20 /
+    // x_10 (x_20 = x^_20 + P1 x_30, x_10 = x^_10 + P2 x^_20 + P2 P1 x_30).
+    IMPC_WF void bwd_chunked(const double *eb, double *xb) {
+        const double *C = lds + CH_OFF;
+        double *ends = lds + CH_OFF + kChEnd + 16;
+        const int w = L >> 6, l = lane_o() & 63, i = l >> 3, j = l & 7;
+        for (int rep_ = 0; rep_ < (IMPC_CHDUP == 1 ? 2 : 1); rep_++)
+        if (w == 0) {
+            (void)bwd_run<false, 9, true>(eb, xb, 30, 8.0 * eb[13 * 39 + j]);  // x_39 (odd: index j)
+        } else if (w == 1) {
+            const double e = bwd_run<true, 10, false>(eb, xb, 20, 0.0);
+            if (j == 0) ends[i] = e;
+        } else if (w == 2) {
+            const double e = bwd_run<true, 10, false>(eb, xb, 10, 0.0);
+            if (j == 0) ends[8 + i] = e;
+        }
+        wv.lsync();
+        for (int rep_ = 0; rep_ < (IMPC_CHDUP == 2 ? 2 : 1); rep_++)
+        if (w == 1) {
+            (void)bwd_run<true, 10, true>(eb, xb, 20, xb[390 + i]);
+        } else if (w == 2) {
+            const double x = wv.sum_contig8(__builtin_fma(C[kChBT1 + l], xb[390 + j], 0.125 * ends[i]));
+            (void)bwd_run<true, 10, true>(eb, xb, 10, x);
+        } else if (w == 3) {
+            const double p = __builtin_fma(C[kChBT2 + l], ends[j],
+                                           __builtin_fma(C[kChBT21 + l], xb[390 + j], 0.125 * ends[8 + i]));
+            (void)bwd_run<true, 10, true>(eb, xb, 0, wv.sum_contig8(p));
         }
     }
 
@@ -951,7 +1130,10 @@ struct WaveQP {
             // One wavefront of the team (rw) runs it -- the others go straight to the barrier and
             // leave their SIMD's issue slots to the co-resident team.
             // (a_0 = t_0 = r_0[:8] is already in rb: stage 0 has no coupling, so S1 left it as is)
-            if ((L >> 6) == rw) {
+            // The long horizon's W = 39 instance runs it in chunks on all four wavefronts (CHUNK).
+            if constexpr (CHUNK) {
+                fwd_chunked(tb, rb);
+            } else if ((L >> 6) == rw) {
                 if (W == LD::WSPEC)
                     fwd_sweep<LD::WSPEC>(tb, rb, W);
                 else
@@ -979,7 +1161,9 @@ struct WaveQP {
             // S4: backward 8-dim recursion x_k[:8] = e_k[:8] - F_k' x_{k+1}[:8] on the same grid and
             // stored layout: even steps reduce over j (contiguous), odd steps over i (strided).
             if (L < 8) xb[13 * W + L] = 8.0 * eb[13 * W + L];
-            if ((L >> 6) == rw) {
+            if constexpr (CHUNK) {
+                bwd_chunked(eb, xb);
+            } else if ((L >> 6) == rw) {
                 if (W == LD::WSPEC)
                     bwd_sweep<((LD::WSPEC - 1) & 1) != 0, LD::WSPEC>(eb, xb, W);
                 else if ((W - 1) & 1)
