@@ -102,6 +102,21 @@ def test_horizons(ctx, kernel, N):
     compare(gpu(ctx, cfg, s, kernel), oracle(cfg, s))
 
 
+@pytest.mark.parametrize("K", [3, 10, 11, 14])
+def test_long_horizon_chunked_recursions(ctx, K):
+    """N = 40 (W = 39): the long shape's stage recursions in four chunks on the four wavefronts
+    (chunk ends from zero, starts from the chunk operators, chunks re-run), over two, three and four
+    general-row slots per lane; rho = 1e-3 forces adaptive-rho refactorisations, which rebuild the
+    chunk operators."""
+    cfg = scenarios.static_config(N=40, K=K, batch=48, identical=False, seed=4000 + K)
+    for rho in (0.1, 1e-3):
+        s = impc.default_settings(rho=rho, **S25)
+        ref = oracle(cfg, s)
+        compare(gpu(ctx, cfg, s, impc.KERNEL_STRUCTURED), ref)
+        if rho < 0.1:
+            assert ref[2]["rho_updates"].max() >= 1
+
+
 def test_grouped_launch_equals_separate_solves(ctx):
     """impc_batch_solve_group over the K / K+1 buckets of a replan gives bitwise the results of
     separate impc_batch_solve calls (one work queue, per-batch tables)."""

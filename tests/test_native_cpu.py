@@ -79,10 +79,17 @@ def test_structured_emulation_short_horizons(N):
 
 
 def test_structured_emulation_long_horizon():
-    """N=40 (n=515): the three-slot team shape of the structured kernel."""
+    """N=40 (n=515): the three-slot team shape of the structured kernel, whose W = 39 instance runs
+    the stage recursions in four chunks (mpc_wave.hpp fwd_chunked / bwd_chunked), including
+    refactorisations by adaptive rho (the chunk operators rebuilt)."""
     cfg = take(scenarios.intent_config(N=40, K=10, instances=1, seed=4040)[10], 1)
     s = impc.default_settings(**S25)
     compare(emulate(cfg, s), oracle(cfg, s))
+    cfg = scenarios.static_config(N=40, K=11, batch=1, identical=False, seed=606)
+    s = impc.default_settings(rho=1e-3, **S25)
+    ref = oracle(cfg, s)
+    assert ref[2]["rho_updates"].max() >= 1
+    compare(emulate(cfg, s), ref)
 
 
 @pytest.mark.parametrize("rho", [0.1, 1e-3])
