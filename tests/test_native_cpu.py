@@ -94,10 +94,10 @@ def test_structured_emulation_long_horizon():
 
 @pytest.mark.parametrize("rho", [0.1, 1e-3])
 def test_structured_emulation_default_horizon_batch(rho):
-    """The default-horizon (W = 19) path of the structured kernel -- pair-blocked stage recursions
-    (mpc_wave.hpp fwd_pair / bwd_pair, H_k / M_k from the factorisation, u_k in S1, v_k in V) --
-    over several QPs of both intent buckets, and with a small initial rho whose adaptive updates
-    refactorise in-kernel (H_k, M_k rebuilt)."""
+    """The default-horizon (W = 19) instance of the structured kernel -- fully unrolled stage
+    recursions with register-captured results (mpc_wave.hpp fwd_sweep / bwd_sweep) -- over several
+    QPs of both intent buckets, and with a small initial rho whose adaptive updates refactorise
+    in-kernel (F_k and the Ahat_k^{-1} rows rebuilt)."""
     s = impc.default_settings(rho=rho, **S25)
     for name in ("config3_K8", "config2"):
         cfg = take(CFG[name], 2)
