@@ -90,7 +90,26 @@ __global__ void kr(double *o, unsigned long long *cyc, int Wr) {
     unsigned long long c0 = 0;
     for (int rep = -1; rep < REP; rep++) {
         if (rep == 0) c0 = __builtin_amdgcn_s_memtime();
-        if (MODE >= 8) {
+        if (MODE == 10) {
+            // two independent chains (different starts) interleaved in one instruction stream:
+            // is a step issue-bound or latency-bound at this occupancy?
+            double a = tb[i], b = tb[26 + i];
+            double fe = Fm[l], te = tb[13 + j], fo = Fm[64 + l], to = tb[26 + i];
+            for (int k = 0; k < W; k += 2) {
+                const double f0 = fe, t0 = te;
+                fe = Fm[64 * (k + 2) + l];
+                te = tb[13 * (k + 3) + j];
+                a = t0 - strided<true>(prod_nc(f0, a));
+                b = 0.5 * t0 - strided<true>(prod_nc(f0, b));
+                if (k + 1 >= W) break;
+                const double f1 = fo, t1 = to;
+                fo = Fm[64 * (k + 3) + l];
+                to = tb[13 * (k + 4) + i];
+                a = t1 - contig<true>(prod_nc(f1, a));
+                b = 0.5 * t1 - contig<true>(prod_nc(f1, b));
+            }
+            acc += a + b;
+        } else if (MODE >= 8) {
             const int r = l & 7, cp = l >> 3;
             double a = tb[r], f[8], fn[8], tn = tb[13 + r];
             double cap[3] = {0, 0, 0};
@@ -212,11 +231,12 @@ __global__ void kr(double *o, unsigned long long *cyc, int Wr) {
 
 int main() {
     double *o;
-    unsigned long long *c, h[10] = {};
+    unsigned long long *c, h[11] = {};
     if (hipMalloc(&o, 512 * sizeof(double)) || hipMalloc(&c, sizeof(h))) return 1;
     const char *nm[] = {"grid, update_dpp, store", "grid, mov_dpp, store", "grid, mov_dpp, capture",
                         "grid, mov_dpp, bare", "broadcast, store", "broadcast, bare", "unrolled, masked store",
-                        "unrolled, const-mask capture", "row-bcast, unrolled capture", "row-bcast, store"};
+                        "unrolled, const-mask capture", "row-bcast, unrolled capture", "row-bcast, store",
+                        "grid, two chains interleaved"};
     for (int threads : {64, 512}) {
         for (int it = 0; it < 2; it++) {
             hipLaunchKernelGGL(kr<0>, 1, threads, 0, 0, o, c, W);
@@ -229,10 +249,11 @@ int main() {
             hipLaunchKernelGGL(kr<7>, 1, threads, 0, 0, o, c, W);
             hipLaunchKernelGGL(kr<8>, 1, threads, 0, 0, o, c, W);
             hipLaunchKernelGGL(kr<9>, 1, threads, 0, 0, o, c, W);
+            hipLaunchKernelGGL(kr<10>, 1, threads, 0, 0, o, c, W);
         }
         if (hipMemcpy(h, c, sizeof(h), hipMemcpyDeviceToHost)) return 1;
         printf("-- %d lanes (%d wave(s) per SIMD)\n", threads, threads > 256 ? 2 : 1);
-        for (int m = 0; m < 10; m++) printf("%-28s %llu cyc/step\n", nm[m], h[m]);
+        for (int m = 0; m < 11; m++) printf("%-28s %llu cyc/step\n", nm[m], h[m]);
     }
     return 0;
 }
