@@ -57,8 +57,15 @@ $(LIBDIR)/impc_qp_prof.o: $(CSRC)/impc_qp.hip $(CSRC)/admm_core.hpp $(CSRC)/symb
 		$(ROOT)/include/impc_fanout.h $(ROOT)/include/impc_predict.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) $(call IDFLAGS,-prof) -DIMPC_SECTION_PROF -c $< -o $@
-$(PROFLIB): $(LIBDIR)/impc_qp_prof.o $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o $(LIBDIR)/minsnap.o
+$(PROFLIB): $(LIBDIR)/impc_qp_prof.o $(LIBDIR)/replan_run.o $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o $(LIBDIR)/minsnap.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ -o $@ $(LDLIBS)
+
+# the batched makePlanWithPred (include/impc_replan.h impc_replan_*): host orchestration + small
+# kernels over the library's own entry points
+$(LIBDIR)/replan_run.o: $(CSRC)/replan_run.hip $(CSRC)/lib_internal.hpp $(ROOT)/include/impc_replan.h \
+		$(ROOT)/include/impc_qp.h $(ROOT)/include/impc_mpc.h $(ROOT)/include/impc_fanout.h $(ROOT)/include/impc_select.h
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIBDIR)/symbolic.o: $(CSRC)/symbolic.cpp $(CSRC)/symbolic.hpp
 	@mkdir -p $(LIBDIR)
@@ -76,7 +83,7 @@ $(LIBDIR)/mpc_structure.o: $(CSRC)/mpc_structure.cpp $(CSRC)/mpc_structure.hpp
 	@mkdir -p $(LIBDIR)
 	$(CXX) $(HOSTFLAGS) -c $< -o $@
 
-$(LIB): $(LIBDIR)/impc_qp.o $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o $(LIBDIR)/minsnap.o
+$(LIB): $(LIBDIR)/impc_qp.o $(LIBDIR)/replan_run.o $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o $(LIBDIR)/minsnap.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ -o $@ $(LDLIBS)
 
 $(ORACLE): $(ROOT)/oracle/osqp_oracle.c
@@ -109,14 +116,14 @@ $(SHIMT): $(ROOT)/tests/native/shim_test.cpp $(ROOT)/include/OsqpEigen/OsqpEigen
 
 # batched makePlanWithPred over the C-ABI only (C++ integration example, driven by the tests)
 $(REPLANX): $(ROOT)/tests/native/replan_example.cpp $(ROOT)/include/impc_qp.h $(ROOT)/include/impc_mpc.h \
-		$(ROOT)/include/impc_fanout.h $(ROOT)/include/impc_select.h $(LIB)
+		$(ROOT)/include/impc_replan.h $(LIB)
 	@mkdir -p $(HARNDIR)
 	$(CXX) -O2 -std=c++17 -Wall -I$(ROOT)/include $< -L$(LIBDIR) -limpc_qp \
 		-Wl,-rpath,'$$ORIGIN/../../../intent-mpc_amd/lib' -o $@
 
 # kernel experiments (tools/ only): make variant V=name DEFS="-DX=1" -> lib/libimpc_qp_<name>.so,
 # selected at run time with IMPC_LIB_VARIANT=<name>
-variant: $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o $(LIBDIR)/minsnap.o
+variant: $(LIBDIR)/replan_run.o $(LIBDIR)/symbolic.o $(LIBDIR)/mpc_qp.o $(LIBDIR)/mpc_structure.o $(LIBDIR)/minsnap.o
 	$(HIPCC) $(HIPFLAGS) $(call IDFLAGS,-$(V)) $(DEFS) -c $(CSRC)/impc_qp.hip -o $(LIBDIR)/impc_qp_$(V).o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(LIBDIR)/impc_qp_$(V).o $^ -o $(LIBDIR)/libimpc_qp_$(V).so $(LDLIBS)
 

@@ -139,7 +139,11 @@ int impc_batch_destroy(impc_batch b);
  * mpcPlanner.cpp:436 / :527) lives on it. */
 int impc_batch_acquire(impc_ctx ctx, int64_t n, int64_t m, const int64_t *Pp, const int64_t *Pi, const int64_t *Ap,
                        const int64_t *Ai, int64_t batch, impc_batch *out);
+/* Releasing a batch that is already in the pool fails (IMPC_INVALID_ARGUMENT); past 64 pooled
+ * batches the oldest is destroyed. */
 int impc_batch_release(impc_batch b);
+/* The pool's size: pooled batches and the device bytes they hold (either pointer may be NULL). */
+int impc_ctx_pool_stats(impc_ctx ctx, int64_t *batches, int64_t *device_bytes);
 
 int impc_batch_set_settings(impc_batch b, const impc_settings *s);
 

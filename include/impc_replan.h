@@ -15,6 +15,7 @@
 #define IMPC_REPLAN_H
 #include <stdint.h>
 #include "impc_qp.h"
+#include "impc_mpc.h"
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -35,6 +36,125 @@ int impc_replan_commit_device(impc_ctx ctx, int32_t horizon, int64_t n, int64_t 
                               const uint64_t *x_cand, int32_t ncand, const int32_t *best_cand, const double *x_rows,
                               const impc_info *info_rows, double *plan_x, double *plan_states, int32_t *prev_count,
                               int8_t *first_time, int8_t *valid, void *stream);
+
+/* ======================================================================================
+ * The whole batched makePlanWithPred behind one call (mpcPlanner.cpp:571-661; its C++ caller is
+ * mpcNavigation.cpp:316-322).  A replan object holds, for I planning instances with K tracked
+ * dynamic obstacles each, the planner state (plan_x / plan_states / prev_count / first_time /
+ * valid, as above) and every device buffer and solver batch of a replan, allocated once.
+ *
+ * impc_replan_run, per instance, as the reference decides (:593-606):
+ *   FANOUT          not firstTime_ and predictions present: findClosestObstacle + getIntentComb
+ *                   (:663-769), the six candidates' castMPCToQP* (K and K + 1 obstacles), their
+ *                   solveTraj with timeLimit, candidate validity (solveProblem NoError = every
+ *                   status but NON_CVX, :513-518), getTrajectoryScore + evaluateTraj (:771-887);
+ *   SINGLE_FIRST    firstTime_ (static and dynamic obstacles cleared, :593-602), or no predictions
+ *                   and no current obstacles: ONE obstacle-free solveTraj, no time limit, no warm
+ *                   start on a first plan;
+ *   SINGLE_CURRENT  not firstTime_, no predictions, current dynamic obstacles kept: ONE solveTraj
+ *                   with each obstacle's current position / size held over the horizon
+ *                   (updateDynamicObstacles :316-341);
+ * all of it in ONE grouped solve, then every plan committed into the state (:636-639 / :653-657).
+ * Everything between the inputs and the committed state stays on the device: the host reads
+ * back the three branch counts only (the shapes' QP counts; 16 bytes), nothing else.
+ *
+ * The budget (:609-628): candidates are issued only while the replan's elapsed time is below
+ * issue_cutoff_s (0.15 s); every candidate carries timeLimit = max(limit - t, limit) (= limit for
+ * t >= 0).  All six candidates of every instance are issued at one instant -- the end of the
+ * device-side assembly -- so the cut-off is one check: past it no candidate is issued and every
+ * fan-out instance selects nothing (validTraj = false).  The single-solve branch has no cut-off.
+ * ====================================================================================== */
+typedef struct impc_replan_s *impc_replan;
+
+#define IMPC_REPLAN_FANOUT 0
+#define IMPC_REPLAN_SINGLE_FIRST 1
+#define IMPC_REPLAN_SINGLE_CURRENT 2
+
+typedef struct {
+    int64_t instances;         /* I planning instances */
+    int32_t num_obstacles;     /* K >= 1 dynamic obstacles per instance (predicted / current) */
+    int32_t pred_len;          /* L prediction steps per obstacle trajectory */
+    impc_mpc_params mpc;       /* initParam values; mpc.horizon = N (the selection's safety
+                                  distances are mpc.dynamic_safety_dist / static_safety_dist) */
+    impc_settings settings;    /* every solveTraj's OSQP settings (the reference: defaults,
+                                  verbose off, warm start on) */
+    double issue_cutoff_s;     /* makePlanWithPred's 0.15 s; <= 0: no cut-off */
+    int32_t queue_order;       /* IMPC_QUEUE_* of the grouped solve (results are identical) */
+    int32_t reserved;
+} impc_replan_config;
+
+/* Per-replan inputs, all DEVICE pointers (K = num_obstacles, L = pred_len, N = horizon). */
+typedef struct {
+    const double *pos, *vel;       /* [I][3] updateCurrStates */
+    const double *xref;            /* [I][N][8] getXRef (e.g. impc_reference_traj_device) */
+    const double *dyn_cur;         /* [I][K][3] dynamicObstaclesPos_ (current positions) */
+    const double *pred_pos;        /* [I][K][4][L][3] obPredPos_ */
+    const double *pred_size;       /* [I][K][4][L][3] obPredSize_ */
+    const double *prob;            /* [I][K][4] obIntentProb_ */
+    const int8_t *has_pred;        /* [I] obPredPos_.size() != 0; NULL = every instance */
+    const double *cur_size;        /* [I][K][3] dynamicObstaclesSize_ kept without predictions;
+                                      NULL = none (updatePredObstacles clears them, :364-371) */
+    const int32_t *cur_count;      /* [I] 0 or K current obstacles; NULL with cur_size = K */
+    double solver_time_limit;      /* solverTimeLimit_ (0.05 s); <= 0: settings.time_limit */
+    double elapsed_s;              /* seconds of the replan already spent before this call
+                                      (counted against the issue cut-off) */
+} impc_replan_inputs;
+
+/* What the last impc_replan_run did (host values). */
+typedef struct {
+    int64_t fanout, single_first, single_current; /* instances per branch */
+    int32_t issued;                                /* candidates issued (cut-off not reached) */
+    int32_t reserved;
+    double time_limit;                             /* the candidates' time limit (s, 0 = none) */
+    double stage_s;                                /* branch table + assembly, host wall (s) */
+    double total_s;                                /* host wall of the call (s); the solve, the
+                                                      selection and the commit are queued, not
+                                                      waited for */
+} impc_replan_stats;
+
+int impc_replan_create(impc_ctx ctx, const impc_replan_config *cfg, impc_replan *out);
+int impc_replan_destroy(impc_replan rp);
+/* The planner state from the host: plan_x [I][n] (currentStatesSol_ then currentControlsSol_ in
+ * QP variable order, n = 13 N - 5; NULL = zeros) and first_time [I] (NULL = every instance on its
+ * first plan).  currentStatesSol_.size() follows: 0 on a first plan, N once a plan exists (the
+ * reference sets firstTime_ = false only together with a full plan, :636-639 / :653-657). */
+int impc_replan_set_state(impc_replan rp, const double *plan_x, const int8_t *first_time);
+/* One batched makePlanWithPred (see above).  Stream-ordered on the context stream; returns once
+ * the solve, selection and commit are queued. */
+int impc_replan_run(impc_replan rp, const impc_replan_inputs *in);
+int impc_replan_get_stats(impc_replan rp, impc_replan_stats *out);
+
+/* DEVICE views, valid until the next run / destroy.  State: plan_x [I+1][n] (row I stays zero),
+ * plan_states [I+1][N][8], prev_count [I], first_time [I], valid [I] (the last replan's validTraj).
+ * Per instance of the last run: branch [I] (IMPC_REPLAN_*), best_cand [I] (fan-out instances:
+ * the selected candidate or -1; -1 otherwise), ob_idx [I] (closest obstacle; -1 for single-solve
+ * instances), cand_type / cand_slot [I][6] (getIntentComb order; -1 for single-solve instances). */
+typedef struct {
+    double *plan_x, *plan_states;
+    int32_t *prev_count;
+    int8_t *first_time, *valid, *branch;
+    int32_t *best_cand, *ob_idx, *cand_type, *cand_slot;
+} impc_replan_view;
+int impc_replan_view_device(impc_replan rp, impc_replan_view *out);
+
+/* Inspection of the last run (tests, tools): the solver batch of one QP shape, its QP count and
+ * its instances (DEVICE int64 [count'] in ascending order; count' = count / 4 or count / 2 for
+ * the fan-out shapes), and the assembled values (DEVICE, QP-major, `count` rows).  Shapes:
+ *   0  fan-out single-intent candidates (K obstacles), row 4 j + slot of fan-out instance j
+ *   1  fan-out two-intent candidates (K + 1 obstacles), row 2 j + slot - 4
+ *   2  single solve, first plan / no obstacles, row j of inst
+ *   3  single solve, current obstacles, row j of inst
+ * A shape not run in the last replan reports count 0 (its batch may still be NULL). */
+int impc_replan_shape(impc_replan rp, int32_t shape, impc_batch *batch, int64_t *count, const int64_t **inst,
+                      const double **Px, const double **q, const double **Ax, const double **l, const double **u);
+
+/* The vehicle following its plan (mpc_node.cpp:216-224: after a successful makePlan, currPos =
+ * getPos(dt), currVel = getVel(dt)): for every instance whose last replan produced a plan
+ * (valid[i] = 1), pos[i] / vel[i] = mpcPlanner::getPos(t) / getVel(t) (mpcPlanner.cpp:1257-1290:
+ * idx = floor(t / ts) clamped to the plan, linear interpolation towards state idx + 1); other
+ * instances keep pos / vel.  DEVICE pos, vel [I][3], updated in place; stream-ordered after the
+ * replan.  The next replan's x0 without a host round trip. */
+int impc_replan_advance_device(impc_replan rp, double t, double *pos, double *vel);
 
 #ifdef __cplusplus
 }

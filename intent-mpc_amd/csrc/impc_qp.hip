@@ -28,6 +28,7 @@
 #include "../../include/impc_predict.h"
 #include "../../include/impc_comm.h"
 #include "../../include/impc_replan.h"
+#include "lib_internal.hpp"
 #include "mpc_qp_internal.hpp"
 #include "admm_core.hpp"
 #include "mpc_structure.hpp"
@@ -691,8 +692,9 @@ int interleave(impc_batch b, const double *src_dev, double *dst, int64_t len, hi
 
 int deinterleave(impc_batch b, const double *src, double *dst_dev, int64_t len, hipStream_t st) {
     if (len <= 0) return IMPC_OK;
-    dim3 grid((unsigned)((len + kTile - 1) / kTile), (unsigned)((b->B + kTile - 1) / kTile));
-    hipLaunchKernelGGL(k_deinterleave, grid, dim3(256), 0, st, src, dst_dev, len, b->B, b->S);
+    // only the active rows: rows >= Bact keep their results (impc_batch_set_active)
+    dim3 grid((unsigned)((len + kTile - 1) / kTile), (unsigned)((b->Bact + kTile - 1) / kTile));
+    hipLaunchKernelGGL(k_deinterleave, grid, dim3(256), 0, st, src, dst_dev, len, b->Bact, b->S);
     HIP_OK(hipGetLastError());
     return IMPC_OK;
 }
@@ -1427,12 +1429,25 @@ int impc_batch_release(impc_batch b) {
     if (!b->pool_hash)  // a batch of impc_batch_create: hash it now
         b->pool_hash = pattern_hash(b->n, b->m, b->B, b->Pp.data(), b->nnzP ? b->Pi.data() : nullptr, b->Ap.data(),
                                     b->Ai.data());
+    for (const auto &e : ctx->pool)
+        if (e.second == b) return fail(IMPC_INVALID_ARGUMENT, "batch released twice");
     constexpr size_t kPoolMax = 64;  // released batches kept per context (oldest freed first)
     if (ctx->pool.size() >= kPoolMax) {
-        (void)impc_batch_destroy(ctx->pool.front().second);
+        // out of the pool first: impc_batch_destroy would otherwise look it up and erase it itself
+        impc_batch old = ctx->pool.front().second;
         ctx->pool.erase(ctx->pool.begin());
+        (void)impc_batch_destroy(old);
     }
     ctx->pool.emplace_back(b->pool_hash, b);
+    return IMPC_OK;
+}
+
+int impc_ctx_pool_stats(impc_ctx ctx, int64_t *batches, int64_t *device_bytes) {
+    if (!ctx) return fail(IMPC_INVALID_ARGUMENT, "null context");
+    int64_t bytes = 0;
+    for (const auto &e : ctx->pool) bytes += e.second->device_bytes;
+    if (batches) *batches = (int64_t)ctx->pool.size();
+    if (device_bytes) *device_bytes = bytes;
     return IMPC_OK;
 }
 
@@ -1628,7 +1643,7 @@ int impc_batch_warm_start(impc_batch b, const double *x, const double *y) {
         if (!rc) rc = interleave(b, b->in_yws, const_cast<double *>(b->dwk.yws), b->m, st);
         if (rc) return rc;
         hipLaunchKernelGGL(k_warm_start, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk,
-                           b->dst, b->B);
+                           b->dst, b->Bact);
         HIP_OK(hipGetLastError());
         return IMPC_OK;
     }
@@ -1927,7 +1942,7 @@ int impc_batch_update_lin_cost(impc_batch b, const double *q) {
     int rc = upload_interleaved(b, q, b->in_q, const_cast<double *>(b->dwk.q), b->n);
     if (rc) return rc;
     hipLaunchKernelGGL(k_update_q, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, b->ctx->stream, b->dsym, b->dwk,
-                       b->dst, b->B);
+                       b->dst, b->Bact);
     HIP_OK(hipGetLastError());
     return IMPC_OK;
 }
@@ -1960,7 +1975,7 @@ int impc_batch_update_bounds(impc_batch b, const double *l, const double *u) {
     if (!rc) rc = upload_interleaved(b, u, b->in_u, const_cast<double *>(b->dwk.u), b->m);
     if (rc) return rc;
     hipLaunchKernelGGL(k_update_bounds, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, b->ctx->stream, b->dsym,
-                       b->dwk, b->dst, b->B);
+                       b->dwk, b->dst, b->Bact);
     HIP_OK(hipGetLastError());
     return IMPC_OK;
 }
@@ -1986,7 +2001,7 @@ int impc_batch_update_lin_cost_device(impc_batch b, const double *q) {
     IMPC_TRY(ctx_order_after_all(b->ctx, st));
     HIP_OK(hipMemcpyAsync(b->in_q, q, bytes, hipMemcpyDeviceToDevice, st));
     IMPC_TRY(interleave(b, b->in_q, const_cast<double *>(b->dwk.q), b->n, st));
-    hipLaunchKernelGGL(k_update_q, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk, b->dst, b->B);
+    hipLaunchKernelGGL(k_update_q, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk, b->dst, b->Bact);
     HIP_OK(hipGetLastError());
     return IMPC_OK;
 }
@@ -2019,7 +2034,7 @@ int impc_batch_update_bounds_device(impc_batch b, const double *l, const double 
     IMPC_TRY(interleave(b, b->in_l, const_cast<double *>(b->dwk.l), b->m, st));
     IMPC_TRY(interleave(b, b->in_u, const_cast<double *>(b->dwk.u), b->m, st));
     hipLaunchKernelGGL(k_update_bounds, dim3((unsigned)(b->S / kBlock)), dim3(kBlock), 0, st, b->dsym, b->dwk, b->dst,
-                       b->B);
+                       b->Bact);
     HIP_OK(hipGetLastError());
     return IMPC_OK;
 }
@@ -2305,3 +2320,44 @@ int impc_copy_to_host(impc_ctx ctx, void *dst, const void *src, int64_t bytes) {
 
 // ---------------------------------------------------------------- replan state (impc_replan.h)
 #include "replan.hpp"
+
+// ---------------------------------------------------------------- hooks for the library's other
+// translation units (lib_internal.hpp; replan_run.hip): error reporting, stream ordering, and
+// direct writes into a batch's device input arrays
+namespace impc_lib {
+int set_error(int code, const std::string &msg) { return fail(code, msg); }
+int num_cu(impc_ctx ctx) { return ctx->num_cu; }
+int device(impc_ctx ctx) { return ctx->device; }
+hipStream_t stream(impc_ctx ctx) { return ctx->stream; }
+int order_after_all(impc_ctx ctx) {
+    HIP_OK(hipSetDevice(ctx->device));
+    return ctx_order_after_all(ctx, ctx->stream);
+}
+int batch_inputs_begin(impc_batch b, BatchInputs *out) {
+    if (!b || !out) return fail(IMPC_INVALID_ARGUMENT, "null batch");
+    IMPC_TRY(order_after_all(b->ctx));  // no launch on any stream still reads the arrays handed out
+    b->in_dirty = b->ws_dirty = false;   // staged host copies are superseded
+    out->Px = b->in_Px, out->q = b->in_q, out->Ax = b->in_Ax, out->l = b->in_l, out->u = b->in_u;
+    out->xws = b->in_xws;
+    out->n = b->n, out->m = b->m, out->nnzP = b->nnzP, out->nnzA = b->nnzA, out->B = b->B;
+    return IMPC_OK;
+}
+int batch_inputs_view(impc_batch b, BatchInputs *out) {
+    if (!b || !out) return fail(IMPC_INVALID_ARGUMENT, "null batch");
+    out->Px = b->in_Px, out->q = b->in_q, out->Ax = b->in_Ax, out->l = b->in_l, out->u = b->in_u;
+    out->xws = b->in_xws;
+    out->n = b->n, out->m = b->m, out->nnzP = b->nnzP, out->nnzA = b->nnzA, out->B = b->B;
+    return IMPC_OK;
+}
+int batch_inputs_end(impc_batch b, bool warm_x) {
+    if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
+    b->shared = false;
+    b->persist_valid = b->q_by_update = false;  // new data: the next solve sets up from scratch
+    b->values_set = true;
+    b->generic_dirty = true;
+    b->has_ws = warm_x;
+    b->ws_y = false;  // zero duals (solveTraj's warm start, mpcPlanner.cpp:480-497)
+    if (warm_x) b->settings.warm_start = b->dst.warm_start = 1;
+    return IMPC_OK;
+}
+}  // namespace impc_lib

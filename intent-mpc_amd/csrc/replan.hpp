@@ -5,7 +5,7 @@
 // :653-657 (single solve): currentStatesSol_ / currentControlsSol_ = the plan, firstTime_ = false.
 #pragma once
 
-namespace impc_replan {
+namespace impc_replan_k {
 
 __global__ __launch_bounds__(256) void k_commit(int32_t N, int64_t n, int64_t count, const int64_t *__restrict__ inst,
                                                 const uint64_t *__restrict__ x_cand, int32_t ncand,
@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void k_commit(int32_t N, int64_t n, int64_t co
     }
 }
 
-}  // namespace impc_replan
+}  // namespace impc_replan_k
 
 extern "C" int impc_replan_commit_device(impc_ctx ctx, int32_t horizon, int64_t n, int64_t count, const int64_t *inst,
                                          const uint64_t *x_cand, int32_t ncand, const int32_t *best_cand,
@@ -57,7 +57,7 @@ extern "C" int impc_replan_commit_device(impc_ctx ctx, int32_t horizon, int64_t 
     // after the solves and the selection, wherever they ran
     IMPC_TRY(ctx_order_after_all(ctx, st));
     const unsigned blocks = (unsigned)std::min<int64_t>(count, (int64_t)ctx->num_cu * 8);
-    hipLaunchKernelGGL(impc_replan::k_commit, dim3(blocks), dim3(256), 0, st, horizon, n, count, inst, x_cand, ncand,
+    hipLaunchKernelGGL(impc_replan_k::k_commit, dim3(blocks), dim3(256), 0, st, horizon, n, count, inst, x_cand, ncand,
                        best_cand, x_rows, info_rows, plan_x, plan_states, prev_count, first_time, valid);
     HIP_OK(hipGetLastError());
     return ctx_note_launch(ctx, st);

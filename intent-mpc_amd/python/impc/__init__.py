@@ -101,6 +101,7 @@ _sig("impc_batch_create", C.c_int, _P, C.c_int64, C.c_int64, _i64p, _i64p, _i64p
 _sig("impc_batch_destroy", C.c_int, _P)
 _sig("impc_batch_acquire", C.c_int, _P, C.c_int64, C.c_int64, _i64p, _i64p, _i64p, _i64p, C.c_int64, C.POINTER(_P))
 _sig("impc_batch_release", C.c_int, _P)
+_sig("impc_ctx_pool_stats", C.c_int, _P, C.POINTER(C.c_int64), C.POINTER(C.c_int64))
 _sig("impc_host_alloc", C.c_int, _P, C.c_int64, C.POINTER(_P))
 _sig("impc_host_free", C.c_int, _P, _P)
 _sig("impc_stream_create", C.c_int, _P, C.POINTER(_P))
@@ -254,7 +255,9 @@ EXPORTED = [
     "impc_batch_set_active", "impc_gather_rows_device", "impc_replan_commit_device", "impc_batch_acquire",
     "impc_batch_release", "impc_host_alloc", "impc_host_free", "impc_stream_create", "impc_stream_destroy",
     "impc_stream_wait", "impc_stream_synchronize", "impc_batch_set_values_async", "impc_batch_get_async",
-    "impc_batch_update_lin_cost_device", "impc_batch_update_bounds_device",
+    "impc_batch_update_lin_cost_device", "impc_batch_update_bounds_device", "impc_ctx_pool_stats",
+    "impc_replan_create", "impc_replan_destroy", "impc_replan_set_state", "impc_replan_run", "impc_replan_get_stats",
+    "impc_replan_view_device", "impc_replan_shape", "impc_replan_advance_device",
 ]
 
 

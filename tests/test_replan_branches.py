@@ -1,5 +1,5 @@
 """makePlanWithPred's two branches in the batched replan, and the planner state carried between
-replans on the device (impc.replan.DeviceReplan + PlanState, include/impc_replan.h), against the
+replans on the device (impc_replan_run through impc.replan.DeviceReplan, include/impc_replan.h), against the
 restatement oracle/replan_ref.py (mpcPlanner.cpp:571-661).
 
 One mixed batch of instances: on a first plan with and without predictions, with predictions
@@ -17,7 +17,7 @@ import pytest
 
 import impc
 from impc import scenarios
-from impc.replan import FANOUT, SINGLE_CURRENT, SINGLE_FIRST, DeviceReplan, PlanState
+from impc.replan import FANOUT, SINGLE_CURRENT, SINGLE_FIRST, DeviceReplan
 from oracle import replan_ref as ref
 
 from helpers import compare
@@ -118,21 +118,21 @@ def test_mixed_branches_three_chained_replans(ctx):
     has_pred = [idx % 3 != 1, idx % 5 != 2, idx % 7 != 3]    # per replan: obPredPos_ non-empty
     cur_count = np.where(idx % 2 == 0, K, 0)                  # current obstacles kept without predictions
     cur_size = np.broadcast_to(inst["size"], (I, K, 3)).copy()
-    state = PlanState(ctx, I, N, inst["prev"], first, np.full(I, N, np.int32))
     rp = DeviceReplan(ctx, p, pd, I, K, L, s)
+    rp.set_state(inst["prev"], first)
     pos, vel, pred = inst["pos"].copy(), inst["vel"].copy(), inst["pred"].copy()
     seen = set()
     try:
         for step in range(3):
-            before = state.plans()
+            before = rp.plans()
             dyn_cur = pred[:, :, 0, 0, :]                     # the obstacles' current positions
             out = rp.run(pos, vel, inst["xref"], dyn_cur=dyn_cur, pred_pos=pred, pred_size=pred_size,
-                         prob=inst["prob_all"], state=state, has_pred=has_pred[step], cur_size=cur_size,
+                         prob=inst["prob_all"], has_pred=has_pred[step], cur_size=cur_size,
                          cur_count=cur_count)
             seen.update(int(b) for b in out["branch"])
             expect, expect_first = _check_replan(out, before, pos, vel, inst["xref"], dyn_cur, pred, pred_size,
                                                  inst["prob_all"], has_pred[step], cur_size, cur_count, pd, s)
-            plan_x, ft, pc, valid = state.plans()
+            plan_x, ft, pc, valid = rp.plans()
             np.testing.assert_array_equal(plan_x, expect)       # the committed plans, bitwise
             np.testing.assert_array_equal(ft, expect_first)
             assert (pc[ft == 0] == N).all()
@@ -142,7 +142,6 @@ def test_mixed_branches_three_chained_replans(ctx):
             pred = np.concatenate([pred[:, :, :, 1:], pred[:, :, :, -1:]], axis=3)
         assert seen == {FANOUT, SINGLE_FIRST, SINGLE_CURRENT}
         # every first-plan instance with a plan fanned out on a later replan with predictions
-        assert (state.plans()[1] == 0).all()
+        assert (rp.plans()[1] == 0).all()
     finally:
         rp.close()
-        state.close()

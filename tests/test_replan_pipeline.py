@@ -1,22 +1,20 @@
-"""A whole makePlanWithPred replan on the device (impc.replan.DeviceReplan): intent fan-out ->
-on-device QP assembly of both candidate shapes -> one grouped solve -> candidate selection,
-against the host-built path of the same scenario (scenarios.intent_config, hypotheses 0-5 =
-getIntentComb's candidates, the distance-based closest obstacle).  Every stage must agree bit for
-bit: the candidate order, the assembled QP values, the solutions and the selected candidate.
+"""A whole makePlanWithPred replan on the device (impc_replan_run through impc.replan.DeviceReplan):
+intent fan-out -> on-device QP assembly of both candidate shapes -> one grouped solve -> candidate
+selection, against the host-array entry points of the same library stages on the same scenario
+(impc.intent_fanout, the host C++ builder impc.mpc_values, separate solves, impc.select_best).
+Every stage must agree bit for bit: the closest obstacle and candidate order, the assembled QP
+values, the solutions and the selected candidate.
 
-Every instance here is on the fan-out branch (not firstTime_, predictions present); its previous
-plan holds a single state (prev_count = 1), so findClosestObstacle takes its distance fallback
-(mpcPlanner.cpp:676-685) -- the scenario's closest obstacle -- while the QPs are linearised at and
-warm-started from the scenario's whole previous plan.  The branch selection itself is
-tests/test_replan_branches.py."""
+Every instance here is on the fan-out branch (not firstTime_, predictions present) with a full
+previous plan (currentStatesSol_.size() = N, the only size a planner past its first plan holds),
+so findClosestObstacle takes its direction-weighted score (mpcPlanner.cpp:687-707).  The branch
+selection itself is tests/test_replan_branches.py."""
 import numpy as np
 import pytest
 
 import impc
 from impc import scenarios
-from impc.replan import DeviceReplan
-
-from helpers import gpu
+from impc.replan import DeviceReplan, candidate_valid
 
 pytestmark = pytest.mark.gpu
 
@@ -28,45 +26,71 @@ def test_device_replan_matches_host_path(ctx):
     p, pd = impc.mpc_params(horizon=N)
     L = inst["pred"].shape[3]
     s = impc.default_settings(verbose=0)
+    pred_size = np.broadcast_to(inst["size"], inst["pred"].shape).copy()
+    zeros = np.zeros(I, np.int8)
     rp = DeviceReplan(ctx, p, pd, I, K, L, s)
     try:
-        pred_size = np.broadcast_to(inst["size"], inst["pred"].shape).copy()
-        out = rp.run(inst["pos"], inst["vel"], inst["xref"], inst["prev"], np.zeros(I, np.int8),
-                     np.ones(I, np.int32), inst["obp"], inst["pred"], pred_size, inst["prob_all"])
+        out = rp.run(inst["pos"], inst["vel"], inst["xref"], inst["prev"], zeros, None, inst["obp"], inst["pred"],
+                     pred_size, inst["prob_all"])
     finally:
         rp.close()
     assert (out["branch"] == 0).all()
-    assert np.array_equal(out["ob_idx"], inst["closest"])
-    for nm, kk in (("single", K), ("pair", K + 1)):
-        bk = buckets[kk]
-        v = bk["values"]
-        for got, key in zip(out["vals_" + nm], ("Px", "q", "Ax", "l", "u")):
-            np.testing.assert_array_equal(got, v[key], err_msg=f"{nm} {key}")
-        x, y, info = gpu(ctx, bk, s)
-        np.testing.assert_array_equal(out["x_" + nm], x)
-        np.testing.assert_array_equal(out["info_" + nm]["iter"], info["iter"])
-    # the host path's selection over the same solutions
+    fo = impc.intent_fanout(ctx, inst["pos"], zeros, inst["prev"], np.full(I, N, np.int32), inst["obp"],
+                            inst["pred"], pred_size, inst["prob_all"])
+    np.testing.assert_array_equal(out["ob_idx"], fo["ob_idx"])
+    np.testing.assert_array_equal(out["cand_type"], fo["cand_type"])
+    np.testing.assert_array_equal(out["cand_slot"], fo["cand_slot"])
+    n = 13 * N - 5
+    ws = np.zeros((I, n))
+    ws[:, : 8 * N] = inst["prev"].reshape(I, -1)
     batches = {}
-    for kk, bk in buckets.items():
-        pat, v = bk["pattern"], bk["values"]
-        b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], v["q"].shape[0])
-        b.set_settings(s)
-        b.set_values(v["Px"], v["q"], v["Ax"], v["l"], v["u"])
-        b.warm_start(bk["x_ws"], None)
-        b.solve()
-        b.get()
-        batches[kk] = b
     try:
-        d = scenarios.selection_arrays(buckets, {kk: b.device_results()[0] for kk, b in batches.items()})
-        params = dict(horizon=N, num_candidates=6, max_dynamic=d["kmax"], pred_len=d["L"], num_static=0, prev_len=N,
+        for nm, rep, kk, dp, dsz in (("single", 4, K, "single_pos", "single_size"), ("pair", 2, K + 1, "pair_pos",
+                                                                                     "pair_size")):
+            rows = np.repeat(np.arange(I), rep)
+            host = impc.mpc_values(p, inst["pos"][rows], inst["vel"][rows], inst["xref"][rows], inst["prev"][rows],
+                                   dyn_pos=fo[dp].reshape(rep * I, kk, L, 3), dyn_size=fo[dsz].reshape(rep * I, kk, L, 3))
+            for got, key in zip(out["vals_" + nm], ("Px", "q", "Ax", "l", "u")):
+                np.testing.assert_array_equal(got, host[key], err_msg=f"{nm} {key}")
+            pat = impc.mpc_pattern(p, 0, kk)
+            b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], rep * I)
+            b.set_settings(s)
+            b.set_values(host["Px"], host["q"], host["Ax"], host["l"], host["u"])
+            b.warm_start(ws[rows], None)
+            b.solve()
+            x, _, info = b.get()
+            np.testing.assert_array_equal(out["x_" + nm], x)
+            np.testing.assert_array_equal(out["info_" + nm]["iter"], info["iter"])
+            batches[nm] = (b, info)
+        # the host entry point of the selection over the same solutions
+        xs = {nm: batches[nm][0].device_results()[0] for nm in batches}
+        slot = fo["cand_slot"]
+        ptrs = np.zeros((I, 6), np.uint64)
+        dyn_count = np.zeros((I, 6), np.int32)
+        dyn_pos = np.zeros((I, 6, K + 1, L, 3))
+        dyn_size = np.zeros((I, 6, K + 1, L, 3))
+        for i in range(I):
+            for c in range(6):
+                sl = int(slot[i, c])
+                if sl < 4:
+                    ptrs[i, c] = xs["single"] + 8 * n * (4 * i + sl)
+                    dyn_count[i, c] = K
+                    dyn_pos[i, c, :K], dyn_size[i, c, :K] = fo["single_pos"][i, sl], fo["single_size"][i, sl]
+                else:
+                    ptrs[i, c] = xs["pair"] + 8 * n * (2 * i + sl - 4)
+                    dyn_count[i, c] = K + 1
+                    dyn_pos[i, c], dyn_size[i, c] = fo["pair_pos"][i, sl - 4], fo["pair_size"][i, sl - 4]
+        valid = candidate_valid(slot, batches["single"][1]["status_val"], batches["pair"][1]["status_val"])
+        params = dict(horizon=N, num_candidates=6, max_dynamic=K + 1, pred_len=L, num_static=0, prev_len=N,
                       dynamic_safety_dist=pd["dynamic_safety_dist"], static_safety_dist=pd["static_safety_dist"])
-        ref = impc.select_best(ctx, params, d["x_ptrs"], np.ones((I, 6), np.int8), np.zeros(I, np.int8), d["prev"],
-                               np.ones(I, np.int32), d["xref"], np.zeros((I, 0, 3)), np.zeros((I, 0, 3)),
-                               d["dyn_count"], d["dyn_pos"], d["dyn_size"], d["prob"])
+        ref = impc.select_best(ctx, params, ptrs.reshape(-1), valid, zeros, inst["prev"], np.full(I, N, np.int32),
+                               inst["xref"], np.zeros((I, 0, 3)), np.zeros((I, 0, 3)), dyn_count, dyn_pos, dyn_size,
+                               fo["closest_prob"])
     finally:
-        for b in batches.values():
+        for b, _ in batches.values():
             b.close()
     np.testing.assert_array_equal(out["best_cand"], ref["best_cand"])
+    assert (out["valid"] == (ref["best_cand"] >= 0)).all()
 
 
 def test_device_replan_from_paths(ctx):
@@ -93,8 +117,8 @@ def test_device_replan_from_paths(ctx):
     try:
         pos = inst["pos"].copy()
         for step in range(2):
-            out = rp.run(pos, inst["vel"], dev, inst["prev"], np.zeros(I, np.int8), np.ones(I, np.int32),
-                         inst["obp"], inst["pred"], pred_size, inst["prob_all"])
+            out = rp.run(pos, inst["vel"], dev, inst["prev"], np.zeros(I, np.int8), None, inst["obp"], inst["pred"],
+                         pred_size, inst["prob_all"])
             exp = np.array([r.xref(pos[i]) for i, r in enumerate(refs)])
             assert np.array_equal(out["xref"], exp), step
             rows = np.repeat(np.arange(I), 4)
@@ -105,53 +129,3 @@ def test_device_replan_from_paths(ctx):
     finally:
         rp.close()
         dev.close()
-
-
-def test_cpp_replan_example_matches_python_replan(ctx, tmp_path):
-    """tests/native/replan_example.cpp -- the batched makePlanWithPred a C++ planner would write
-    over the C-ABI alone (fan-out, per-candidate copies, assembly, grouped solve, selection) --
-    gives bit for bit the selection and solutions of impc.replan.DeviceReplan on one scenario."""
-    import ctypes as C
-    import os
-    import subprocess
-    exe = os.path.join(os.path.dirname(__file__), "native", "build", "replan_example")
-    I, K, N = 32, 4, 20
-    buckets = scenarios.intent_config(N=N, K=K, instances=I, hyps=6, seed=709)
-    inst = next(iter(buckets.values()))["instances"]
-    p, pd = impc.mpc_params(horizon=N)
-    L = inst["pred"].shape[3]
-    s = impc.default_settings(verbose=0)
-    pred_size = np.broadcast_to(inst["size"], inst["pred"].shape).copy()
-    first = np.zeros(I, np.int8)
-    pcount = np.ones(I, np.int32)
-    rp = DeviceReplan(ctx, p, pd, I, K, L, s)
-    try:
-        out = rp.run(inst["pos"], inst["vel"], inst["xref"], inst["prev"], first, pcount, inst["obp"], inst["pred"],
-                     pred_size, inst["prob_all"])
-    finally:
-        rp.close()
-    fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
-    with open(fin, "wb") as f:
-        f.write(np.array([I, K, L, N, inst["prev"].shape[1]], np.int32).tobytes())
-        f.write(bytes(p))
-        f.write(bytes(s))
-        f.write(np.array([pd["dynamic_safety_dist"], pd["static_safety_dist"]]).tobytes())
-        for a, dt in ((inst["pos"], np.float64), (inst["vel"], np.float64), (inst["xref"], np.float64),
-                      (inst["prev"], np.float64), (first, np.int8), (pcount, np.int32), (inst["obp"], np.float64),
-                      (inst["pred"], np.float64), (pred_size, np.float64), (inst["prob_all"], np.float64)):
-            f.write(np.ascontiguousarray(a, dt).tobytes())
-    r = subprocess.run([exe, str(fin), str(fout)], capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0, r.stdout + r.stderr
-    raw = open(fout, "rb").read()
-    best = np.frombuffer(raw[: 4 * I], np.int32)
-    np.testing.assert_array_equal(best, out["best_cand"])
-    off = 4 * I
-    for nm, cnt, kk in (("single", 4, K), ("pair", 2, K + 1)):
-        n = buckets[kk]["pattern"]["n"]
-        x = np.frombuffer(raw[off: off + 8 * cnt * I * n], np.float64).reshape(cnt * I, n)
-        off += 8 * cnt * I * n
-        it = np.frombuffer(raw[off: off + 8 * cnt * I], np.int64)
-        off += 8 * cnt * I
-        np.testing.assert_array_equal(x, out["x_" + nm])
-        np.testing.assert_array_equal(it, out["info_" + nm]["iter"])
-    assert off == len(raw)

@@ -249,3 +249,74 @@ def oracle_solve(cfg):
     from helpers import oracle
     import impc
     return oracle(cfg, impc.default_settings(verbose=0))
+
+
+@pytest.mark.gpu
+def test_workspace_pool_is_bounded_and_rejects_double_release(ctx):
+    """Releasing more than the pool's 64 batches (distinct capacities, so no reuse) destroys the
+    oldest: the pool stays at 64 batches and its device bytes stay those of 64 batches; releasing
+    a pooled batch again is refused (the eviction used to drop a second batch unfreed)."""
+    import ctypes as C
+    import impc
+    from impc import scenarios
+    cfg = scenarios.first_call_config(batch=1, seed=5)
+    pat = cfg["pattern"]
+    arrs = [np.ascontiguousarray(pat[k], np.int64) for k in ("Pp", "Pi", "Ap", "Ai")]
+    ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int64))  # noqa: E731
+    nb, nbytes = C.c_int64(), C.c_int64()
+    handles = []
+    for cap in range(1, 73):
+        h = C.c_void_p()
+        assert impc.lib.impc_batch_acquire(ctx.h, pat["n"], pat["m"], *[ip(a) for a in arrs], cap, C.byref(h)) == 0
+        handles.append(h)
+    assert impc.lib.impc_ctx_pool_stats(ctx.h, C.byref(nb), C.byref(nbytes)) == 0
+    base = nb.value  # batches other tests left pooled (acquires of a pooled capacity took them out)
+    per = []
+    for k, h in enumerate(handles):
+        assert impc.lib.impc_batch_release(h) == 0
+        assert impc.lib.impc_ctx_pool_stats(ctx.h, C.byref(nb), C.byref(nbytes)) == 0
+        assert nb.value == min(base + k + 1, 64), (k, nb.value)
+        per.append(nbytes.value)
+    # the last 64 released batches remain, and they alone hold the pool's device memory
+    assert impc.lib.impc_batch_release(handles[-1]) == 101  # IMPC_INVALID_ARGUMENT
+    assert impc.lib.impc_ctx_pool_stats(ctx.h, C.byref(nb), C.byref(nbytes)) == 0
+    assert nb.value == 64 and nbytes.value == per[-1]
+    # past 64, each release adds one batch of capacity c and evicts the one of capacity c - 64:
+    # the pool's bytes move by the difference of the two, never by a whole extra batch
+    steps = np.diff(per[-8:])
+    assert (steps == steps[0]).all(), steps
+
+
+@pytest.mark.gpu
+def test_set_active_generic_kernel_leaves_inactive_rows(ctx):
+    """impc_batch_set_active on the generic kernel: rows >= count keep the results they held (the
+    kernel, the warm-start and update kernels and the result copy take the active rows only)."""
+    import impc
+    from impc import scenarios
+    bk = scenarios.intent_config(N=20, K=3, instances=2, hyps=4, seed=21)[3]
+    pat, v = bk["pattern"], bk["values"]
+    B = v["q"].shape[0]
+    b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], B).set_kernel(
+        impc.KERNEL_GENERIC)
+    try:
+        s = impc.default_settings(verbose=0)
+        b.set_settings(s)
+        b.set_values(v["Px"], v["q"], v["Ax"], v["l"], v["u"])
+        b.warm_start(bk["x_ws"], None)
+        b.solve()
+        x0, y0, i0 = b.get()
+        b.set_active(B // 2)
+        b.set_values(v["Px"], 0.5 * v["q"], v["Ax"], v["l"], v["u"])
+        b.warm_start(bk["x_ws"], None)
+        b.solve()
+        x1, y1, i1 = b.get()
+        np.testing.assert_array_equal(x1[B // 2:], x0[B // 2:])
+        np.testing.assert_array_equal(y1[B // 2:], y0[B // 2:])
+        np.testing.assert_array_equal(i1["iter"][B // 2:], i0["iter"][B // 2:])
+        assert (x1[: B // 2] != x0[: B // 2]).any()
+        b.update_lin_cost(v["q"])  # the persistent update of the active rows only
+        b.solve()
+        x2, _, _ = b.get()
+        np.testing.assert_array_equal(x2[B // 2:], x0[B // 2:])
+    finally:
+        b.close()
