@@ -21,12 +21,19 @@ Workloads (--workload):
       grouped launch over its ~42 pattern buckets per step, and each step ends with one RCCL
       all_gather of every QP's cost record (the 64-byte impc_info, read straight from HBM).
   config5 (BASELINE.json configs[4]): 65,536 N=40 QPs (8192 instances x 8 hypotheses, 10(+1)
-      dynamic obstacles), split by instance across the ranks, as a receding window on persistent
-      workspaces: setup + first solve before the timed region, then every step is
-      osqp_update_lin_cost (the shifted reference) + osqp_update_bounds (the next x0) + the solve
-      resuming from the kept scaling, rho and iterates (impc_batch_update_*_device: each step's
-      values are built on the device beforehand by impc_mpc_build_values_device), and one RCCL
-      all_gather of the cost records (N > 1).
+      dynamic obstacles), split by instance across the ranks, as a CLOSED receding window on
+      persistent workspaces: setup + first solve before the timed region, then every timed step,
+      all on the device: each QP's next x0 = getPos / getVel(dt) of its own last solution
+      (impc_batch_follow_plan_device, mpc_node.cpp:216-224), the reference one step further along
+      the path and the predicted obstacles one step on (impc_copy_rows_device windows), the next
+      q, l, u built by impc_mpc_build_values_device (linearisation point and A kept: the
+      factorisation is reused, BASELINE configs[4]), osqp_update_lin_cost + osqp_update_bounds
+      (impc_batch_update_*_device) and the solve resuming from the kept scaling, rho and iterates;
+      one RCCL all_gather of the cost records (N > 1).
+  live: the reference's live planner horizon N = 30 (autonomous_flight planner_param.yaml:25) on
+      config 3's workload -- 8192 instances x 8 intent hypotheses, 8(+1) dynamic obstacles, full
+      setup + warm start + solve per QP every step (the long shape's compile-time W = 29 instance);
+      split by instance like config 3.
 
 Multi-GPU: one process per GPU.  `python bench.py --gpus N` without a torchrun environment
 starts `torch.distributed.run` with N processes itself (before touching the GPU) and exits with
@@ -250,7 +257,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=("config3", "config4", "config5"), default="config3")
+    ap.add_argument("--workload", choices=("config3", "config4", "config5", "live"), default="config3")
     ap.add_argument("--instances", type=int, default=8192,
                     help="config3 / config5: planning instances of the job (x8 hypotheses)")
     ap.add_argument("--total-qps", type=int, default=262144, help="config4: QPs of the whole job")
@@ -292,8 +299,8 @@ def main():
     settings = impc.default_settings(verbose=0)
     strong = args.workload != "config3" or args.scaling == "strong"
     t_gen = time.time()
-    if args.workload in ("config3", "config5"):
-        N_, K_, seed_ = (20, 8, 3000) if args.workload == "config3" else (40, 10, 5000)
+    if args.workload in ("config3", "config5", "live"):
+        N_, K_, seed_ = {"config3": (20, 8, 3000), "config5": (40, 10, 5000), "live": (30, 8, 3030)}[args.workload]
         buckets = scenarios.intent_config(N=N_, K=K_, instances=args.instances, hyps=8,
                                           seed=seed_ if strong else D.rank_seed(seed_, rank))
         if strong:  # equal instance ranges (every instance carries the same 8 hypotheses)
@@ -330,23 +337,16 @@ def main():
     comm = D.make_comm(dist, ctx) if (world > 1 or args.workload == "config4") else None
     receding = None
     if args.workload == "config5":  # persistent workspaces: setup + first solve, untimed
-        for _, b in batches:
-            b.set_persistent(True)
-        impc.solve_group([b for _, b in batches]) if len(batches) > 1 else batches[0][1].solve()
-        ctx.synchronize()
-        receding = receding_values(impc, scenarios, ctx, bks, args.warmup + args.steps)
-        rstep = [0]
+        receding = RecedingLoop(impc, ctx, batches, args.warmup + args.steps)
+        receding.start()
     max_qps = max(counts)
     recv = impc.DeviceArray(ctx, (world * max_qps,), impc.INFO_DTYPE) if comm is not None else None
     # strong scaling: the cost records of the step's QPs reach every rank inside the step
     gather_in_step = (args.workload == "config4" or (strong and world > 1)) and not args.no_allgather
 
     def launch():
-        if receding is not None:  # the next receding-window step's updates (values already on the device)
-            for (_, b), (q, l, u) in zip(batches, receding[rstep[0]]):
-                b.update_lin_cost_device(q.ptr)
-                b.update_bounds_device(l.ptr, u.ptr)
-            rstep[0] += 1
+        if receding is not None:  # the closed loop's next step, built on the device
+            receding.advance()
         if grouped:  # one persistent launch over all pattern buckets (impc_batch_solve_group)
             impc.solve_group([b for _, b in batches])
         else:
@@ -443,12 +443,23 @@ def main():
             e2e["frac_of_resident"] = e2e["qps_per_s"] / (total_qps * args.steps / elapsed) if world == 1 else None
 
     cpu = parity = None
-    if rank == 0 and world == 1 and args.cpu_sample > 0 and receding is not None:
-        cpu, ref = cpu_baseline_receding(impc, ctx, bks, settings, receding, min(args.cpu_sample, 128))
-        parity = parity_vs_oracle(results, ref)
-        parity["what"] = ("the last receding step's x, y, status, iterations for the CPU sample's QPs vs the oracle's "
-                          "persistent workspaces after the same setup + update sequence (parity unpinned against the "
-                          "real libosqp, DESIGN.md 3)")
+    per_step = None
+    if receding is not None:
+        # untimed replay of the same closed loop (the device is deterministic: its last step must
+        # equal the timed run's bit for bit), recording every step's iterations / statuses and the
+        # CPU sample's per-step q, l, u for the oracle
+        k_sample = min(args.cpu_sample, 1024) if (rank == 0 and world == 1) else 0
+        rec = receding.replay(k_sample)
+        per_step = rec["per_step"]
+        per_step_det = all(np.array_equal(r[0], x) and np.array_equal(r[2]["iter"], inf["iter"])
+                           for r, (x, _, inf) in zip(rec["last"], results))
+        per_step = {"steps": per_step, "replay_bitwise_equal": bool(per_step_det)}
+        if k_sample:
+            cpu, ref = cpu_baseline_receding(bks, settings, rec, args.cpu_threads)
+            parity = parity_vs_oracle(results, ref)
+            parity["what"] = ("the last closed-loop step's x, y, status, iterations for the CPU sample's QPs vs the "
+                              "oracle's persistent workspaces after the same setup + per-step update sequence (parity "
+                              "unpinned against the real libosqp, DESIGN.md 3)")
         args.cpu_all_cores = 0
     elif rank == 0 and world == 1 and args.cpu_sample > 0:
         cpu, ref = cpu_baseline(bks, settings, args.cpu_sample, args.cpu_threads)
@@ -470,12 +481,21 @@ def main():
             "global_batch": global_batch, "batch_per_gpu": total_qps, "shard_qps": counts,
             "buckets": {str(bk["K"]): int(b.B) for bk, b in batches},
         }
+    elif args.workload == "live":
+        config = {
+            "workload": ("live planner horizon: 65536 N=30 QPs = 8192 instances x 8 intent hypotheses, 8(+1) dynamic "
+                         "obstacles (planner_param.yaml:25), split by instance over the ranks, full setup + warm start "
+                         "+ solve per QP, per-step RCCL all-gather of the cost records (N>1)"),
+            "global_batch": global_batch, "batch_per_gpu": total_qps, "shard_qps": counts,
+            "buckets": {str(bk["K"]): int(b.B) for bk, b in batches},
+        }
     elif args.workload == "config5":
         config = {
             "workload": ("configs[4]: 65536 N=40 QPs = 8192 instances x 8 intent hypotheses, 10(+1) dynamic obstacles, "
-                         "split by instance over the ranks, receding window on persistent workspaces (per step: "
-                         "update q + update l, u + solve from the kept scaling / rho / iterates), per-step RCCL "
-                         "all-gather of the cost records (N>1)"),
+                         "split by instance over the ranks, closed receding window on persistent workspaces (per step, "
+                         "on the device: x0 = getPos/getVel(dt) of each QP's last solution, reference and predicted "
+                         "obstacles one step on, q / l / u built, update q + update l, u + solve from the kept "
+                         "scaling / rho / iterates), per-step RCCL all-gather of the cost records (N>1)"),
             "global_batch": global_batch, "batch_per_gpu": total_qps, "shard_qps": counts,
             "buckets": {str(bk["K"]): int(b.B) for bk, b in batches},
         }
@@ -540,10 +560,13 @@ def main():
         "e2e_serial": e2e_serial,
         "selection": sel,
         "cost_allgather": gathered,
+        "receding_steps": per_step,
         "gen_seconds": t_gen,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if receding is not None:
+        receding.close()
     if recv is not None:
         recv.free()
     if comm is not None:
@@ -576,40 +599,119 @@ def select_candidates(impc, scenarios, ctx, buckets, batch_by_k, pd_params):
             "picked_histogram": [int(v) for v in picks]}
 
 
-def receding_values(impc, scenarios, ctx, bks, steps):
-    """Config 5's receding window: for shift s = 1..steps, every QP's next values q, l, u (xRef
-    shifted s steps along the path, x0 = the previous plan's state s, the same linearisation points
-    and obstacles -- scenarios.receding_update's step), built on the device by the MPC builder.
-    Returns [step][bucket] = (q, l, u) device arrays."""
-    out = [[] for _ in range(steps)]
-    for bk in bks:
-        N, K = bk["N"], bk["K"]
-        d, inst = bk["instances"], bk["inst"]
-        xref, prev = d["xref"][inst], d["prev"][inst]
-        nb = inst.size
-        p, _ = impc.mpc_params(horizon=N)
-        L = bk["dyn_pos"].shape[2]
-        bld = impc.MpcBuilder(ctx, p, 0, K, L)
-        n, m, nnzP, nnzA = impc.mpc_dims(p, 0, K)
-        keep = [impc.DeviceArray(ctx, np.ascontiguousarray(a, np.float64)) for a in (prev, bk["dyn_pos"], bk["dyn_size"])]
-        Px, Ax = impc.DeviceArray(ctx, (nb, nnzP)), impc.DeviceArray(ctx, (nb, nnzA))
-        step = xref[:, -1, :] - xref[:, -2, :]
-        for s in range(1, steps + 1):
-            ext = xref[:, -1:, :] + step[:, None, :] * np.arange(1, s + 1)[None, :, None]
-            xr = np.concatenate([xref[:, s:], ext], axis=1)
-            tmp = [impc.DeviceArray(ctx, np.ascontiguousarray(a, np.float64))
-                   for a in (prev[:, s, 0:3], prev[:, s, 3:6], xr)]
-            q, l, u = impc.DeviceArray(ctx, (nb, n)), impc.DeviceArray(ctx, (nb, m)), impc.DeviceArray(ctx, (nb, m))
-            bld.build(nb, tmp[0].ptr, tmp[1].ptr, tmp[2].ptr, keep[0].ptr, None, None, None, keep[1].ptr, keep[2].ptr,
-                      Px.ptr, q.ptr, Ax.ptr, l.ptr, u.ptr)
-            ctx.synchronize()
-            for t in tmp:
-                t.free()
-            out[s - 1].append((q, l, u))
-        for a in keep + [Px, Ax]:
-            a.free()
-        bld.close()
-    return out
+class RecedingLoop:
+    """Config 5's closed receding window on the device (module docstring).  Per bucket: each QP's
+    reference path extended past the horizon (the last segment continued, as getReferenceTraj pads),
+    its predicted obstacles extended by their last entry (the builder's .back() rule), the
+    linearisation point of the setup (the previous plan: A and the factorisation are kept), x0 /
+    v0 device rows updated from each solve (impc_batch_follow_plan_device)."""
+
+    def __init__(self, impc, ctx, batches, steps):
+        self.impc, self.ctx, self.batches, self.steps, self.t = impc, ctx, batches, steps, 0
+        self.buckets = []
+        for bk, b in batches:
+            N, K = bk["N"], bk["K"]
+            d, inst = bk["instances"], bk["inst"]
+            xref, prev = d["xref"][inst], d["prev"][inst]
+            nb = inst.size
+            p, pd = impc.mpc_params(horizon=N)
+            L = bk["dyn_pos"].shape[2]
+            T = steps + 1
+            step = xref[:, -1, :] - xref[:, -2, :]
+            ext = xref[:, -1:, :] + step[:, None, :] * np.arange(1, T + 1)[None, :, None]
+            path = np.ascontiguousarray(np.concatenate([xref, ext], axis=1))            # [nb][N + T][8]
+            dpx = np.concatenate([bk["dyn_pos"], np.repeat(bk["dyn_pos"][:, :, -1:], T, axis=2)], axis=2)
+            dsx = np.concatenate([bk["dyn_size"], np.repeat(bk["dyn_size"][:, :, -1:], T, axis=2)], axis=2)
+            n, m, nnzP, nnzA = impc.mpc_dims(p, 0, K)
+            D = impc.DeviceArray
+            e = dict(N=N, K=K, L=L, T=T, nb=nb, ts=pd["ts"], b=b, bk=bk,
+                     bld=impc.MpcBuilder(ctx, p, 0, K, L),
+                     path=D(ctx, path), dpx=D(ctx, np.ascontiguousarray(dpx)), dsx=D(ctx, np.ascontiguousarray(dsx)),
+                     lin=D(ctx, np.ascontiguousarray(prev, np.float64)),
+                     pos0=np.ascontiguousarray(d["pos"][inst], np.float64),
+                     vel0=np.ascontiguousarray(d["vel"][inst], np.float64),
+                     pos=D(ctx, (nb, 3)), vel=D(ctx, (nb, 3)), xr=D(ctx, (nb, N, 8)), dp=D(ctx, (nb, K, L, 3)),
+                     ds=D(ctx, (nb, K, L, 3)), Px=D(ctx, (nb, nnzP)), Ax=D(ctx, (nb, nnzA)), q=D(ctx, (nb, n)),
+                     l=D(ctx, (nb, m)), u=D(ctx, (nb, m)))
+            self.buckets.append(e)
+
+    def _solve(self):
+        bs = [b for _, b in self.batches]
+        self.impc.solve_group(bs) if len(bs) > 1 else bs[0].solve()
+
+    def start(self):
+        """Setup + first solve of every QP from the scenario's values and warm start (untimed)."""
+        for e in self.buckets:
+            bk, b = e["bk"], e["b"]
+            v = bk["values"]
+            b.set_persistent(True)
+            split = self.impc.shared_split(v["Px"], v["Ax"])
+            if split is None:
+                b.set_values(v["Px"], v["q"], v["Ax"], v["l"], v["u"])
+            else:
+                b.set_values_shared(*split, v["q"], v["l"], v["u"])
+            b.warm_start(bk["x_ws"], None)
+            e["pos"].set(e["pos0"])
+            e["vel"].set(e["vel0"])
+        self._solve()
+        self.ctx.synchronize()
+        self.t = 0
+
+    def build(self):
+        """The next step's x0 (from the last solve), windows and q, l, u -- all enqueued on the device."""
+        impc, ctx = self.impc, self.ctx
+        self.t += 1
+        t = self.t
+        for e in self.buckets:
+            N, K, L, T, nb = e["N"], e["K"], e["L"], e["T"], e["nb"]
+            e["b"].follow_plan_device(N, e["ts"], e["ts"], e["pos"].ptr, e["vel"].ptr)
+            impc.copy_rows_device(ctx, e["xr"].ptr, 64 * N, e["path"].ptr + 64 * t, 64 * (N + T), 64 * N, nb)
+            for src, dst in (("dpx", "dp"), ("dsx", "ds")):
+                impc.copy_rows_device(ctx, e[dst].ptr, 24 * L, e[src].ptr + 24 * t, 24 * (L + T), 24 * L, nb * K)
+            e["bld"].build(nb, e["pos"].ptr, e["vel"].ptr, e["xr"].ptr, e["lin"].ptr, None, None, None, e["dp"].ptr,
+                           e["ds"].ptr, e["Px"].ptr, e["q"].ptr, e["Ax"].ptr, e["l"].ptr, e["u"].ptr)
+
+    def advance(self):
+        """One timed closed-loop step: next values on the device, persistent updates (the solve
+        follows in the caller's launch)."""
+        self.build()
+        for e in self.buckets:
+            e["b"].update_lin_cost_device(e["q"].ptr)
+            e["b"].update_bounds_device(e["l"].ptr, e["u"].ptr)
+
+    def replay(self, k_sample):
+        """The same loop again from the setup, untimed: per step the iterations / statuses of every
+        QP and the first k_sample QPs' q, l, u (bucket-proportional) for the oracle; the last step's
+        results per bucket."""
+        total = sum(e["nb"] for e in self.buckets)
+        for e in self.buckets:
+            e["k"] = min(e["nb"], max(1, int(round(k_sample * e["nb"] / total)))) if k_sample else 0
+            e["ups"] = []
+        self.start()
+        per_step = []
+        for _ in range(self.steps):
+            self.advance()
+            for e in self.buckets:
+                if e["k"]:
+                    e["ups"].append(tuple(rows_to_host(self.impc, self.ctx, e[a], e["k"]) for a in ("q", "l", "u")))
+            self._solve()
+            its, sts = [], []
+            for e in self.buckets:
+                _, _, info = e["b"].get()
+                its.append(info["iter"])
+                sts.append(info["status_val"])
+            it, st = np.concatenate(its), np.concatenate(sts)
+            per_step.append({"step": self.t, "mean_iter": float(it.mean()), "p50_iter": float(np.median(it)),
+                             "max_iter": int(it.max()),
+                             "status_counts": {str(int(k)): int(v) for k, v in zip(*np.unique(st, return_counts=True))}})
+        last = [e["b"].get() for e in self.buckets]
+        return {"per_step": per_step, "last": last, "buckets": self.buckets}
+
+    def close(self):
+        for e in self.buckets:
+            e["bld"].close()
+            for k in ("path", "dpx", "dsx", "lin", "pos", "vel", "xr", "dp", "ds", "Px", "Ax", "q", "l", "u"):
+                e[k].free()
 
 
 def rows_to_host(impc, ctx, darr, k):
@@ -621,42 +723,54 @@ def rows_to_host(impc, ctx, darr, k):
     return out
 
 
-def cpu_baseline_receding(impc, ctx, bks, settings, receding, sample):
+def cpu_baseline_receding(bks, settings, rec, threads):
     """Config 5's CPU path: the oracle's persistent workspaces (osqp_setup, warm start, solve once,
-    then per receding step osqp_update_lin_cost + osqp_update_bounds + osqp_solve, the reference's
-    polyTrajSolver pattern) over a bounded sample -- the first QPs of each bucket, one thread; the
-    timed part is the update + solve steps.  Returns (line object, [(k, x, y, info) per bucket] of
-    the last step, for the parity check)."""
+    then per closed-loop step osqp_update_lin_cost + osqp_update_bounds + osqp_solve with the step's
+    q, l, u -- the reference's polyTrajSolver pattern) over a bounded sample, the first QPs of each
+    bucket, on `threads` host threads (one QP's chain per task; the oracle's C calls release the
+    GIL); the timed part is the update + solve steps.  Returns (line object, [(k, x, y, info) per
+    bucket] of the last step, for the parity check)."""
+    from concurrent.futures import ThreadPoolExecutor
+
     from oracle import osqp_oracle as ora
-    total = sum(bk["values"]["q"].shape[0] for bk in bks)
     s = ora.settings_from(settings)
     ref, t_all, n_all = [], 0.0, 0
-    for j, bk in enumerate(bks):
-        B = bk["values"]["q"].shape[0]
-        k = min(B, max(1, int(round(sample * B / total))))
+    for e in rec["buckets"]:
+        bk, k, ups = e["bk"], e["k"], e["ups"]
         v = bk["values"]
-        ups = [tuple(rows_to_host(impc, ctx, a, k) for a in step[j]) for step in receding]
-        xs, ys, infos = [], [], []
-        for i in range(k):
+
+        def setup(i):
             w = ora.Workspace(bk["pattern"], v["Px"][i], v["q"][i], v["Ax"][i], v["l"][i], v["u"][i], s)
             w.warm_start(bk["x_ws"][i], np.zeros(int(bk["pattern"]["m"])))
             w.solve()
-            t = time.perf_counter()
+            return w
+
+        with ThreadPoolExecutor(max_workers=threads) as ex:
+            ws = list(ex.map(setup, range(k)))
+
+        def chain(i):
+            out = None
             for q, l, u in ups:
-                w.update_lin_cost(q[i])
-                w.update_bounds(l[i], u[i])
-                x, y, info = w.solve()
-            t_all += time.perf_counter() - t
-            n_all += len(ups)
+                ws[i].update_lin_cost(q[i])
+                ws[i].update_bounds(l[i], u[i])
+                out = ws[i].solve()
+            return out
+
+        t = time.perf_counter()
+        with ThreadPoolExecutor(max_workers=threads) as ex:
+            res = list(ex.map(chain, range(k)))
+        t_all += time.perf_counter() - t
+        n_all += k * len(ups)
+        for w in ws:
             w.close()
-            xs.append(x)
-            ys.append(y)
-            infos.append(info)
-        ref.append((k, np.array(xs), np.array(ys), np.array(infos, dtype=infos[0].dtype)))
-    return {"value": n_all / t_all, "unit": "QP-solves/s", "cores": 1, "kind": "port",
+        ref.append((k, np.array([r[0] for r in res]), np.array([r[1] for r in res]),
+                    np.array([r[2] for r in res], dtype=res[0][2].dtype)))
+    steps = len(rec["buckets"][0]["ups"])
+    return {"value": n_all / t_all, "unit": "QP-solves/s", "cores": threads, "kind": "port",
             "host_cpus": os.cpu_count(), "cpu_model": cpu_info(),
-            "sample": f"{sum(r[0] for r in ref)} QPs of the workload (first of each bucket) x {len(receding)} receding "
-                      f"steps, oracle persistent workspaces (update q, update l/u, solve), one thread ({t_all:.1f} s)"}, ref
+            "sample": f"{sum(r[0] for r in ref)} QPs of the workload (first of each bucket) x {steps} closed-loop "
+                      f"steps, oracle persistent workspaces (update q, update l/u, solve) with the device-built values "
+                      f"of each step, {threads} threads ({t_all:.1f} s)"}, ref
 
 
 def measured_traffic(build_id, qps, kernel, values_mode, workload):

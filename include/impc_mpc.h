@@ -121,6 +121,13 @@ int impc_repeat_rows_device(impc_ctx ctx, const void *src, int64_t rows, int64_t
 int impc_gather_rows_device(impc_ctx ctx, const void *src, int64_t row_bytes, const int64_t *idx, int64_t count,
                             void *dst, void *stream);
 
+/* Strided device-to-device copy (hipMemcpy2DAsync): `rows` rows of `width` bytes from src (row
+ * pitch spitch bytes) to dst (pitch dpitch) -- a receding window's next slice of each QP's longer
+ * reference / prediction arrays, or x0 columns out of the QP-major solutions.  Asynchronous on
+ * `stream` (NULL = the context's stream). */
+int impc_copy_rows_device(impc_ctx ctx, void *dst, int64_t dpitch, const void *src, int64_t spitch, int64_t width,
+                          int64_t rows, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -156,6 +156,13 @@ int impc_replan_shape(impc_replan rp, int32_t shape, impc_batch *batch, int64_t 
  * replan.  The next replan's x0 without a host round trip. */
 int impc_replan_advance_device(impc_replan rp, double t, double *pos, double *vel);
 
+/* The same for a receding window of single QPs (a persistent batch of mpcPlanner QPs, n = 13
+ * horizon - 5): QP b's next x0, pos[b] / vel[b] [B][3], = getPos(t) / getVel(t) of its own last
+ * solution when the solve returned one (status SOLVED, SOLVED_INACCURATE, MAX_ITER_REACHED,
+ * TIME_LIMIT_REACHED); a QP without one (infeasible: x is OSQP_NAN) keeps its x0.  DEVICE pos, vel,
+ * updated in place after the batch's last solve, on the context stream. */
+int impc_batch_follow_plan_device(impc_batch b, int32_t horizon, double ts, double t, double *pos, double *vel);
+
 #ifdef __cplusplus
 }
 #endif

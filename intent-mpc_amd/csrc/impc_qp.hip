@@ -896,10 +896,14 @@ int64_t resident_groups(int num_cu, size_t lds, int64_t work) {
     return std::min<int64_t>(work, (int64_t)num_cu * per_cu);
 }
 
-// the default-horizon instance (compile-time W) takes the batch when its W is the shape's WSPEC
-bool spec_ok(impc_batch b) {
-    const int ws = b->vs == kWaveVSLong ? impc::WaveLds<256, kWaveVSLong, 2>::WSPEC : impc::WaveLds<256, kWaveVS, 2>::WSPEC;
-    return b->ms->W == ws;
+// the compile-time horizon instance that takes the batch: its W when the shape has one for it
+// (WSPEC: the default horizon of the shape; WSPEC2: the long shape's N = 30), else 0 (runtime W)
+int spec_w(impc_batch b) {
+    using LL = impc::WaveLds<256, kWaveVSLong, 2>;
+    using LD1 = impc::WaveLds<256, kWaveVS, 2>;
+    const int W = b->ms->W;
+    if (b->vs == kWaveVSLong) return (W == LL::WSPEC || (LL::WSPEC2 && W == LL::WSPEC2)) ? W : 0;
+    return (W == LD1::WSPEC || (LD1::WSPEC2 && W == LD1::WSPEC2)) ? W : 0;
 }
 
 // ---- work-queue order (impc_batch_set_queue_order, csrc/queue.hpp)
@@ -1040,13 +1044,16 @@ int launch_group_w(impc_ctx ctx, hipStream_t st, const GroupEntry *entries, int 
     HIP_OK(hipGetLastError());
     return IMPC_OK;
 }
-// spec: every batch of the group has the shape's default horizon
+// spec: the compile-time horizon every batch of the launch shares (spec_w), or 0
 template <int VS, int GS, bool TIER = false>
 int launch_group(impc_ctx ctx, hipStream_t st, const GroupEntry *entries, int count, int64_t total, size_t lds,
-                 unsigned *counter, bool spec, const uint32_t *ord) {
-    constexpr int WS = impc::WaveLds<Shape<VS>::NL, VS, GS>::WSPEC;
-    return spec ? launch_group_w<VS, GS, WS, TIER>(ctx, st, entries, count, total, lds, counter, ord)
-                : launch_group_w<VS, GS, 0, TIER>(ctx, st, entries, count, total, lds, counter, ord);
+                 unsigned *counter, int spec, const uint32_t *ord) {
+    using LD = impc::WaveLds<Shape<VS>::NL, VS, GS>;
+    constexpr int WS = LD::WSPEC, WS2 = LD::WSPEC2;
+    if (spec && spec == WS) return launch_group_w<VS, GS, WS, TIER>(ctx, st, entries, count, total, lds, counter, ord);
+    if constexpr (WS2 != 0)
+        if (spec == WS2) return launch_group_w<VS, GS, WS2, TIER>(ctx, st, entries, count, total, lds, counter, ord);
+    return launch_group_w<VS, GS, 0, TIER>(ctx, st, entries, count, total, lds, counter, ord);
 }
 
 // dynamic LDS bytes of the structured kernel for a shape (team VS, GS) and pattern (CG, n); 0 if
@@ -1785,7 +1792,7 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
         int first, count;
         int64_t total;
         size_t lds;
-        bool spec;
+        int spec;  // the launch's compile-time horizon (-1: no batch yet; 0: runtime W)
         unsigned *counter;
     };
     std::vector<Launch> launches;
@@ -1797,11 +1804,11 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
         impc_batch b = bs[order[(size_t)p]];
         if (launches.empty() || launches.back().vs != b->vs || launches.back().gs != b->gs ||
             launches.back().tier != b->tier)
-            launches.push_back(Launch{b->vs, b->gs, b->tier, p, 0, 0, 0, true, b->d_counter});
+            launches.push_back(Launch{b->vs, b->gs, b->tier, p, 0, 0, 0, -1, b->d_counter});
         Launch &L = launches.back();
         L.count++;
         L.lds = std::max(L.lds, wave_lds_bytes(b->vs, b->gs, b->wt));
-        L.spec = L.spec && spec_ok(b);
+        L.spec = L.spec < 0 ? spec_w(b) : (L.spec == spec_w(b) ? L.spec : 0);
         GroupEntry &e = entries[(size_t)p];
         e.T = b->wt;
         e.io = wave_io(b);

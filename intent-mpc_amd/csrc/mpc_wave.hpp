@@ -159,6 +159,9 @@ struct WaveLds {
     // stage count whose recursions are fully unrolled (the reference's default horizon N = 20
     // for the one-variable-per-lane shape, N = 40 for the long-horizon shape)
     static constexpr int WSPEC = NMAX <= 256 ? 19 : 39;
+    // a second compile-time horizon of the long shape: the reference's live planner, N = 30
+    // (autonomous_flight planner_param.yaml:25, mpc_interactive mpc_param.yaml:1); 0 = none
+    static constexpr int WSPEC2 = NMAX <= 256 ? 0 : 29;
     // exchange vector length: zero tail past NMAX, and room for the factorisation scratch
     // (the sweeps' two-steps-ahead prefetches read at most 13 (W + 4) + 8 past the start), and
     // room for the factorisation's dense stage scratch (FA .. DIAGX below)
@@ -247,7 +250,7 @@ IMPC_WF int row_type(double l, double u) {  // set_rho_vec (auxil.h:34)
 template <class WV, int NL, int VS, int GS, int WF = 0, bool TIER = false>
 struct WaveQP {
     using LD = WaveLds<NL, VS, GS>;
-    static_assert(WF == 0 || WF == LD::WSPEC, "WF is 0 or the shape's default horizon");
+    static_assert(WF == 0 || WF == LD::WSPEC || WF == LD::WSPEC2, "WF is 0 or one of the shape's compiled horizons");
     IMPC_WF int Wst() const { return WF ? WF : T.W; }
     WV &wv;
     const WaveTables &T;
@@ -330,19 +333,24 @@ struct WaveQP {
     IMPC_WF double *xbuf() { return lds + LD::X_OFF; }
     IMPC_WF double *pbuf() { return lds + LD::P_OFF; }
 
-    // Chunked stage recursions of the long horizon (the W = 39 instance of the three-slot shape).
-    // That shape runs one team per CU, so the three wavefronts that wait out a serial sweep leave
-    // their SIMDs idle.  Each 39-step sweep runs as four chunks of <= 10 steps, one per wavefront,
-    // in two rounds: wave 0 runs the first chunk from the true start while waves 1 and 2 run theirs
-    // from zero for the chunk-end values only; after a barrier each of waves 1..3 forms its chunk's
-    // true start from those ends and the chunk operators (products of the chunk's -F_k, or -F_k^T
-    // backward, built with the factorisation: a_{o+10} = a^_{o+10} + P a_o) in one 8-lane reduction
-    // and runs its chunk again.  Dependent chain per sweep: 39 steps -> 20 steps and one reduction.
-    // Operators and ends live in the F region's tail (blocks >= 42, never read at W = 39).
-    static constexpr bool CHUNK = WF == 39 && NL == 256;
-    static constexpr int CH_OFF = LD::F_OFF + 64 * 42;
+    // Chunked stage recursions of the long horizon (the compile-time W = 39 and W = 29 instances of
+    // the three-slot shape).  That shape runs one team per CU, so the three wavefronts that wait out
+    // a serial sweep leave their SIMDs idle.  Each W-step sweep runs as four chunks, CL = 2 ceil(W/8)
+    // steps each and W - 3 CL in the last (W = 39: 10, 10, 10, 9; W = 29: 8, 8, 8, 5), one per
+    // wavefront, in two rounds: wave 0 runs the first chunk from the true start while waves 1 and 2
+    // run theirs from zero for the chunk-end values only; after a barrier each of waves 1..3 forms
+    // its chunk's true start from those ends and the chunk operators (products of the chunk's -F_k,
+    // or -F_k^T backward, built with the factorisation: a_{o+CL} = a^_{o+CL} + P a_o) in one 8-lane
+    // reduction and runs its chunk again.  Dependent chain per sweep: W steps -> 2 CL steps and one
+    // reduction.  Operators and ends live in the F region's tail (blocks >= W + 3, never read).
+    // CL is even, so every chunk starts on an even stage (the sweeps' index parity).
+    static constexpr bool CHUNK = WF > 0 && NL == 256 && VS == 3;
+    static constexpr int CL = WF > 0 ? 2 * ((WF + 7) / 8) : 2;
+    static constexpr int CLAST = WF - 3 * CL;
+    static constexpr int CH_OFF = LD::F_OFF + 64 * (WF + 3);
     enum { kChFP1 = 0, kChFP2 = 64, kChFP21 = 128, kChBT1 = 192, kChBT2 = 256, kChBT21 = 320, kChEnd = 384 };
     static_assert(!CHUNK || CH_OFF + kChEnd + 32 <= LD::R_OFF, "chunk operators do not fit the F region");
+    static_assert(!CHUNK || (CLAST >= 1 && CLAST <= CL), "chunk lengths");
 
     // zero the exchange vectors (their tails are the zero slots read by padded entries)
     IMPC_WF void clear_exchange() {
@@ -766,21 +774,21 @@ struct WaveQP {
         return !(k & 1) ? Fm[64 * k + 8 * c + r] : Fm[64 * k + 8 * r + c];
     }
 
-    // The chunk operators (CHUNK): wave 0 / 1 the forward chunks 1 / 2 (steps 10..19 / 20..29,
-    // P <- -F_k P with k ascending), wave 2 / 3 the backward chunks 1 / 2 (steps 20..29 / 10..19,
-    // P <- -F_k^T P with k descending); lane (i, j) holds P[i][j].  Then the two-chunk operators of
-    // the last chunk's start, P2 P1, forward and backward.
+    // The chunk operators (CHUNK): wave 0 / 1 the forward chunks 1 / 2 (steps CL..2CL-1 /
+    // 2CL..3CL-1, P <- -F_k P with k ascending), wave 2 / 3 the backward chunks 1 / 2 (steps
+    // 3CL-1..2CL / 2CL-1..CL, P <- -F_k^T P with k descending); lane (i, j) holds P[i][j].  Then the
+    // two-chunk operators of the last chunk's start, P2 P1, forward and backward.
     IMPC_WF void chunk_ops() {
         const double *Fm = F();
         double *C = lds + CH_OFF;
         const int w = L >> 6, l = L & 63, i = l >> 3, j = l & 7;
         const bool fwd = w < 2;
-        const int o = (w == 0 || w == 3) ? 10 : 20;
+        const int o = (w == 0 || w == 3) ? CL : 2 * CL;
         double *P = C + (fwd ? kChFP1 + 64 * w : kChBT1 + 64 * (w - 2));
         P[l] = i == j ? 1.0 : 0.0;
         wv.wsync();
-        for (int s = 0; s < 10; s++) {
-            const int k = fwd ? o + s : o + 9 - s;
+        for (int s = 0; s < CL; s++) {
+            const int k = fwd ? o + s : o + CL - 1 - s;
             double pc[8];
             _Pragma("unroll") for (int m = 0; m < 8; m++) pc[m] = P[8 * m + j];
             double v = 0.0;
@@ -1012,63 +1020,68 @@ struct WaveQP {
         }
     }
 
-    // S2 in chunks (CHUNK; see CH_OFF): steps 0..9 / 10..19 / 20..29 / 30..38 on waves 0..3.
-    // a_20 = a^_20 + P1 a_10, a_30 = a^_30 + P2 a^_20 + P2 P1 a_10 (a^: the chunk run from zero).
+    // S2 in chunks (CHUNK; see CH_OFF): steps 0..CL-1 / CL..2CL-1 / 2CL..3CL-1 / 3CL..W-1 on waves
+    // 0..3.  a_2CL = a^_2CL + P1 a_CL, a_3CL = a^_3CL + P2 a^_2CL + P2 P1 a_CL (a^: the chunk run from
+    // zero); chunk starts are even stages, so a_CL sits at index i (captured by wave 0 in rb).
     IMPC_WF void fwd_chunked(const double *tb, double *rb) {
         const double *C = lds + CH_OFF;
         double *ends = lds + CH_OFF + kChEnd;
         const int w = L >> 6, l = lane_o() & 63, i = l >> 3, j = l & 7;
+        constexpr int A1 = 13 * CL;  // a_CL in rb
         for (int rep_ = 0; rep_ < (IMPC_CHDUP == 1 ? 2 : 1); rep_++)
         if (w == 0) {
-            (void)fwd_run<10, true>(tb, rb, 0, 8.0 * tb[i]);  // a_0 = t_0 (tb holds t / 8)
+            (void)fwd_run<CL, true>(tb, rb, 0, 8.0 * tb[i]);  // a_0 = t_0 (tb holds t / 8)
         } else if (w == 1) {
-            const double e = fwd_run<10, false>(tb, rb, 10, 0.0);
+            const double e = fwd_run<CL, false>(tb, rb, CL, 0.0);
             if (j == 0) ends[i] = e;
         } else if (w == 2) {
-            const double e = fwd_run<10, false>(tb, rb, 20, 0.0);
+            const double e = fwd_run<CL, false>(tb, rb, 2 * CL, 0.0);
             if (j == 0) ends[8 + i] = e;
         }
         wv.lsync();
         for (int rep_ = 0; rep_ < (IMPC_CHDUP == 2 ? 2 : 1); rep_++)
         if (w == 1) {
-            (void)fwd_run<10, true>(tb, rb, 10, rb[130 + i]);
+            (void)fwd_run<CL, true>(tb, rb, CL, rb[A1 + i]);
         } else if (w == 2) {
-            const double a = wv.sum_contig8(__builtin_fma(C[kChFP1 + l], rb[130 + j], 0.125 * ends[i]));
-            (void)fwd_run<10, true>(tb, rb, 20, a);
+            const double a = wv.sum_contig8(__builtin_fma(C[kChFP1 + l], rb[A1 + j], 0.125 * ends[i]));
+            (void)fwd_run<CL, true>(tb, rb, 2 * CL, a);
         } else if (w == 3) {
             const double p = __builtin_fma(C[kChFP2 + l], ends[j],
-                                           __builtin_fma(C[kChFP21 + l], rb[130 + j], 0.125 * ends[8 + i]));
-            (void)fwd_run<9, true>(tb, rb, 30, wv.sum_contig8(p));
+                                           __builtin_fma(C[kChFP21 + l], rb[A1 + j], 0.125 * ends[8 + i]));
+            (void)fwd_run<CLAST, true>(tb, rb, 3 * CL, wv.sum_contig8(p));
         }
     }
 
-    // S4 in chunks: steps 38..30 / 29..20 / 19..10 / 9..0 on waves 0..3, from x_39 / x_30 / x_20 /
-    // x_10 (x_20 = x^_20 + P1 x_30, x_10 = x^_10 + P2 x^_20 + P2 P1 x_30).
+    // S4 in chunks: steps W-1..3CL / 3CL-1..2CL / 2CL-1..CL / CL-1..0 on waves 0..3, from x_W /
+    // x_3CL / x_2CL / x_CL (x_2CL = x^_2CL + P1 x_3CL, x_CL = x^_CL + P2 x^_2CL + P2 P1 x_3CL).
     IMPC_WF void bwd_chunked(const double *eb, double *xb) {
         const double *C = lds + CH_OFF;
         double *ends = lds + CH_OFF + kChEnd + 16;
         const int w = L >> 6, l = lane_o() & 63, i = l >> 3, j = l & 7;
+        constexpr int X3 = 13 * 3 * CL;     // x_3CL in xb (even stage: index i)
+        constexpr bool LODD = (WF - 1) & 1;  // parity of the last chunk's first step W - 1
         for (int rep_ = 0; rep_ < (IMPC_CHDUP == 1 ? 2 : 1); rep_++)
         if (w == 0) {
-            (void)bwd_run<false, 9, true>(eb, xb, 30, 8.0 * eb[13 * 39 + j]);  // x_39 (odd: index j)
+            // x_W = e_W: at index j for odd W, i for even W
+            (void)bwd_run<LODD, CLAST, true>(eb, xb, 3 * CL, 8.0 * eb[13 * WF + (LODD ? i : j)]);
         } else if (w == 1) {
-            const double e = bwd_run<true, 10, false>(eb, xb, 20, 0.0);
+            const double e = bwd_run<true, CL, false>(eb, xb, 2 * CL, 0.0);
             if (j == 0) ends[i] = e;
         } else if (w == 2) {
-            const double e = bwd_run<true, 10, false>(eb, xb, 10, 0.0);
+            const double e = bwd_run<true, CL, false>(eb, xb, CL, 0.0);
             if (j == 0) ends[8 + i] = e;
         }
         wv.lsync();
         for (int rep_ = 0; rep_ < (IMPC_CHDUP == 2 ? 2 : 1); rep_++)
         if (w == 1) {
-            (void)bwd_run<true, 10, true>(eb, xb, 20, xb[390 + i]);
+            (void)bwd_run<true, CL, true>(eb, xb, 2 * CL, xb[X3 + i]);
         } else if (w == 2) {
-            const double x = wv.sum_contig8(__builtin_fma(C[kChBT1 + l], xb[390 + j], 0.125 * ends[i]));
-            (void)bwd_run<true, 10, true>(eb, xb, 10, x);
+            const double x = wv.sum_contig8(__builtin_fma(C[kChBT1 + l], xb[X3 + j], 0.125 * ends[i]));
+            (void)bwd_run<true, CL, true>(eb, xb, CL, x);
         } else if (w == 3) {
             const double p = __builtin_fma(C[kChBT2 + l], ends[j],
-                                           __builtin_fma(C[kChBT21 + l], xb[390 + j], 0.125 * ends[8 + i]));
-            (void)bwd_run<true, 10, true>(eb, xb, 0, wv.sum_contig8(p));
+                                           __builtin_fma(C[kChBT21 + l], xb[X3 + j], 0.125 * ends[8 + i]));
+            (void)bwd_run<true, CL, true>(eb, xb, 0, wv.sum_contig8(p));
         }
     }
 

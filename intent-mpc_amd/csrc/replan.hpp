@@ -62,3 +62,54 @@ extern "C" int impc_replan_commit_device(impc_ctx ctx, int32_t horizon, int64_t 
     HIP_OK(hipGetLastError());
     return ctx_note_launch(ctx, st);
 }
+
+// ---- a receding window's next initial state from the last solve (impc_batch_follow_plan_device)
+namespace impc_replan_k {
+// mpcPlanner::getPos / getVel (mpcPlanner.cpp:1257-1290) on QP b's own solution, for the QPs
+// whose solve returned one; pos / vel [B][3] updated in place
+__global__ void k_follow(int64_t B, int32_t N, int64_t n, double ts, double t, const double *__restrict__ x,
+                         const impc_info *__restrict__ info, double *__restrict__ pos, double *__restrict__ vel) {
+    for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < B; b += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t st = info[b].status_val;
+        if (st != IMPC_SOLVED && st != IMPC_SOLVED_INACCURATE && st != IMPC_MAX_ITER_REACHED &&
+            st != IMPC_TIME_LIMIT_REACHED)
+            continue;
+        int idx = (int)floor(t / ts);
+        const double dt = t - idx * ts;
+        idx = max(0, min(idx, N - 1));
+        const int nxt = min(idx + 1, N - 1);
+        const double *s = x + b * n + 8 * idx, *e = x + b * n + 8 * nxt;
+        for (int c = 0; c < 3; c++) {
+            pos[3 * b + c] = s[c] + (e[c] - s[c]) / ts * dt;
+            vel[3 * b + c] = s[3 + c] + (e[3 + c] - s[3 + c]) / ts * dt;
+        }
+    }
+}
+}  // namespace impc_replan_k
+
+extern "C" int impc_batch_follow_plan_device(impc_batch b, int32_t horizon, double ts, double t, double *pos,
+                                             double *vel) {
+    if (!b || horizon < 2 || b->n != 13 * (int64_t)horizon - 5 || !(ts > 0.0) || !(t >= 0.0) || !pos || !vel)
+        return fail(IMPC_INVALID_ARGUMENT, "follow plan: an mpcPlanner batch (n = 13 horizon - 5), ts > 0, t >= 0");
+    HIP_OK(hipSetDevice(b->ctx->device));
+    hipStream_t st = b->ctx->stream;
+    IMPC_TRY(ctx_order_after_all(b->ctx, st));  // after the solve, wherever it ran
+    const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((b->Bact + 255) / 256, 4096));
+    hipLaunchKernelGGL(impc_replan_k::k_follow, dim3(blocks), dim3(256), 0, st, b->Bact, horizon, b->n, ts, t, b->d_xout,
+                       b->d_info, pos, vel);
+    HIP_OK(hipGetLastError());
+    return IMPC_OK;
+}
+
+extern "C" int impc_copy_rows_device(impc_ctx ctx, void *dst, int64_t dpitch, const void *src, int64_t spitch,
+                                     int64_t width, int64_t rows, void *stream) {
+    if (!ctx || rows < 0 || width < 0 || (rows && width && (!dst || !src || dpitch < width || spitch < width)))
+        return fail(IMPC_INVALID_ARGUMENT, "copy rows: pitches >= width");
+    if (!rows || !width) return IMPC_OK;
+    HIP_OK(hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    IMPC_TRY(ctx_order_launch(ctx, st));
+    HIP_OK(hipMemcpy2DAsync(dst, (size_t)dpitch, src, (size_t)spitch, (size_t)width, (size_t)rows,
+                            hipMemcpyDeviceToDevice, st));
+    return ctx_note_launch(ctx, st);
+}

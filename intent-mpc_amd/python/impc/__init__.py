@@ -142,6 +142,8 @@ _sig("impc_copy_to_device", C.c_int, _P, _P, _P, C.c_int64)
 _sig("impc_copy_to_host", C.c_int, _P, _P, _P, C.c_int64)
 _sig("impc_reference_traj_device", C.c_int, _P, C.c_int32, C.c_double, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P)
 _sig("impc_repeat_rows_device", C.c_int, _P, _P, C.c_int64, C.c_int64, C.c_int32, _P, _P)
+_sig("impc_copy_rows_device", C.c_int, _P, _P, C.c_int64, _P, C.c_int64, C.c_int64, C.c_int64, _P)
+_sig("impc_batch_follow_plan_device", C.c_int, _P, C.c_int32, C.c_double, C.c_double, _P, _P)
 # include/impc_comm.h
 COMM_ID_BYTES = 128
 _sig("impc_comm_unique_id", C.c_int, C.POINTER(C.c_ubyte))
@@ -257,7 +259,8 @@ EXPORTED = [
     "impc_stream_wait", "impc_stream_synchronize", "impc_batch_set_values_async", "impc_batch_get_async",
     "impc_batch_update_lin_cost_device", "impc_batch_update_bounds_device", "impc_ctx_pool_stats",
     "impc_replan_create", "impc_replan_destroy", "impc_replan_set_state", "impc_replan_run", "impc_replan_get_stats",
-    "impc_replan_view_device", "impc_replan_shape", "impc_replan_advance_device",
+    "impc_replan_view_device", "impc_replan_shape", "impc_replan_advance_device", "impc_batch_follow_plan_device",
+    "impc_copy_rows_device",
 ]
 
 
@@ -463,6 +466,12 @@ class Batch:
             raise ValueError(f"update_bounds: l / u have {la.size} / {ua.size} values, expected B*m = "
                              f"{self.B * self.m}")
         _check(lib.impc_batch_update_bounds(self.h, _d(la), _d(ua)), "impc_batch_update_bounds")
+
+    def follow_plan_device(self, horizon, ts, t, pos_ptr, vel_ptr):
+        """impc_batch_follow_plan_device: pos / vel [B][3] (device) = getPos(t) / getVel(t) of each
+        QP's own last solution (QPs with a solution)."""
+        _check(lib.impc_batch_follow_plan_device(self.h, int(horizon), float(ts), float(t), _P(pos_ptr), _P(vel_ptr)),
+               "impc_batch_follow_plan_device")
 
     def update_lin_cost_device(self, q_ptr):
         """impc_batch_update_lin_cost_device: q [B][n] in device memory (address)."""
@@ -773,6 +782,12 @@ def repeat_rows_device(ctx, src_ptr, rows, row_bytes, repeat, dst_ptr, stream=No
     """impc_repeat_rows_device: dst row r * repeat + c = src row r (device pointers)."""
     _check(lib.impc_repeat_rows_device(ctx.h, _P(src_ptr), int(rows), int(row_bytes), int(repeat), _P(dst_ptr),
                                        _P(stream) if stream else None), "impc_repeat_rows_device")
+
+
+def copy_rows_device(ctx, dst_ptr, dpitch, src_ptr, spitch, width, rows, stream=None):
+    """impc_copy_rows_device: rows x width bytes, strided, device to device."""
+    _check(lib.impc_copy_rows_device(ctx.h, _P(dst_ptr), int(dpitch), _P(src_ptr), int(spitch), int(width), int(rows),
+                                     _P(stream) if stream else None), "impc_copy_rows_device")
 
 
 def gather_rows_device(ctx, src_ptr, row_bytes, idx_ptr, count, dst_ptr, stream=None):

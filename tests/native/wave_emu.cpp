@@ -132,13 +132,16 @@ void run_w(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSet
     for (auto &t : th) t.join();
 }
 
-// the product's dispatch: the default-horizon specialisation when W matches (impc_qp.hip launch_wave)
+// the product's dispatch: a compile-time horizon instance when W matches one (impc_qp.hip
+// launch_group: WSPEC, or the long shape's WSPEC2)
 template <int VS, int GS>
 void run(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSettings &st) {
-    constexpr int WS = impc::WaveLds<NL, VS, GS>::WSPEC;
+    constexpr int WS = impc::WaveLds<NL, VS, GS>::WSPEC, WS2 = impc::WaveLds<NL, VS, GS>::WSPEC2;
     const bool tier = T.T1r < impc::WaveLds<NL, VS, GS>::cg4(T.CG);
     if (T.W == WS)
         tier ? run_w<VS, GS, WS, true>(T, io, st) : run_w<VS, GS, WS, false>(T, io, st);
+    else if (WS2 && T.W == WS2)
+        tier ? run_w<VS, GS, WS2, true>(T, io, st) : run_w<VS, GS, WS2, false>(T, io, st);
     else
         tier ? run_w<VS, GS, 0, true>(T, io, st) : run_w<VS, GS, 0, false>(T, io, st);
 }

@@ -240,3 +240,120 @@ def test_two_rank_config3_strong_split_matches_whole_batch():
         o, it, K = whole[(int(row[1]), int(row[2]))]
         assert row[3] == o and row[5] == it and row[6] == K
         assert row[0] == (0 if row[1] < 2 else 1)
+
+
+def _closed_loop_oracle(bks, steps, s):
+    """bench.py --workload config5's closed receding window (RecedingLoop) restated on the CPU for
+    a rank's buckets: oracle persistent workspaces; per step each QP's x0 = state 1 of its own last
+    solution (when it has one, impc_batch_follow_plan_device), the reference and the predicted
+    obstacles one step on, q / l / u from the host builder with the setup's linearisation point,
+    update_lin_cost + update_bounds + solve.  Returns per step the (inst, hyp, obj, status, iter)
+    rows of every QP."""
+    import impc
+    from oracle import osqp_oracle as ora
+    out = [[] for _ in range(steps)]
+    so = ora.settings_from(s)
+    for bk in bks:
+        N, K = bk["N"], bk["K"]
+        d, inst = bk["instances"], bk["inst"]
+        xref, prev = d["xref"][inst], d["prev"][inst]
+        p, _ = impc.mpc_params(horizon=N)
+        T = steps + 1
+        step = xref[:, -1, :] - xref[:, -2, :]
+        path = np.concatenate([xref, xref[:, -1:, :] + step[:, None, :] * np.arange(1, T + 1)[None, :, None]], axis=1)
+        dpx = np.concatenate([bk["dyn_pos"], np.repeat(bk["dyn_pos"][:, :, -1:], T, axis=2)], axis=2)
+        dsx = np.concatenate([bk["dyn_size"], np.repeat(bk["dyn_size"][:, :, -1:], T, axis=2)], axis=2)
+        L = bk["dyn_pos"].shape[2]
+        v = bk["values"]
+        pos, vel = d["pos"][inst].copy(), d["vel"][inst].copy()
+        ws, sol = [], []
+        for i in range(inst.size):
+            w = ora.Workspace(bk["pattern"], v["Px"][i], v["q"][i], v["Ax"][i], v["l"][i], v["u"][i], so)
+            w.warm_start(bk["x_ws"][i], np.zeros(int(bk["pattern"]["m"])))
+            sol.append(w.solve())
+            ws.append(w)
+        for t in range(1, steps + 1):
+            for i, (x, _, info) in enumerate(sol):
+                if int(info["status_val"]) in (1, 2, -2, -6):
+                    pos[i], vel[i] = x[8:11], x[11:14]
+            vals = impc.mpc_values(p, pos, vel, path[:, t:t + N], prev, dyn_pos=dpx[:, :, t:t + L],
+                                   dyn_size=dsx[:, :, t:t + L])
+            for i, w in enumerate(ws):
+                w.update_lin_cost(vals["q"][i])
+                w.update_bounds(vals["l"][i], vals["u"][i])
+                sol[i] = w.solve()
+                out[t - 1].append((bk.get("inst_global", bk["inst"])[i], bk["hyp"][i], sol[i][2]["obj_val"], sol[i][2]["status_val"],
+                                   sol[i][2]["iter"]))
+        for w in ws:
+            w.close()
+    return [np.array(r, dtype=np.float64).reshape(-1, 5) for r in out]
+
+
+def _config5_worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(WORLD))
+    try:
+        import sys
+        here = os.path.dirname(os.path.abspath(__file__))
+        sys.path[:0] = [here, os.path.dirname(here)]
+        import impc
+        from impc import scenarios
+        r, lr, w = D.env()
+        dist = D.init("gloo", lr)
+        # bench.py --workload config5's rank path at a small job: one fixed N = 40 scenario split by
+        # instance, per-rank persistent workspaces through the closed receding loop, and every
+        # step's cost records gathered (padded to the largest shard)
+        I, steps = 3, 2
+        full = scenarios.intent_config(N=40, K=10, instances=I, hyps=8, seed=5000)
+        bounds = D.equal_instance_bounds(I, w)
+        mine = scenarios.slice_instances(full, int(bounds[r]), int(bounds[r + 1]))
+        counts = [8 * int(bounds[k + 1] - bounds[k]) for k in range(w)]
+        s = impc.default_settings(verbose=0)
+        per_step = _closed_loop_oracle([bk for _, bk in sorted(mine.items())], steps, s)
+        gathered = []
+        for rec in per_step:
+            full_rec = np.zeros((rec.shape[0], 8))
+            full_rec[:, 0] = r
+            full_rec[:, 1:6] = rec
+            gathered.append(D.gather_costs(dist, full_rec, counts))
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((r, per_step, gathered, counts))
+    except Exception:  # surface the failure in the parent
+        import traceback
+        q.put((rank, traceback.format_exc(), None, None))
+
+
+def test_two_rank_config5_closed_loop_split_matches_whole_batch():
+    """configs[4]'s multi-GPU path rehearsed on two gloo ranks: the N = 40 instances split by
+    instance, each rank's persistent workspaces stepping the closed receding window (x0 from its
+    own solutions, reference and obstacles moving on), every step's cost records gathered to every
+    rank -- equal, step by step, to the whole batch stepped in one process."""
+    import impc
+    from impc import scenarios
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_config5_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(WORLD):
+        r, per_step, gathered, counts = q.get(timeout=600)
+        assert gathered is not None, per_step
+        out[r] = (per_step, gathered, counts)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out[0][2] == [8, 16]
+    whole = _closed_loop_oracle([bk for _, bk in sorted(scenarios.intent_config(N=40, K=10, instances=3, hyps=8,
+                                                                                   seed=5000).items())],
+                                2, impc.default_settings(verbose=0))
+    for t in range(2):
+        g0, g1 = out[0][1][t], out[1][1][t]
+        np.testing.assert_array_equal(g0, g1)                       # every rank holds every record
+        assert g0.shape[0] == 24
+        ref = {(int(a[0]), int(a[1])): a[2:] for a in whole[t]}
+        for row in g0:
+            np.testing.assert_array_equal(row[3:6], ref[(int(row[1]), int(row[2]))])
+            assert row[0] == (0 if row[1] < 1 else 1)

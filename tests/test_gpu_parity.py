@@ -117,6 +117,39 @@ def test_long_horizon_chunked_recursions(ctx, K):
             assert ref[2]["rho_updates"].max() >= 1
 
 
+@pytest.mark.parametrize("rho", [0.1, 1e-3])
+def test_live_horizon_N30_intent_buckets(ctx, rho):
+    """N = 30, the reference's live planner horizon (planner_param.yaml:25): the long shape's
+    compile-time W = 29 instance (chunked recursions of 8 / 8 / 8 / 5 steps).  The K = 8 / 9
+    intent buckets of config 3's generator at N = 30, warm-started from the previous plan, in ONE
+    grouped launch, against the oracle; rho = 1e-3 forces refactorisations (chunk operators
+    rebuilt)."""
+    buckets = scenarios.intent_config(N=30, K=8, instances=24, hyps=8, seed=3030 if rho == 0.1 else 3031)
+    s = impc.default_settings(rho=rho, **S25)
+    bs = []
+    try:
+        for K, bk in sorted(buckets.items()):
+            pat, v = bk["pattern"], bk["values"]
+            b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], v["q"].shape[0])
+            b.set_settings(s)
+            b.set_values(v["Px"], v["q"], v["Ax"], v["l"], v["u"])
+            b.warm_start(bk["x_ws"], None)
+            st = b.stats()
+            assert st["kernel"] == impc.KERNEL_STRUCTURED and st["var_slots"] == 3, st
+            bs.append((b, bk))
+        impc.solve_group([b for b, _ in bs])
+        upd = 0
+        for b, bk in bs:
+            ref = oracle(bk, s)
+            compare(b.get(), ref)
+            upd += int(ref[2]["rho_updates"].max())
+        if rho < 0.1:
+            assert upd >= 1
+    finally:
+        for b, _ in bs:
+            b.close()
+
+
 def test_grouped_launch_equals_separate_solves(ctx):
     """impc_batch_solve_group over the K / K+1 buckets of a replan gives bitwise the results of
     separate impc_batch_solve calls (one work queue, per-batch tables)."""

@@ -92,6 +92,20 @@ def test_structured_emulation_long_horizon():
     compare(emulate(cfg, s), ref)
 
 
+def test_structured_emulation_live_horizon():
+    """N=30 (n=385, the reference's live planner horizon, planner_param.yaml:25): the three-slot
+    shape's W = 29 instance, chunked recursions of 8 / 8 / 8 / 5 steps, with adaptive-rho
+    refactorisations."""
+    cfg = take(scenarios.intent_config(N=30, K=8, instances=1, seed=3030)[8], 1)
+    s = impc.default_settings(**S25)
+    compare(emulate(cfg, s), oracle(cfg, s))
+    cfg = scenarios.static_config(N=30, K=9, batch=1, identical=False, seed=3031)
+    s = impc.default_settings(rho=1e-3, **S25)
+    ref = oracle(cfg, s)
+    assert ref[2]["rho_updates"].max() >= 1
+    compare(emulate(cfg, s), ref)
+
+
 @pytest.mark.parametrize("rho", [0.1, 1e-3])
 def test_structured_emulation_default_horizon_batch(rho):
     """The default-horizon (W = 19) instance of the structured kernel -- fully unrolled stage
