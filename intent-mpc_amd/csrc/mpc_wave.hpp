@@ -58,6 +58,12 @@ namespace impc {
 #ifndef IMPC_CHDUP
 #define IMPC_CHDUP 0
 #endif
+// A/B switch (tools/exp.sh variants only): IMPC_CHUNK19=1 runs the default horizon's (W = 19)
+// stage recursions in chunks too (the long shape's form, chunks of 6 / 6 / 6 / 1 steps), their
+// operators in an LDS region past the products (the one-slot shape's F region has no tail)
+#ifndef IMPC_CHUNK19
+#define IMPC_CHUNK19 0
+#endif
 #define IMPC_REP(X) for (int rep_ = 0; rep_ < (IMPC_DUP == (X) ? 2 : 1); rep_++)
 // Branch counters of the CPU emulation's instrumented builds (tools only; nothing in the product)
 #ifndef IMPC_COUNT
@@ -205,7 +211,10 @@ struct WaveLds {
         return c > f ? c : f;
     }
     static IMPC_WF int p_size(const WaveTables &T) { return p_size(T.CG, T.n, T.HS, T.mg, T.T1r); }
-    static IMPC_WF int size(const WaveTables &T) { return P_OFF + p_size(T) + 8; }
+    // the chunk operators' region of the one-slot shape (IMPC_CHUNK19), after the products
+    static constexpr int CHX = (VS == 1 && IMPC_CHUNK19) ? 448 : 0;
+    static IMPC_WF int ch_off(const WaveTables &T) { return P_OFF + p_size(T) + 8; }
+    static IMPC_WF int size(const WaveTables &T) { return P_OFF + p_size(T) + 8 + CHX; }
     // factorisation aliases (inside R..X region and the products buffer)
     static constexpr int FA = R_OFF, FL = FA + 169, FI = FL + 169, FB = FI + 169, FG = FB + 104, FE = FG + 104,
                          DIAGX = FE + 64;
@@ -344,12 +353,14 @@ struct WaveQP {
     // reduction and runs its chunk again.  Dependent chain per sweep: W steps -> 2 CL steps and one
     // reduction.  Operators and ends live in the F region's tail (blocks >= W + 3, never read).
     // CL is even, so every chunk starts on an even stage (the sweeps' index parity).
-    static constexpr bool CHUNK = WF > 0 && NL == 256 && VS == 3;
+    static constexpr bool CHUNK = WF > 0 && NL == 256 && (VS == 3 || (VS == 1 && IMPC_CHUNK19 != 0));
     static constexpr int CL = WF > 0 ? 2 * ((WF + 7) / 8) : 2;
     static constexpr int CLAST = WF - 3 * CL;
     static constexpr int CH_OFF = LD::F_OFF + 64 * (WF + 3);
     enum { kChFP1 = 0, kChFP2 = 64, kChFP21 = 128, kChBT1 = 192, kChBT2 = 256, kChBT21 = 320, kChEnd = 384 };
-    static_assert(!CHUNK || CH_OFF + kChEnd + 32 <= LD::R_OFF, "chunk operators do not fit the F region");
+    static_assert(!CHUNK || VS == 1 || CH_OFF + kChEnd + 32 <= LD::R_OFF, "chunk operators do not fit the F region");
+    static_assert(!CHUNK || VS != 1 || LD::CHX >= kChEnd + 32, "chunk operator region");
+    IMPC_WF double *chbuf() const { return lds + (VS == 1 ? LD::ch_off(T) : CH_OFF); }
     static_assert(!CHUNK || (CLAST >= 1 && CLAST <= CL), "chunk lengths");
 
     // zero the exchange vectors (their tails are the zero slots read by padded entries)
@@ -780,7 +791,7 @@ struct WaveQP {
     // two-chunk operators of the last chunk's start, P2 P1, forward and backward.
     IMPC_WF void chunk_ops() {
         const double *Fm = F();
-        double *C = lds + CH_OFF;
+        double *C = chbuf();
         const int w = L >> 6, l = L & 63, i = l >> 3, j = l & 7;
         const bool fwd = w < 2;
         const int o = (w == 0 || w == 3) ? CL : 2 * CL;
@@ -1024,8 +1035,8 @@ struct WaveQP {
     // 0..3.  a_2CL = a^_2CL + P1 a_CL, a_3CL = a^_3CL + P2 a^_2CL + P2 P1 a_CL (a^: the chunk run from
     // zero); chunk starts are even stages, so a_CL sits at index i (captured by wave 0 in rb).
     IMPC_WF void fwd_chunked(const double *tb, double *rb) {
-        const double *C = lds + CH_OFF;
-        double *ends = lds + CH_OFF + kChEnd;
+        const double *C = chbuf();
+        double *ends = chbuf() + kChEnd;
         const int w = L >> 6, l = lane_o() & 63, i = l >> 3, j = l & 7;
         constexpr int A1 = 13 * CL;  // a_CL in rb
         for (int rep_ = 0; rep_ < (IMPC_CHDUP == 1 ? 2 : 1); rep_++)
@@ -1055,8 +1066,8 @@ struct WaveQP {
     // S4 in chunks: steps W-1..3CL / 3CL-1..2CL / 2CL-1..CL / CL-1..0 on waves 0..3, from x_W /
     // x_3CL / x_2CL / x_CL (x_2CL = x^_2CL + P1 x_3CL, x_CL = x^_CL + P2 x^_2CL + P2 P1 x_3CL).
     IMPC_WF void bwd_chunked(const double *eb, double *xb) {
-        const double *C = lds + CH_OFF;
-        double *ends = lds + CH_OFF + kChEnd + 16;
+        const double *C = chbuf();
+        double *ends = chbuf() + kChEnd + 16;
         const int w = L >> 6, l = lane_o() & 63, i = l >> 3, j = l & 7;
         constexpr int X3 = 13 * 3 * CL;     // x_3CL in xb (even stage: index i)
         constexpr bool LODD = (WF - 1) & 1;  // parity of the last chunk's first step W - 1

@@ -274,12 +274,28 @@ class DeviceReplan:
         self.ctx.synchronize()
         t_run = time.perf_counter() - t1
         st = self.stats()
+        out = self.results(values, profile)
+        out["xref"] = xd.get() if xd is not None else np.asarray(xref, np.float64).reshape(I, N, 8)
+        if profile:
+            for b in [self.shape(k)[0] for k in range(4)]:
+                if b:
+                    _check(lib.impc_batch_set_profiling(_P(b), 0), "impc_batch_set_profiling")
+        for d in tmp:
+            d.free()
+        if timings is not None:
+            timings.update(upload_s=t_up, run_s=t_run, stage_s=st["stage_s"], call_s=st["total_s"])
+        return out
+
+    def results(self, values=True, profile=False):
+        """Host copies of the last replan's per-instance outputs, state and per-shape results
+        (test / tool inspection after the call)."""
+        I = self.I
+        st = self.stats()
         v = self.view()
         out = dict(branch=_get(self.ctx, v.branch, I, np.int8), best_cand=_get(self.ctx, v.best_cand, I, np.int32),
                    ob_idx=_get(self.ctx, v.ob_idx, I, np.int32), cand_type=_get(self.ctx, v.cand_type, (I, 6), np.int32),
                    cand_slot=_get(self.ctx, v.cand_slot, (I, 6), np.int32), valid=_get(self.ctx, v.valid, I, np.int8),
-                   issued=bool(st["issued"]), time_limit=st["time_limit"],
-                   xref=xd.get() if xd is not None else np.asarray(xref, np.float64).reshape(I, N, 8))
+                   issued=bool(st["issued"]), time_limit=st["time_limit"])
         br = out["branch"]
         out["inst_fanout"], out["inst_first"], out["inst_current"] = [np.flatnonzero(br == b) for b in
                                                                       (FANOUT, SINGLE_FIRST, SINGLE_CURRENT)]
@@ -294,15 +310,7 @@ class DeviceReplan:
                 _check(lib.impc_batch_get_qp_latency(_P(r["batch"]), ms.ctypes.data_as(C.POINTER(C.c_double))),
                        "impc_batch_get_qp_latency")
                 out["lat_" + nm] = ms[: r["x"].shape[0]]
-        if profile:
-            for b in [self.shape(k)[0] for k in range(4)]:
-                if b:
-                    _check(lib.impc_batch_set_profiling(_P(b), 0), "impc_batch_set_profiling")
         self.first_time_h = _get(self.ctx, v.first_time, I, np.int8)
-        for d in tmp:
-            d.free()
-        if timings is not None:
-            timings.update(upload_s=t_up, run_s=t_run, stage_s=st["stage_s"], call_s=st["total_s"])
         return out
 
     def close(self):

@@ -8,6 +8,7 @@ derives from dynus_obstacles_node.cpp:74-133 and the predictor's 4-intent models
 (dynamicPredictor.cpp:351-501: FORWARD / LEFT / RIGHT / STOP at 0.1 s steps).
 """
 import math
+import os
 
 import numpy as np
 
@@ -309,3 +310,60 @@ def receding_update(bk, shift=1, params=None):
     p, _ = params if params is not None else mpc_params(horizon=N)
     return mpc_values(p, prev[:, shift, 0:3], prev[:, shift, 3:6], xr2, prev, dyn_pos=bk["dyn_pos"],
                       dyn_size=bk["dyn_size"])
+
+
+# ------------------------------------------------------------------ the live replan loop
+# The reference's predefined benchmark path (autonomous_flight/cfg/mpc_navigation/
+# ref_trajectory_dynus_benchmark.txt: "t x y z" per line, read by mpcNavigation::getRefTraj,
+# mpcNavigation.cpp:189-218, and handed to updatePath(path, 0.1) as is, :227-236), kept as a data
+# fixture so no run reads /root/reference.
+DYNUS_PATH_FILE = os.path.join(os.path.dirname(__file__), "..", "..", "..", "tests", "golden",
+                               "ref_trajectory_dynus_benchmark.txt")
+
+
+def dynus_path():
+    """[P][3] points of the reference's benchmark path (the t column dropped, as getRefTraj does)."""
+    rows = []
+    with open(DYNUS_PATH_FILE) as f:
+        for ln in f:
+            parts = ln.split()
+            if len(parts) < 4:
+                break
+            rows.append([float(parts[1]), float(parts[2]), float(parts[3])])
+    return np.array(rows)
+
+
+def live_loop(instances, K, replans, N=30, seed=4100, params=None):
+    """R chained replans of I planning instances flying the reference's benchmark path, each
+    instance's copy of the path shifted sideways / up by a seeded offset, K dynamic obstacles per
+    instance crossing it at constant velocity (re-predicted every 0.1 s replan by the predictor's
+    four kinematic intent models, predict_intents), constant intent probabilities per obstacle.
+    The vehicle starts at rest at its path's first point on its first plan (firstTime_).
+    Returns dict(paths [I][P][3], pos0 / vel0 [I][3], pred_pos [R][I][K][4][L][3] (the predictions
+    handed to replan r), pred_size [I][K][4][L][3], prob [I][K][4], dyn_cur [R][I][K][3], size,
+    params, pd, N, K, L)."""
+    p, pd = params if params is not None else mpc_params(horizon=N)
+    rng = np.random.default_rng(seed)
+    I, ts = instances, pd["ts"]
+    base = dynus_path()
+    off = np.stack([np.zeros(I), rng.uniform(-1.5, 1.5, I), rng.uniform(-0.5, 0.5, I)], axis=1)
+    paths = base[None, :, :] + off[:, None, :]
+    pos0 = paths[:, 0, :].copy()
+    vel0 = np.zeros((I, 3))
+    # obstacles: ahead along x, 4-9 m to the side of the path, drifting across it or along it
+    side = np.where(rng.uniform(size=(I, K)) < 0.5, -1.0, 1.0)
+    obp = np.stack([pos0[:, None, 0] + rng.uniform(8, 60, (I, K)),
+                    pos0[:, None, 1] + side * rng.uniform(4, 9, (I, K)),
+                    pos0[:, None, 2] + rng.uniform(-0.3, 0.3, (I, K))], axis=2)
+    spd = rng.uniform(0.2, 1.0, (I, K))
+    hdg = np.where(side < 0, 0.5 * math.pi, -0.5 * math.pi) + rng.uniform(-1.0, 1.0, (I, K))
+    obv = np.stack([spd * np.cos(hdg), spd * np.sin(hdg), np.zeros((I, K))], axis=2)
+    prob = rng.dirichlet(np.full(4, 2.0), size=(I, K))
+    L = PRED_STEPS + 1
+    pred = np.empty((replans, I, K, 4, L, 3))
+    for r in range(replans):
+        pred[r] = predict_intents(obp + obv * (r * ts), obv, ts=ts)
+    size = np.full(3, 0.8)
+    pred_size = np.ascontiguousarray(np.broadcast_to(size, (I, K, 4, L, 3)))
+    return dict(paths=paths, pos0=pos0, vel0=vel0, pred_pos=pred, pred_size=pred_size, prob=prob,
+                dyn_cur=np.ascontiguousarray(pred[:, :, :, FORWARD, 0, :]), size=size, params=p, pd=pd, N=N, K=K, L=L)

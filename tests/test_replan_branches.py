@@ -63,7 +63,7 @@ def test_oracle_chain_first_plan_then_fanout():
 
 def _check_replan(out, before, pos, vel, xref, dyn_cur, pred, pred_size, prob, has_pred, cur_size, cur_count, pd, s):
     plan_x, first, _, _ = before
-    for i in range(I):
+    for i in range(len(out["branch"])):
         assert out["branch"][i] == ref.branch(first[i], has_pred[i], cur_count[i]), i
     expect = plan_x.copy()
     expect_first = first.copy()
