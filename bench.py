@@ -275,6 +275,9 @@ def main():
     ap.add_argument("--e2e-steps", type=int, default=4,
                     help="end-to-end steps after the timed region: host arrays in -> solve -> results on the host")
     ap.add_argument("--no-allgather", action="store_true")
+    ap.add_argument("--receding-replay", type=int, default=1,
+                    help="config5: the untimed replay after the timed steps (per-step stats, CPU baseline, parity); "
+                         "0 for profiler passes that must see only the timed launches")
     ap.add_argument("--full-values", action="store_true",
                     help="ship every QP's full CSC values (default: shared P / dynamics / box values, "
                          "per-QP obstacle rows, impc_batch_set_values_shared)")
@@ -444,7 +447,7 @@ def main():
 
     cpu = parity = None
     per_step = None
-    if receding is not None:
+    if receding is not None and args.receding_replay:
         # untimed replay of the same closed loop (the device is deterministic: its last step must
         # equal the timed run's bit for bit), recording every step's iterations / statuses and the
         # CPU sample's per-step q, l, u for the oracle
@@ -777,17 +780,18 @@ def measured_traffic(build_id, qps, kernel, values_mode, workload):
     """HBM bytes per launch from the committed PMC summary (tools/pmc_summary.py), only when it was
     measured on this very library (its build_id equals impc_build_id()) and this workload; else
     (None, reason)."""
-    path = os.path.join(ROOT, "profiles", "pmc_k_solve.json")
+    name = "pmc_k_solve.json" if workload == "config3" else f"pmc_{workload}.json"
+    path = os.path.join(ROOT, "profiles", name)
     try:
         pm = json.load(open(path))
     except (OSError, ValueError):
-        return None, "no PMC summary (profiles/pmc_k_solve.json)"
+        return None, f"no PMC summary (profiles/{name})"
     if pm.get("build_id") != build_id:
         return None, f"PMC summary is of build {pm.get('build_id')}, not the loaded library {build_id}"
     if pm.get("qps_per_launch") != qps or pm.get("kernel") != kernel or pm.get("values", "full") != values_mode or \
             pm.get("workload", "config3") != workload:
         return None, "PMC summary is of another workload / kernel / value mode"
-    return pm.get("hbm_bytes_per_launch"), f"profiles/pmc_k_solve.json (build {build_id}, {pm.get('source', '')})"
+    return pm.get("hbm_bytes_per_launch"), f"profiles/{name} (build {build_id}, {pm.get('source', '')})"
 
 
 def parity_vs_oracle(results, ref):

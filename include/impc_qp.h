@@ -214,6 +214,14 @@ int impc_batch_update_bounds(impc_batch b, const double *l, const double *u);
  * receding-horizon loop builds the next step's values on the device). */
 int impc_batch_update_lin_cost_device(impc_batch b, const double *q);
 int impc_batch_update_bounds_device(impc_batch b, const double *l, const double *u);
+/* osqp_update_P / osqp_update_A / osqp_update_P_A (osqp.h:137-156, OsqpEigen Solver.tpp:15-212) on
+ * a persistent structured workspace: new values of P and / or A (host, QP-major [B][nnzP] /
+ * [B][nnzA], same patterns; NULL = unchanged).  As OSQP 0.6.2 does (unscale_data, the new values,
+ * scale_data, update_matrices), the next solve runs the Ruiz scaling afresh on the new data,
+ * refactors with the kept rho and continues from the kept SCALED iterates (x, z, y are not
+ * rescaled).  The generic kernel has no in-place form (IMPC_UNSUPPORTED: set the values again and
+ * warm start). */
+int impc_batch_update_matrices(impc_batch b, const double *Px, const double *Ax);
 
 /* Kernel selection.  AUTO picks the one-QP-per-wavefront structured kernel when the pattern is
  * the stage-structured mpcPlanner QP and fits its register layout, else the

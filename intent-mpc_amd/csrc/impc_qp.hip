@@ -589,6 +589,7 @@ struct impc_batch_s {
     // persistent workspace of the structured kernel (impc_batch_set_persistent)
     double *d_persist = nullptr;
     bool persist_on = false, persist_valid = false, q_by_update = false;
+    bool rescale = false;  // new P / A values on a persistent workspace (impc_batch_update_matrices)
     bool qpt_valid = false;
     // shared-structure values (impc_batch_set_values_shared)
     bool shared = false, shared_expanded = false;
@@ -711,7 +712,7 @@ impc::WaveIO wave_io(impc_batch b) {
     if (b->tlim_on) io.tlim = b->d_tlim;
     if (b->persist_on && b->d_persist) {
         io.persist = b->d_persist;
-        io.resume = b->persist_valid ? 1 : 0;
+        io.resume = b->persist_valid ? (b->rescale ? 2 : 1) : 0;
         io.q_updated = b->q_by_update ? 1 : 0;
     }
     b->qpt_valid = io.qpt != nullptr;
@@ -1018,6 +1019,7 @@ int with_shape(int vs, int gs, bool tier, F &&f) {
 void structured_solved(impc_batch b) {
     if (!b->persist_on) return;
     b->persist_valid = true;
+    b->rescale = false;
     b->has_ws = false;
 }
 
@@ -1202,7 +1204,7 @@ void reset_batch(impc_batch b) {
     b->dst.tick_s = b->ctx->tick_s;
     b->kernel_req = IMPC_KERNEL_AUTO;
     b->values_set = b->has_ws = b->ws_y = b->tlim_on = false;
-    b->persist_on = b->persist_valid = b->q_by_update = false;
+    b->persist_on = b->persist_valid = b->q_by_update = b->rescale = false;
     b->profile = b->qpt_valid = b->ev_setup = b->ev_solve = false;
     b->queue_mode = IMPC_QUEUE_FIFO;
     b->queue_qw = 0.0;
@@ -1478,7 +1480,7 @@ int impc_batch_set_settings(impc_batch b, const impc_settings *s) {
         return fail(IMPC_UNSUPPORTED, "persistent workspaces support scaling <= 20 Ruiz passes");
     if (s->rho != b->settings.rho || s->sigma != b->settings.sigma || s->scaling != b->settings.scaling) {
         b->generic_dirty = true;
-        b->persist_valid = b->q_by_update = false;  // a different setup: the next solve starts over
+        b->persist_valid = b->q_by_update = b->rescale = false;  // a different setup: the next solve starts over
     }
     b->settings = *s;
     b->dst = d;
@@ -1515,7 +1517,7 @@ int impc_batch_set_values(impc_batch b, const double *Px, const double *q, const
         }
         b->in_dirty = true;  // uploaded with the warm start by the next call that needs them (flush_staged)
         b->shared = false;
-        b->persist_valid = b->q_by_update = false;
+        b->persist_valid = b->q_by_update = b->rescale = false;
         b->values_set = true;
         b->generic_dirty = true;
         return IMPC_OK;
@@ -1529,7 +1531,7 @@ int impc_batch_set_values(impc_batch b, const double *Px, const double *q, const
         IMPC_TRY(h2d_sync(b->ctx->stream, b->in_u, u, sizeof(double) * b->m * B));
     }
     b->shared = false;
-    b->persist_valid = b->q_by_update = false;  // new data: the next solve sets up from scratch
+    b->persist_valid = b->q_by_update = b->rescale = false;  // new data: the next solve sets up from scratch
     b->values_set = true;
     b->generic_dirty = true;
     return IMPC_OK;
@@ -1583,7 +1585,7 @@ int impc_batch_set_values_shared(impc_batch b, const double *Px, const double *A
     b->nvar = nvar;
     b->shared = true;
     b->shared_expanded = false;
-    b->persist_valid = b->q_by_update = false;
+    b->persist_valid = b->q_by_update = b->rescale = false;
     b->values_set = true;
     b->generic_dirty = true;
     return IMPC_OK;
@@ -1607,7 +1609,7 @@ int impc_batch_set_values_device(impc_batch b, const double *Px, const double *q
         HIP_OK(hipMemcpyAsync(b->in_u, u, sizeof(double) * b->m * B, hipMemcpyDeviceToDevice, st));
     }
     b->shared = false;
-    b->persist_valid = b->q_by_update = false;  // new data: the next solve sets up from scratch
+    b->persist_valid = b->q_by_update = b->rescale = false;  // new data: the next solve sets up from scratch
     b->values_set = true;
     b->generic_dirty = true;
     return IMPC_OK;
@@ -1683,7 +1685,7 @@ int impc_batch_set_values_async(impc_batch b, const double *Ax_var, const double
     b->ws_y = false;
     if (x_ws) b->settings.warm_start = b->dst.warm_start = 1;
     b->shared_expanded = false;
-    b->persist_valid = b->q_by_update = false;
+    b->persist_valid = b->q_by_update = b->rescale = false;
     b->values_set = true;
     b->generic_dirty = true;
     return IMPC_OK;
@@ -1735,7 +1737,7 @@ int impc_batch_set_active(impc_batch b, int64_t count) {
     if (count < 1 || count > b->B) return fail(IMPC_INVALID_ARGUMENT, "active count must be in [1, B]");
     if (count != b->Bact) {
         b->Bact = count;
-        b->persist_valid = b->q_by_update = false;  // the stored workspaces cover other QPs
+        b->persist_valid = b->q_by_update = b->rescale = false;  // the stored workspaces cover other QPs
         b->generic_dirty = true;
     }
     return IMPC_OK;
@@ -2046,6 +2048,32 @@ int impc_batch_update_bounds_device(impc_batch b, const double *l, const double 
     return IMPC_OK;
 }
 
+int impc_batch_update_matrices(impc_batch b, const double *Px, const double *Ax) {
+    if (!b || (!Px && !Ax)) return fail(IMPC_INVALID_ARGUMENT, "null batch, or neither P nor A values");
+    IMPC_TRY(flush_staged(b));
+    if (!use_structured(b))
+        return fail(IMPC_UNSUPPORTED, "generic kernel: no in-place matrix update (impc_batch_set_values + warm start)");
+    if (!b->persist_on || !b->persist_valid)
+        return fail(IMPC_WORKSPACE_NOT_INIT_ERROR,
+                    "structured kernel: impc_batch_set_persistent(b, 1) and one solve before updates");
+    HIP_OK(hipSetDevice(b->ctx->device));
+    IMPC_TRY(ctx_quiesce(b->ctx));  // no launch in flight reads the arrays replaced below
+    hipStream_t st = b->ctx->stream;
+    if (b->shared) {  // the kept half of the values into the per-QP arrays first
+        const int64_t tot = b->B * (b->nnzP + b->nnzA);
+        const int64_t blocks = std::min<int64_t>((tot + 255) / 256, (int64_t)b->ctx->num_cu * 16);
+        hipLaunchKernelGGL(k_expand_shared, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, st, b->d_shPx,
+                           b->d_shAx, b->d_vmap, b->d_Axv, b->nvar, b->nnzP, b->nnzA, b->B, b->in_Px, b->in_Ax);
+        HIP_OK(hipGetLastError());
+        b->shared = false;
+    }
+    if (Px && b->nnzP) IMPC_TRY(h2d_sync(st, b->in_Px, Px, sizeof(double) * b->nnzP * b->B));
+    if (Ax && b->nnzA) IMPC_TRY(h2d_sync(st, b->in_Ax, Ax, sizeof(double) * b->nnzA * b->B));
+    b->rescale = true;
+    b->generic_dirty = true;
+    return IMPC_OK;
+}
+
 int impc_batch_get_stats(impc_batch b, impc_batch_stats *out) {
     if (!b || !out) return fail(IMPC_INVALID_ARGUMENT, "null argument");
     std::memset(out, 0, sizeof(*out));
@@ -2097,7 +2125,7 @@ int impc_batch_set_persistent(impc_batch b, int on) {
         b->device_bytes += (int64_t)bytes;
     }
     b->persist_on = on != 0;
-    b->persist_valid = b->q_by_update = false;  // the next solve sets up from scratch
+    b->persist_valid = b->q_by_update = b->rescale = false;  // the next solve sets up from scratch
     return IMPC_OK;
 }
 
@@ -2359,7 +2387,7 @@ int batch_inputs_view(impc_batch b, BatchInputs *out) {
 int batch_inputs_end(impc_batch b, bool warm_x) {
     if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
     b->shared = false;
-    b->persist_valid = b->q_by_update = false;  // new data: the next solve sets up from scratch
+    b->persist_valid = b->q_by_update = b->rescale = false;  // new data: the next solve sets up from scratch
     b->values_set = true;
     b->generic_dirty = true;
     b->has_ws = warm_x;

@@ -117,7 +117,9 @@ struct WaveIO {
     const double *Ax_var = nullptr;
     // persistent workspace (impc_batch_set_persistent, OSQP's workspace between solves): per QP
     // [kPersistHdr + 3 n + 2 mg]: cost-scaling factors of the Ruiz passes, rho, then the scaled
-    // iterates x, z (box), y (box), z (general), y (general).  resume = 1: scale with the stored
+    // iterates x, z (box), y (box), z (general), y (general).  resume = 2 (osqp_update_P / _A: new
+    // matrix values): Ruiz scaling afresh on the new data, the stored rho and scaled iterates kept, as
+    // OSQP 0.6.2 unscales, rescales and refactors but keeps work->x, z, y.  resume = 1: scale with the stored
     // factors (the same D, E, c and scaled P, A as the first setup), start from the stored rho and
     // iterates, and -- when q_updated -- scale q as osqp_update_lin_cost does ((D q) c).
     double *persist = nullptr;
@@ -593,7 +595,7 @@ struct WaveQP {
             ct = ct > kMaxScaling ? kMaxScaling : ct;
             ct = 1. / ct;
             if (ps) {
-                if (io.resume)
+                if (io.resume == 1)  // replay; resume 2 (new P / A: osqp_update_P / _A) scales afresh
                     ct = ps[it];
                 else if (L == 0)
                     ps[it] = ct;
@@ -1558,7 +1560,7 @@ struct WaveQP {
         {
             double D[VS], Eb[VS], Eg[GS];
             scale(b, D, Eb, Eg, ps);
-            if (ps && io.resume && io.q_updated)  // osqp_update_lin_cost: q = c (D q)
+            if (ps && io.resume == 1 && io.q_updated)  // osqp_update_lin_cost: q = c (D q)
                 _Pragma("unroll") for (int s = 0; s < VS; s++)
                     if (vok[s]) q[s] = (D[s] * io.q[b * n + T.var_orig[NL * s + L]]) * c;
         }

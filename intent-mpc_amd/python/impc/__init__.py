@@ -128,6 +128,7 @@ _sig("impc_batch_update_lin_cost", C.c_int, _P, _dp)
 _sig("impc_batch_update_bounds", C.c_int, _P, _dp, _dp)
 _sig("impc_batch_update_lin_cost_device", C.c_int, _P, _P)
 _sig("impc_batch_update_bounds_device", C.c_int, _P, _P, _P)
+_sig("impc_batch_update_matrices", C.c_int, _P, _dp, _dp)
 _sig("impc_batch_get_stats", C.c_int, _P, C.POINTER(Stats))
 _sig("impc_batch_get_perm", C.c_int, _P, _i64p)
 _sig("impc_batch_set_profiling", C.c_int, _P, C.c_int)
@@ -260,7 +261,7 @@ EXPORTED = [
     "impc_batch_update_lin_cost_device", "impc_batch_update_bounds_device", "impc_ctx_pool_stats",
     "impc_replan_create", "impc_replan_destroy", "impc_replan_set_state", "impc_replan_run", "impc_replan_get_stats",
     "impc_replan_view_device", "impc_replan_shape", "impc_replan_advance_device", "impc_batch_follow_plan_device",
-    "impc_copy_rows_device",
+    "impc_copy_rows_device", "impc_batch_update_matrices",
 ]
 
 
@@ -472,6 +473,16 @@ class Batch:
         QP's own last solution (QPs with a solution)."""
         _check(lib.impc_batch_follow_plan_device(self.h, int(horizon), float(ts), float(t), _P(pos_ptr), _P(vel_ptr)),
                "impc_batch_follow_plan_device")
+
+    def update_matrices(self, Px=None, Ax=None):
+        """impc_batch_update_matrices: new P / A values [B][nnz] (host; None = unchanged)."""
+        P = None if Px is None else np.ascontiguousarray(Px, np.float64)
+        A = None if Ax is None else np.ascontiguousarray(Ax, np.float64)
+        if P is not None and P.size != self.B * self.nnzP:
+            raise ValueError("update_matrices: Px must be [B][nnzP]")
+        if A is not None and A.size != self.B * self.nnzA:
+            raise ValueError("update_matrices: Ax must be [B][nnzA]")
+        _check(lib.impc_batch_update_matrices(self.h, _d(P), _d(A)), "impc_batch_update_matrices")
 
     def update_lin_cost_device(self, q_ptr):
         """impc_batch_update_lin_cost_device: q [B][n] in device memory (address)."""

@@ -1132,6 +1132,42 @@ int ora_update_bounds(ora_ws *w, const c_float *l_new, const c_float *u_new) {
     return update_rho_vec(w);
 }
 
+/* scaling.h:40 unscale_data: P, q, A, l, u back to the problem's own units */
+static void unscale_data(ora_ws *w) {
+    c_int n = w->n, m = w->m;
+    for (c_int k = 0; k < w->P->p[n]; k++) w->P->x[k] *= w->cinv;                       /* mat_mult_scalar */
+    for (c_int j = 0; j < n; j++)                                                        /* mat_premult_diag */
+        for (c_int k = w->P->p[j]; k < w->P->p[j + 1]; k++) w->P->x[k] *= w->Dinv[w->P->i[k]];
+    for (c_int j = 0; j < n; j++)                                                        /* mat_postmult_diag */
+        for (c_int k = w->P->p[j]; k < w->P->p[j + 1]; k++) w->P->x[k] *= w->Dinv[j];
+    for (c_int i = 0; i < n; i++) w->q[i] *= w->cinv;
+    for (c_int i = 0; i < n; i++) w->q[i] = w->Dinv[i] * w->q[i];
+    for (c_int j = 0; j < n; j++)
+        for (c_int k = w->A->p[j]; k < w->A->p[j + 1]; k++) w->A->x[k] *= w->Einv[w->A->i[k]];
+    for (c_int j = 0; j < n; j++)
+        for (c_int k = w->A->p[j]; k < w->A->p[j + 1]; k++) w->A->x[k] *= w->Dinv[j];
+    for (c_int i = 0; i < m; i++) w->l[i] = w->Einv[i] * w->l[i];
+    for (c_int i = 0; i < m; i++) w->u[i] = w->Einv[i] * w->u[i];
+}
+
+/* osqp.h:137 / :147 osqp_update_P / osqp_update_A with every value (Px_new_idx = OSQP_NULL):
+ * unscale_data, the new values, scale_data, update_matrices (refactor with the current rho_vec),
+ * reset_info.  The iterates x, z, y stay as they are (scaled with the old scaling). */
+static int update_matrix(ora_ws *w, const c_float *Px_new, const c_float *Ax_new) {
+    if (!w) return OSQP_WORKSPACE_NOT_INIT_ERROR;
+    if (w->scaled) unscale_data(w);
+    if (Px_new) memcpy(w->P->x, Px_new, sizeof(c_float) * (size_t)w->P->p[w->n]);
+    if (Ax_new) memcpy(w->A->x, Ax_new, sizeof(c_float) * (size_t)w->A->p[w->n]);
+    if (w->scaled) scale_data(w);
+    if (linsys_factor(w)) return OSQP_NONCVX_ERROR;
+    w->info.status_val = OSQP_UNSOLVED;
+    w->info.rho_updates = 0;
+    return 0;
+}
+int ora_update_P(ora_ws *w, const c_float *Px_new) { return update_matrix(w, Px_new, NULL); }
+int ora_update_A(ora_ws *w, const c_float *Ax_new) { return update_matrix(w, NULL, Ax_new); }
+int ora_update_P_A(ora_ws *w, const c_float *Px_new, const c_float *Ax_new) { return update_matrix(w, Px_new, Ax_new); }
+
 /* osqp.h:78 osqp_solve */
 int ora_solve_ws(ora_ws *w) {
     int exitflag = 0, can_check_termination = 0;

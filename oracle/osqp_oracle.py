@@ -53,6 +53,7 @@ def lib():
         L.ora_get.restype = None
         L.ora_update_lin_cost.argtypes = [C.c_void_p, dp]
         L.ora_update_bounds.argtypes = [C.c_void_p, dp, dp]
+        L.ora_update_P_A.argtypes = [C.c_void_p, dp, dp]
         L.ora_cleanup.argtypes = [C.c_void_p]
         L.ora_get_setup.argtypes = [C.c_void_p, dp, ip, dp, dp, dp]
         L.ora_cleanup.restype = None
@@ -132,6 +133,14 @@ class Workspace:
 
     def update_bounds(self, l, u):
         lib().ora_update_bounds(self.h, _d(np.ascontiguousarray(l, float)), _d(np.ascontiguousarray(u, float)))
+
+    def update_matrices(self, Px=None, Ax=None):
+        """osqp_update_P / osqp_update_A / osqp_update_P_A with every value (ora_update_P_A)."""
+        P = None if Px is None else np.ascontiguousarray(Px, float)
+        A = None if Ax is None else np.ascontiguousarray(Ax, float)
+        rc = lib().ora_update_P_A(self.h, _d(P), _d(A))
+        if rc:
+            raise RuntimeError(f"ora_update_P_A failed: {rc}")
 
     def setup_state(self):
         """rho_vec, constr_type, D, E and c as osqp_setup left them (ora_get_setup)."""
