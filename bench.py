@@ -23,13 +23,14 @@ Workloads (--workload):
   config5 (BASELINE.json configs[4]): 65,536 N=40 QPs (8192 instances x 8 hypotheses, 10(+1)
       dynamic obstacles), split by instance across the ranks, as a CLOSED receding window on
       persistent workspaces: setup + first solve before the timed region, then every timed step,
-      all on the device: each QP's next x0 = getPos / getVel(dt) of its own last solution
-      (impc_batch_follow_plan_device, mpc_node.cpp:216-224), the reference one step further along
-      the path and the predicted obstacles one step on (impc_copy_rows_device windows), the next
-      q, l, u built by impc_mpc_build_values_device (linearisation point and A kept: the
-      factorisation is reused, BASELINE configs[4]), osqp_update_lin_cost + osqp_update_bounds
-      (impc_batch_update_*_device) and the solve resuming from the kept scaling, rho and iterates;
-      one RCCL all_gather of the cost records (N > 1).
+      all on the device: each QP's next x0 = getPos / getVel(dt) of its own last solution and its
+      next linearisation point = that solution's states (impc_batch_follow_plan_device,
+      mpc_node.cpp:216-224, mpcPlanner.cpp:1042-1051), the reference one step further along the
+      path and the predicted obstacles one step on (impc_copy_rows_device windows), the next A
+      (obstacle rows), q, l, u built by impc_mpc_build_values_device, osqp_update_A +
+      osqp_update_lin_cost + osqp_update_bounds (impc_batch_update_*_device) and the solve
+      continuing from the kept rho and scaled iterates (the warm-started receding window; the
+      device refactors on every resume); one RCCL all_gather of the cost records (N > 1).
   live: the reference's live planner horizon N = 30 (autonomous_flight planner_param.yaml:25) on
       config 3's workload -- 8192 instances x 8 intent hypotheses, 8(+1) dynamic obstacles, full
       setup + warm start + solve per QP every step (the long shape's compile-time W = 29 instance);
@@ -605,9 +606,9 @@ def select_candidates(impc, scenarios, ctx, buckets, batch_by_k, pd_params):
 class RecedingLoop:
     """Config 5's closed receding window on the device (module docstring).  Per bucket: each QP's
     reference path extended past the horizon (the last segment continued, as getReferenceTraj pads),
-    its predicted obstacles extended by their last entry (the builder's .back() rule), the
-    linearisation point of the setup (the previous plan: A and the factorisation are kept), x0 /
-    v0 device rows updated from each solve (impc_batch_follow_plan_device)."""
+    its predicted obstacles extended by their last entry (the builder's .back() rule), x0 / v0 and
+    the linearisation point (initially the scenario's previous plan) as device rows updated from
+    each solve (impc_batch_follow_plan_device)."""
 
     def __init__(self, impc, ctx, batches, steps):
         self.impc, self.ctx, self.batches, self.steps, self.t = impc, ctx, batches, steps, 0
@@ -630,7 +631,7 @@ class RecedingLoop:
             e = dict(N=N, K=K, L=L, T=T, nb=nb, ts=pd["ts"], b=b, bk=bk,
                      bld=impc.MpcBuilder(ctx, p, 0, K, L),
                      path=D(ctx, path), dpx=D(ctx, np.ascontiguousarray(dpx)), dsx=D(ctx, np.ascontiguousarray(dsx)),
-                     lin=D(ctx, np.ascontiguousarray(prev, np.float64)),
+                     lin=D(ctx, np.ascontiguousarray(prev, np.float64)), lin0=np.ascontiguousarray(prev, np.float64),
                      pos0=np.ascontiguousarray(d["pos"][inst], np.float64),
                      vel0=np.ascontiguousarray(d["vel"][inst], np.float64),
                      pos=D(ctx, (nb, 3)), vel=D(ctx, (nb, 3)), xr=D(ctx, (nb, N, 8)), dp=D(ctx, (nb, K, L, 3)),
@@ -656,6 +657,7 @@ class RecedingLoop:
             b.warm_start(bk["x_ws"], None)
             e["pos"].set(e["pos0"])
             e["vel"].set(e["vel0"])
+            e["lin"].set(e["lin0"])
         self._solve()
         self.ctx.synchronize()
         self.t = 0
@@ -667,7 +669,7 @@ class RecedingLoop:
         t = self.t
         for e in self.buckets:
             N, K, L, T, nb = e["N"], e["K"], e["L"], e["T"], e["nb"]
-            e["b"].follow_plan_device(N, e["ts"], e["ts"], e["pos"].ptr, e["vel"].ptr)
+            e["b"].follow_plan_device(N, e["ts"], e["ts"], e["pos"].ptr, e["vel"].ptr, e["lin"].ptr)
             impc.copy_rows_device(ctx, e["xr"].ptr, 64 * N, e["path"].ptr + 64 * t, 64 * (N + T), 64 * N, nb)
             for src, dst in (("dpx", "dp"), ("dsx", "ds")):
                 impc.copy_rows_device(ctx, e[dst].ptr, 24 * L, e[src].ptr + 24 * t, 24 * (L + T), 24 * L, nb * K)
@@ -675,10 +677,11 @@ class RecedingLoop:
                            e["ds"].ptr, e["Px"].ptr, e["q"].ptr, e["Ax"].ptr, e["l"].ptr, e["u"].ptr)
 
     def advance(self):
-        """One timed closed-loop step: next values on the device, persistent updates (the solve
-        follows in the caller's launch)."""
+        """One timed closed-loop step: next values on the device, persistent updates -- the new A
+        (osqp_update_A), q, l, u (the solve follows in the caller's launch)."""
         self.build()
         for e in self.buckets:
+            e["b"].update_matrices_device(None, e["Ax"].ptr)
             e["b"].update_lin_cost_device(e["q"].ptr)
             e["b"].update_bounds_device(e["l"].ptr, e["u"].ptr)
 
@@ -696,7 +699,7 @@ class RecedingLoop:
             self.advance()
             for e in self.buckets:
                 if e["k"]:
-                    e["ups"].append(tuple(rows_to_host(self.impc, self.ctx, e[a], e["k"]) for a in ("q", "l", "u")))
+                    e["ups"].append(tuple(rows_to_host(self.impc, self.ctx, e[a], e["k"]) for a in ("Ax", "q", "l", "u")))
             self._solve()
             its, sts = [], []
             for e in self.buckets:
@@ -728,8 +731,8 @@ def rows_to_host(impc, ctx, darr, k):
 
 def cpu_baseline_receding(bks, settings, rec, threads):
     """Config 5's CPU path: the oracle's persistent workspaces (osqp_setup, warm start, solve once,
-    then per closed-loop step osqp_update_lin_cost + osqp_update_bounds + osqp_solve with the step's
-    q, l, u -- the reference's polyTrajSolver pattern) over a bounded sample, the first QPs of each
+    then per closed-loop step osqp_update_A + osqp_update_lin_cost + osqp_update_bounds + osqp_solve
+    with the step's A, q, l, u) over a bounded sample, the first QPs of each
     bucket, on `threads` host threads (one QP's chain per task; the oracle's C calls release the
     GIL); the timed part is the update + solve steps.  Returns (line object, [(k, x, y, info) per
     bucket] of the last step, for the parity check)."""
@@ -753,7 +756,8 @@ def cpu_baseline_receding(bks, settings, rec, threads):
 
         def chain(i):
             out = None
-            for q, l, u in ups:
+            for Ax, q, l, u in ups:
+                ws[i].update_matrices(None, Ax[i])
                 ws[i].update_lin_cost(q[i])
                 ws[i].update_bounds(l[i], u[i])
                 out = ws[i].solve()
@@ -772,7 +776,7 @@ def cpu_baseline_receding(bks, settings, rec, threads):
     return {"value": n_all / t_all, "unit": "QP-solves/s", "cores": threads, "kind": "port",
             "host_cpus": os.cpu_count(), "cpu_model": cpu_info(),
             "sample": f"{sum(r[0] for r in ref)} QPs of the workload (first of each bucket) x {steps} closed-loop "
-                      f"steps, oracle persistent workspaces (update q, update l/u, solve) with the device-built values "
+                      f"steps, oracle persistent workspaces (update A, q, l/u, solve) with the device-built values "
                       f"of each step, {threads} threads ({t_all:.1f} s)"}, ref
 
 

@@ -222,6 +222,9 @@ int impc_batch_update_bounds_device(impc_batch b, const double *l, const double 
  * rescaled).  The generic kernel has no in-place form (IMPC_UNSUPPORTED: set the values again and
  * warm start). */
 int impc_batch_update_matrices(impc_batch b, const double *Px, const double *Ax);
+/* The same from DEVICE arrays, stream-ordered on the context stream (a receding loop that
+ * re-linearises its obstacle rows on the device every step). */
+int impc_batch_update_matrices_device(impc_batch b, const double *Px, const double *Ax);
 
 /* Kernel selection.  AUTO picks the one-QP-per-wavefront structured kernel when the pattern is
  * the stage-structured mpcPlanner QP and fits its register layout, else the

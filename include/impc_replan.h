@@ -159,9 +159,12 @@ int impc_replan_advance_device(impc_replan rp, double t, double *pos, double *ve
 /* The same for a receding window of single QPs (a persistent batch of mpcPlanner QPs, n = 13
  * horizon - 5): QP b's next x0, pos[b] / vel[b] [B][3], = getPos(t) / getVel(t) of its own last
  * solution when the solve returned one (status SOLVED, SOLVED_INACCURATE, MAX_ITER_REACHED,
- * TIME_LIMIT_REACHED); a QP without one (infeasible: x is OSQP_NAN) keeps its x0.  DEVICE pos, vel,
- * updated in place after the batch's last solve, on the context stream. */
-int impc_batch_follow_plan_device(impc_batch b, int32_t horizon, double ts, double t, double *pos, double *vel);
+ * TIME_LIMIT_REACHED), and (lin_states != NULL) its next linearisation point lin_states[b]
+ * [horizon][8] = the solution's states (currentStatesSol_); a QP without a solution (infeasible: x
+ * is OSQP_NAN) keeps both.  DEVICE arrays, updated in place after the batch's last solve, on the
+ * context stream. */
+int impc_batch_follow_plan_device(impc_batch b, int32_t horizon, double ts, double t, double *pos, double *vel,
+                                  double *lin_states);
 
 #ifdef __cplusplus
 }

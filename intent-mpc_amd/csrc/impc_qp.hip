@@ -2074,6 +2074,34 @@ int impc_batch_update_matrices(impc_batch b, const double *Px, const double *Ax)
     return IMPC_OK;
 }
 
+int impc_batch_update_matrices_device(impc_batch b, const double *Px, const double *Ax) {
+    if (!b || (!Px && !Ax)) return fail(IMPC_INVALID_ARGUMENT, "null batch, or neither P nor A values");
+    HIP_OK(hipSetDevice(b->ctx->device));
+    IMPC_TRY(flush_staged(b));
+    if (!use_structured(b))
+        return fail(IMPC_UNSUPPORTED, "generic kernel: no in-place matrix update (impc_batch_set_values + warm start)");
+    if (!b->persist_on || !b->persist_valid)
+        return fail(IMPC_WORKSPACE_NOT_INIT_ERROR,
+                    "structured kernel: impc_batch_set_persistent(b, 1) and one solve before updates");
+    hipStream_t st = b->ctx->stream;
+    IMPC_TRY(ctx_order_after_all(b->ctx, st));  // after every launch that may still read the values
+    if (b->shared) {
+        const int64_t tot = b->B * (b->nnzP + b->nnzA);
+        const int64_t blocks = std::min<int64_t>((tot + 255) / 256, (int64_t)b->ctx->num_cu * 16);
+        hipLaunchKernelGGL(k_expand_shared, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, st, b->d_shPx,
+                           b->d_shAx, b->d_vmap, b->d_Axv, b->nvar, b->nnzP, b->nnzA, b->B, b->in_Px, b->in_Ax);
+        HIP_OK(hipGetLastError());
+        b->shared = false;
+    }
+    if (Px && b->nnzP)
+        HIP_OK(hipMemcpyAsync(b->in_Px, Px, sizeof(double) * b->nnzP * b->B, hipMemcpyDeviceToDevice, st));
+    if (Ax && b->nnzA)
+        HIP_OK(hipMemcpyAsync(b->in_Ax, Ax, sizeof(double) * b->nnzA * b->B, hipMemcpyDeviceToDevice, st));
+    b->rescale = true;
+    b->generic_dirty = true;
+    return IMPC_OK;
+}
+
 int impc_batch_get_stats(impc_batch b, impc_batch_stats *out) {
     if (!b || !out) return fail(IMPC_INVALID_ARGUMENT, "null argument");
     std::memset(out, 0, sizeof(*out));

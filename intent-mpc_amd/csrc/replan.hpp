@@ -68,7 +68,8 @@ namespace impc_replan_k {
 // mpcPlanner::getPos / getVel (mpcPlanner.cpp:1257-1290) on QP b's own solution, for the QPs
 // whose solve returned one; pos / vel [B][3] updated in place
 __global__ void k_follow(int64_t B, int32_t N, int64_t n, double ts, double t, const double *__restrict__ x,
-                         const impc_info *__restrict__ info, double *__restrict__ pos, double *__restrict__ vel) {
+                         const impc_info *__restrict__ info, double *__restrict__ pos, double *__restrict__ vel,
+                         double *__restrict__ lin) {
     for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < B; b += (int64_t)gridDim.x * blockDim.x) {
         const int64_t st = info[b].status_val;
         if (st != IMPC_SOLVED && st != IMPC_SOLVED_INACCURATE && st != IMPC_MAX_ITER_REACHED &&
@@ -83,12 +84,15 @@ __global__ void k_follow(int64_t B, int32_t N, int64_t n, double ts, double t, c
             pos[3 * b + c] = s[c] + (e[c] - s[c]) / ts * dt;
             vel[3 * b + c] = s[3 + c] + (e[3 + c] - s[3 + c]) / ts * dt;
         }
+        // currentStatesSol_: the next linearisation point (castMPCToQPConstraintMatrix :1042-1051)
+        if (lin)
+            for (int k = 0; k < 8 * N; k++) lin[b * 8 * (int64_t)N + k] = x[b * n + k];
     }
 }
 }  // namespace impc_replan_k
 
 extern "C" int impc_batch_follow_plan_device(impc_batch b, int32_t horizon, double ts, double t, double *pos,
-                                             double *vel) {
+                                             double *vel, double *lin_states) {
     if (!b || horizon < 2 || b->n != 13 * (int64_t)horizon - 5 || !(ts > 0.0) || !(t >= 0.0) || !pos || !vel)
         return fail(IMPC_INVALID_ARGUMENT, "follow plan: an mpcPlanner batch (n = 13 horizon - 5), ts > 0, t >= 0");
     HIP_OK(hipSetDevice(b->ctx->device));
@@ -96,7 +100,7 @@ extern "C" int impc_batch_follow_plan_device(impc_batch b, int32_t horizon, doub
     IMPC_TRY(ctx_order_after_all(b->ctx, st));  // after the solve, wherever it ran
     const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((b->Bact + 255) / 256, 4096));
     hipLaunchKernelGGL(impc_replan_k::k_follow, dim3(blocks), dim3(256), 0, st, b->Bact, horizon, b->n, ts, t, b->d_xout,
-                       b->d_info, pos, vel);
+                       b->d_info, pos, vel, lin_states);
     HIP_OK(hipGetLastError());
     return IMPC_OK;
 }

@@ -129,6 +129,7 @@ _sig("impc_batch_update_bounds", C.c_int, _P, _dp, _dp)
 _sig("impc_batch_update_lin_cost_device", C.c_int, _P, _P)
 _sig("impc_batch_update_bounds_device", C.c_int, _P, _P, _P)
 _sig("impc_batch_update_matrices", C.c_int, _P, _dp, _dp)
+_sig("impc_batch_update_matrices_device", C.c_int, _P, _P, _P)
 _sig("impc_batch_get_stats", C.c_int, _P, C.POINTER(Stats))
 _sig("impc_batch_get_perm", C.c_int, _P, _i64p)
 _sig("impc_batch_set_profiling", C.c_int, _P, C.c_int)
@@ -144,7 +145,7 @@ _sig("impc_copy_to_host", C.c_int, _P, _P, _P, C.c_int64)
 _sig("impc_reference_traj_device", C.c_int, _P, C.c_int32, C.c_double, C.c_int64, _P, _P, _P, _P, C.c_int32, _P, _P)
 _sig("impc_repeat_rows_device", C.c_int, _P, _P, C.c_int64, C.c_int64, C.c_int32, _P, _P)
 _sig("impc_copy_rows_device", C.c_int, _P, _P, C.c_int64, _P, C.c_int64, C.c_int64, C.c_int64, _P)
-_sig("impc_batch_follow_plan_device", C.c_int, _P, C.c_int32, C.c_double, C.c_double, _P, _P)
+_sig("impc_batch_follow_plan_device", C.c_int, _P, C.c_int32, C.c_double, C.c_double, _P, _P, _P)
 # include/impc_comm.h
 COMM_ID_BYTES = 128
 _sig("impc_comm_unique_id", C.c_int, C.POINTER(C.c_ubyte))
@@ -261,7 +262,7 @@ EXPORTED = [
     "impc_batch_update_lin_cost_device", "impc_batch_update_bounds_device", "impc_ctx_pool_stats",
     "impc_replan_create", "impc_replan_destroy", "impc_replan_set_state", "impc_replan_run", "impc_replan_get_stats",
     "impc_replan_view_device", "impc_replan_shape", "impc_replan_advance_device", "impc_batch_follow_plan_device",
-    "impc_copy_rows_device", "impc_batch_update_matrices",
+    "impc_copy_rows_device", "impc_batch_update_matrices", "impc_batch_update_matrices_device",
 ]
 
 
@@ -468,11 +469,16 @@ class Batch:
                              f"{self.B * self.m}")
         _check(lib.impc_batch_update_bounds(self.h, _d(la), _d(ua)), "impc_batch_update_bounds")
 
-    def follow_plan_device(self, horizon, ts, t, pos_ptr, vel_ptr):
+    def follow_plan_device(self, horizon, ts, t, pos_ptr, vel_ptr, lin_ptr=None):
         """impc_batch_follow_plan_device: pos / vel [B][3] (device) = getPos(t) / getVel(t) of each
-        QP's own last solution (QPs with a solution)."""
-        _check(lib.impc_batch_follow_plan_device(self.h, int(horizon), float(ts), float(t), _P(pos_ptr), _P(vel_ptr)),
-               "impc_batch_follow_plan_device")
+        QP's own last solution, lin [B][N][8] = its states (QPs with a solution)."""
+        _check(lib.impc_batch_follow_plan_device(self.h, int(horizon), float(ts), float(t), _P(pos_ptr), _P(vel_ptr),
+                                                 _P(lin_ptr) if lin_ptr else None), "impc_batch_follow_plan_device")
+
+    def update_matrices_device(self, Px_ptr=None, Ax_ptr=None):
+        """impc_batch_update_matrices_device: new P / A values [B][nnz] in device memory (None = unchanged)."""
+        _check(lib.impc_batch_update_matrices_device(self.h, _P(Px_ptr) if Px_ptr else None,
+                                                     _P(Ax_ptr) if Ax_ptr else None), "impc_batch_update_matrices_device")
 
     def update_matrices(self, Px=None, Ax=None):
         """impc_batch_update_matrices: new P / A values [B][nnz] (host; None = unchanged)."""

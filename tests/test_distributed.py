@@ -245,10 +245,10 @@ def test_two_rank_config3_strong_split_matches_whole_batch():
 def _closed_loop_oracle(bks, steps, s):
     """bench.py --workload config5's closed receding window (RecedingLoop) restated on the CPU for
     a rank's buckets: oracle persistent workspaces; per step each QP's x0 = state 1 of its own last
-    solution (when it has one, impc_batch_follow_plan_device), the reference and the predicted
-    obstacles one step on, q / l / u from the host builder with the setup's linearisation point,
-    update_lin_cost + update_bounds + solve.  Returns per step the (inst, hyp, obj, status, iter)
-    rows of every QP."""
+    solution and its linearisation point = that solution's states (when it has one,
+    impc_batch_follow_plan_device), the reference and the predicted obstacles one step on, A / q /
+    l / u from the host builder, update A + update_lin_cost + update_bounds + solve.  Returns per
+    step the (inst, hyp, obj, status, iter) rows of every QP."""
     import impc
     from oracle import osqp_oracle as ora
     out = [[] for _ in range(steps)]
@@ -265,7 +265,7 @@ def _closed_loop_oracle(bks, steps, s):
         dsx = np.concatenate([bk["dyn_size"], np.repeat(bk["dyn_size"][:, :, -1:], T, axis=2)], axis=2)
         L = bk["dyn_pos"].shape[2]
         v = bk["values"]
-        pos, vel = d["pos"][inst].copy(), d["vel"][inst].copy()
+        pos, vel, lin = d["pos"][inst].copy(), d["vel"][inst].copy(), prev.copy()
         ws, sol = [], []
         for i in range(inst.size):
             w = ora.Workspace(bk["pattern"], v["Px"][i], v["q"][i], v["Ax"][i], v["l"][i], v["u"][i], so)
@@ -275,10 +275,11 @@ def _closed_loop_oracle(bks, steps, s):
         for t in range(1, steps + 1):
             for i, (x, _, info) in enumerate(sol):
                 if int(info["status_val"]) in (1, 2, -2, -6):
-                    pos[i], vel[i] = x[8:11], x[11:14]
-            vals = impc.mpc_values(p, pos, vel, path[:, t:t + N], prev, dyn_pos=dpx[:, :, t:t + L],
+                    pos[i], vel[i], lin[i] = x[8:11], x[11:14], x[: 8 * N].reshape(N, 8)
+            vals = impc.mpc_values(p, pos, vel, path[:, t:t + N], lin, dyn_pos=dpx[:, :, t:t + L],
                                    dyn_size=dsx[:, :, t:t + L])
             for i, w in enumerate(ws):
+                w.update_matrices(None, vals["Ax"][i])
                 w.update_lin_cost(vals["q"][i])
                 w.update_bounds(vals["l"][i], vals["u"][i])
                 sol[i] = w.solve()
