@@ -310,6 +310,12 @@ class Solver {
             return had ? warm_start_raw(wx, wy) : true;
         }
         std::vector<double> &dst = hessian ? d.Px : d.Ax;
+        if (in_place() && structured()) {  // osqp_update_P / osqp_update_A on the kept workspace
+            int rc = impc_batch_update_matrices(m_batch, hessian ? x.data() : nullptr, hessian ? nullptr : x.data());
+            if (rc) { detail::debug_impc("impc_batch_update_matrices", rc); return false; }
+            dst = x;
+            return true;
+        }
         std::vector<double> old = dst;
         dst = x;
         if (resetup_from_data()) return true;
@@ -515,11 +521,14 @@ public:
         return updateBounds(l, upperBound);
     }
 
-    /* Solver.tpp:15-113 / :116-212.  Same pattern: the new values are set up afresh and the solve
-     * resumes from the last solution (OSQP's osqp_update_P / _A re-scale and refactor but keep the
-     * scaled iterates; here the unscaled iterate is carried into the new scaling instead -- the same
-     * fixed point, a different first iteration).  New pattern: a new batch, warm-started, as
-     * OsqpEigen re-initialises its solver.  No reference caller updates P or A. */
+    /* Solver.tpp:15-113 / :116-212.  Same pattern on the persistent structured workspace (the
+     * mpcPlanner QP): osqp_update_P / osqp_update_A -- the next solve re-runs the scaling on the new
+     * data, refactors with the kept rho and continues from the kept scaled iterates, as OSQP 0.6.2
+     * does (impc_batch_update_matrices).  Same pattern on the generic kernel (any other QP), or
+     * before the first solve: the new values are set up afresh and the solve resumes from the last
+     * solution, unscaled (a documented deviation: the same fixed point, a different first
+     * iteration).  New pattern: a new batch, warm-started, as OsqpEigen re-initialises its solver.
+     * No reference caller updates P or A. */
     template <typename Derived>
     bool updateHessianMatrix(const Eigen::SparseCompressedBase<Derived> &hessianMatrix) {
         return update_matrix(hessianMatrix, true);

@@ -590,6 +590,8 @@ struct impc_batch_s {
     double *d_persist = nullptr;
     bool persist_on = false, persist_valid = false, q_by_update = false;
     bool rescale = false;  // new P / A values on a persistent workspace (impc_batch_update_matrices)
+    bool q_after = false;  // ... and q updated after them: d_qsnap holds the q at the matrix update
+    double *d_qsnap = nullptr;
     bool qpt_valid = false;
     // shared-structure values (impc_batch_set_values_shared)
     bool shared = false, shared_expanded = false;
@@ -713,6 +715,7 @@ impc::WaveIO wave_io(impc_batch b) {
     if (b->persist_on && b->d_persist) {
         io.persist = b->d_persist;
         io.resume = b->persist_valid ? (b->rescale ? 2 : 1) : 0;
+        if (b->persist_valid && b->rescale && b->q_after) io.q_scale = b->d_qsnap;
         io.q_updated = b->q_by_update ? 1 : 0;
     }
     b->qpt_valid = io.qpt != nullptr;
@@ -1019,7 +1022,7 @@ int with_shape(int vs, int gs, bool tier, F &&f) {
 void structured_solved(impc_batch b) {
     if (!b->persist_on) return;
     b->persist_valid = true;
-    b->rescale = false;
+    b->rescale = b->q_after = false;
     b->has_ws = false;
 }
 
@@ -1204,7 +1207,7 @@ void reset_batch(impc_batch b) {
     b->dst.tick_s = b->ctx->tick_s;
     b->kernel_req = IMPC_KERNEL_AUTO;
     b->values_set = b->has_ws = b->ws_y = b->tlim_on = false;
-    b->persist_on = b->persist_valid = b->q_by_update = b->rescale = false;
+    b->persist_on = b->persist_valid = b->q_by_update = b->rescale = b->q_after = false;
     b->profile = b->qpt_valid = b->ev_setup = b->ev_solve = false;
     b->queue_mode = IMPC_QUEUE_FIFO;
     b->queue_qw = 0.0;
@@ -1401,7 +1404,7 @@ int impc_batch_destroy(impc_batch b) {
     if (b->h_stage) (void)hipHostFree(b->h_stage);
     void *ptrs[] = {b->d_in,     b->d_xout,  b->d_tables, b->d_scal, b->d_counter,
                     b->d_sym,    b->d_work,  b->d_sec,   b->d_shPx,  b->d_shAx,   b->d_Axv,  b->d_vmap,
-                    b->d_qpt,    b->d_persist, b->d_tlim, b->d_csr, b->d_qscr};
+                    b->d_qpt,    b->d_persist, b->d_tlim, b->d_csr, b->d_qscr, b->d_qsnap};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete b;
@@ -1480,7 +1483,7 @@ int impc_batch_set_settings(impc_batch b, const impc_settings *s) {
         return fail(IMPC_UNSUPPORTED, "persistent workspaces support scaling <= 20 Ruiz passes");
     if (s->rho != b->settings.rho || s->sigma != b->settings.sigma || s->scaling != b->settings.scaling) {
         b->generic_dirty = true;
-        b->persist_valid = b->q_by_update = b->rescale = false;  // a different setup: the next solve starts over
+        b->persist_valid = b->q_by_update = b->rescale = b->q_after = false;  // a different setup: the next solve starts over
     }
     b->settings = *s;
     b->dst = d;
@@ -1517,7 +1520,7 @@ int impc_batch_set_values(impc_batch b, const double *Px, const double *q, const
         }
         b->in_dirty = true;  // uploaded with the warm start by the next call that needs them (flush_staged)
         b->shared = false;
-        b->persist_valid = b->q_by_update = b->rescale = false;
+        b->persist_valid = b->q_by_update = b->rescale = b->q_after = false;
         b->values_set = true;
         b->generic_dirty = true;
         return IMPC_OK;
@@ -1531,7 +1534,7 @@ int impc_batch_set_values(impc_batch b, const double *Px, const double *q, const
         IMPC_TRY(h2d_sync(b->ctx->stream, b->in_u, u, sizeof(double) * b->m * B));
     }
     b->shared = false;
-    b->persist_valid = b->q_by_update = b->rescale = false;  // new data: the next solve sets up from scratch
+    b->persist_valid = b->q_by_update = b->rescale = b->q_after = false;  // new data: the next solve sets up from scratch
     b->values_set = true;
     b->generic_dirty = true;
     return IMPC_OK;
@@ -1585,7 +1588,7 @@ int impc_batch_set_values_shared(impc_batch b, const double *Px, const double *A
     b->nvar = nvar;
     b->shared = true;
     b->shared_expanded = false;
-    b->persist_valid = b->q_by_update = b->rescale = false;
+    b->persist_valid = b->q_by_update = b->rescale = b->q_after = false;
     b->values_set = true;
     b->generic_dirty = true;
     return IMPC_OK;
@@ -1609,7 +1612,7 @@ int impc_batch_set_values_device(impc_batch b, const double *Px, const double *q
         HIP_OK(hipMemcpyAsync(b->in_u, u, sizeof(double) * b->m * B, hipMemcpyDeviceToDevice, st));
     }
     b->shared = false;
-    b->persist_valid = b->q_by_update = b->rescale = false;  // new data: the next solve sets up from scratch
+    b->persist_valid = b->q_by_update = b->rescale = b->q_after = false;  // new data: the next solve sets up from scratch
     b->values_set = true;
     b->generic_dirty = true;
     return IMPC_OK;
@@ -1685,7 +1688,7 @@ int impc_batch_set_values_async(impc_batch b, const double *Ax_var, const double
     b->ws_y = false;
     if (x_ws) b->settings.warm_start = b->dst.warm_start = 1;
     b->shared_expanded = false;
-    b->persist_valid = b->q_by_update = b->rescale = false;
+    b->persist_valid = b->q_by_update = b->rescale = b->q_after = false;
     b->values_set = true;
     b->generic_dirty = true;
     return IMPC_OK;
@@ -1737,7 +1740,7 @@ int impc_batch_set_active(impc_batch b, int64_t count) {
     if (count < 1 || count > b->B) return fail(IMPC_INVALID_ARGUMENT, "active count must be in [1, B]");
     if (count != b->Bact) {
         b->Bact = count;
-        b->persist_valid = b->q_by_update = b->rescale = false;  // the stored workspaces cover other QPs
+        b->persist_valid = b->q_by_update = b->rescale = b->q_after = false;  // the stored workspaces cover other QPs
         b->generic_dirty = true;
     }
     return IMPC_OK;
@@ -1941,6 +1944,7 @@ int impc_batch_update_lin_cost(impc_batch b, const double *q) {
         IMPC_TRY(ctx_quiesce(b->ctx));
         IMPC_TRY(h2d_sync(b->ctx->stream, b->in_q, q, sizeof(double) * b->n * b->B));
         b->q_by_update = true;
+        b->q_after = b->rescale;
         b->generic_dirty = true;
         return IMPC_OK;
     }
@@ -2002,6 +2006,7 @@ int impc_batch_update_lin_cost_device(impc_batch b, const double *q) {
         IMPC_TRY(ctx_order_after_all(b->ctx, st));
         HIP_OK(hipMemcpyAsync(b->in_q, q, bytes, hipMemcpyDeviceToDevice, st));
         b->q_by_update = true;
+        b->q_after = b->rescale;
         b->generic_dirty = true;
         return IMPC_OK;
     }
@@ -2048,6 +2053,19 @@ int impc_batch_update_bounds_device(impc_batch b, const double *l, const double 
     return IMPC_OK;
 }
 
+// The q of the workspace at a matrix update (OSQP's scale_data normalises the cost with it; a later
+// matrix update rescales again with the q current then): kept for the next solve in case q is
+// updated before it (impc_batch_update_lin_cost after the matrices)
+static int snapshot_q(impc_batch b, hipStream_t st) {
+    if (!b->d_qsnap) {
+        HIP_OK(hipMalloc((void **)&b->d_qsnap, sizeof(double) * (size_t)(b->n * b->B)));
+        b->device_bytes += (int64_t)sizeof(double) * b->n * b->B;
+    }
+    HIP_OK(hipMemcpyAsync(b->d_qsnap, b->in_q, sizeof(double) * (size_t)(b->n * b->B), hipMemcpyDeviceToDevice, st));
+    b->q_after = false;
+    return IMPC_OK;
+}
+
 int impc_batch_update_matrices(impc_batch b, const double *Px, const double *Ax) {
     if (!b || (!Px && !Ax)) return fail(IMPC_INVALID_ARGUMENT, "null batch, or neither P nor A values");
     IMPC_TRY(flush_staged(b));
@@ -2069,6 +2087,7 @@ int impc_batch_update_matrices(impc_batch b, const double *Px, const double *Ax)
     }
     if (Px && b->nnzP) IMPC_TRY(h2d_sync(st, b->in_Px, Px, sizeof(double) * b->nnzP * b->B));
     if (Ax && b->nnzA) IMPC_TRY(h2d_sync(st, b->in_Ax, Ax, sizeof(double) * b->nnzA * b->B));
+    IMPC_TRY(snapshot_q(b, st));
     b->rescale = true;
     b->generic_dirty = true;
     return IMPC_OK;
@@ -2097,6 +2116,7 @@ int impc_batch_update_matrices_device(impc_batch b, const double *Px, const doub
         HIP_OK(hipMemcpyAsync(b->in_Px, Px, sizeof(double) * b->nnzP * b->B, hipMemcpyDeviceToDevice, st));
     if (Ax && b->nnzA)
         HIP_OK(hipMemcpyAsync(b->in_Ax, Ax, sizeof(double) * b->nnzA * b->B, hipMemcpyDeviceToDevice, st));
+    IMPC_TRY(snapshot_q(b, st));
     b->rescale = true;
     b->generic_dirty = true;
     return IMPC_OK;
@@ -2153,7 +2173,7 @@ int impc_batch_set_persistent(impc_batch b, int on) {
         b->device_bytes += (int64_t)bytes;
     }
     b->persist_on = on != 0;
-    b->persist_valid = b->q_by_update = b->rescale = false;  // the next solve sets up from scratch
+    b->persist_valid = b->q_by_update = b->rescale = b->q_after = false;  // the next solve sets up from scratch
     return IMPC_OK;
 }
 
@@ -2415,7 +2435,7 @@ int batch_inputs_view(impc_batch b, BatchInputs *out) {
 int batch_inputs_end(impc_batch b, bool warm_x) {
     if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
     b->shared = false;
-    b->persist_valid = b->q_by_update = b->rescale = false;  // new data: the next solve sets up from scratch
+    b->persist_valid = b->q_by_update = b->rescale = b->q_after = false;  // new data: the next solve sets up from scratch
     b->values_set = true;
     b->generic_dirty = true;
     b->has_ws = warm_x;

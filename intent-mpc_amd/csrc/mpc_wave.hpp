@@ -127,6 +127,10 @@ struct WaveIO {
     // per-QP time limits [B] (impc_batch_set_time_limits: each solveTraj call sets its own), or
     // nullptr for the settings' time_limit
     const double *tlim = nullptr;
+    // resume = 2 with q updated after the matrix update: the q the workspace held when P / A
+    // changed [B][n].  OSQP's scale_data after osqp_update_P / _A normalises the cost with that q;
+    // the new q (io.q) is then scaled as osqp_update_lin_cost does, (D q) c
+    const double *q_scale = nullptr;
 };
 
 constexpr int kPersistHdr = 24;      // ct[0 .. kPersistMaxScaling), rho at kPersistHdr - 1
@@ -396,7 +400,7 @@ struct WaveQP {
             _Pragma("unroll") for (int cc = 0; cc < 8; cc++) cp[s][cc] = 0.0;
             if (vok[s]) {
                 int ov = T.var_orig[v];
-                q[s] = io.q[bn + ov];
+                q[s] = (io.q_scale ? io.q_scale : io.q)[bn + ov];
                 int pp = T.var_pdiag[v];
                 pd[s] = pp >= 0 ? io.Px[bP + pp] : 0.0;
                 ab[s] = Aval(T.var_boxpos[v]);
@@ -1560,7 +1564,7 @@ struct WaveQP {
         {
             double D[VS], Eb[VS], Eg[GS];
             scale(b, D, Eb, Eg, ps);
-            if (ps && io.resume == 1 && io.q_updated)  // osqp_update_lin_cost: q = c (D q)
+            if (ps && ((io.resume == 1 && io.q_updated) || io.q_scale))  // osqp_update_lin_cost: q = c (D q)
                 _Pragma("unroll") for (int s = 0; s < VS; s++)
                     if (vok[s]) q[s] = (D[s] * io.q[b * n + T.var_orig[NL * s + L]]) * c;
         }

@@ -1164,6 +1164,26 @@ static int update_matrix(ora_ws *w, const c_float *Px_new, const c_float *Ax_new
     w->info.rho_updates = 0;
     return 0;
 }
+/* Study variant (tools / tests only, not OSQP): replace P, q, A, l, u by raw values and scale them
+ * afresh from the problem's own units -- no unscale round trip of the old scaled data -- keeping
+ * rho and the scaled iterates; the row types follow the new scaled bounds. */
+int ora_rescale_raw(ora_ws *w, const c_float *Px, const c_float *q, const c_float *Ax, const c_float *l,
+                    const c_float *u) {
+    if (!w) return OSQP_WORKSPACE_NOT_INIT_ERROR;
+    memcpy(w->P->x, Px, sizeof(c_float) * (size_t)w->P->p[w->n]);
+    memcpy(w->A->x, Ax, sizeof(c_float) * (size_t)w->A->p[w->n]);
+    memcpy(w->q, q, sizeof(c_float) * (size_t)w->n);
+    for (c_int i = 0; i < w->m; i++) {
+        w->l[i] = fmin(fmax(l[i], -OSQP_INFTY), OSQP_INFTY);
+        w->u[i] = fmin(fmax(u[i], -OSQP_INFTY), OSQP_INFTY);
+    }
+    if (w->scaled) scale_data(w);
+    update_rho_vec(w);
+    if (linsys_factor(w)) return OSQP_NONCVX_ERROR;
+    w->info.status_val = OSQP_UNSOLVED;
+    w->info.rho_updates = 0;
+    return 0;
+}
 int ora_update_P(ora_ws *w, const c_float *Px_new) { return update_matrix(w, Px_new, NULL); }
 int ora_update_A(ora_ws *w, const c_float *Ax_new) { return update_matrix(w, NULL, Ax_new); }
 int ora_update_P_A(ora_ws *w, const c_float *Px_new, const c_float *Ax_new) { return update_matrix(w, Px_new, Ax_new); }

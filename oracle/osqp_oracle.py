@@ -54,6 +54,7 @@ def lib():
         L.ora_update_lin_cost.argtypes = [C.c_void_p, dp]
         L.ora_update_bounds.argtypes = [C.c_void_p, dp, dp]
         L.ora_update_P_A.argtypes = [C.c_void_p, dp, dp]
+        L.ora_rescale_raw.argtypes = [C.c_void_p, dp, dp, dp, dp, dp]
         L.ora_cleanup.argtypes = [C.c_void_p]
         L.ora_get_setup.argtypes = [C.c_void_p, dp, ip, dp, dp, dp]
         L.ora_cleanup.restype = None
@@ -141,6 +142,13 @@ class Workspace:
         rc = lib().ora_update_P_A(self.h, _d(P), _d(A))
         if rc:
             raise RuntimeError(f"ora_update_P_A failed: {rc}")
+
+    def rescale_raw(self, Px, q, Ax, l, u):
+        """Study variant (not OSQP): new raw data scaled afresh, rho and scaled iterates kept."""
+        a = [np.ascontiguousarray(v, float) for v in (Px, q, Ax, l, u)]
+        rc = lib().ora_rescale_raw(self.h, *[_d(v) for v in a])
+        if rc:
+            raise RuntimeError(f"ora_rescale_raw failed: {rc}")
 
     def setup_state(self):
         """rho_vec, constr_type, D, E and c as osqp_setup left them (ora_get_setup)."""

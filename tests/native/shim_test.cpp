@@ -141,8 +141,9 @@ static void structured_case() {
 }
 
 // Replay file layout (little-endian): int64 header {n, m, nnzP, nnzA, nqp, flags} (flags bit 0:
-// warm start x per QP, bit 1: update sequence q2 / l3 / u3 per QP), int64 Pp[n+1] Pi Ap[n+1] Ai,
-// then per QP double Px q Ax l u [x_ws] [q2 l3 u3].  Output per QP and step: double status, iter,
+// warm start x per QP, bit 1: update sequence q2 / l3 / u3 per QP, bit 2 (with bit 1): then
+// updateHessianMatrix(P4) -> solve -> updateLinearConstraintsMatrix(A4) -> solve), int64 Pp[n+1]
+// Pi Ap[n+1] Ai, then per QP double Px q Ax l u [x_ws] [q2 l3 u3] [P4 A4].  Output per QP and step: double status, iter,
 // obj, x[n], y[m].  P is inserted with both triangles (as an Eigen user holding the full symmetric
 // matrix does); the shim keeps the upper one (OsqpEigen Data.tpp:38-39).
 static int replay(const char *in, const char *out) {
@@ -162,18 +163,24 @@ static int replay(const char *in, const char *out) {
         return e;
     };
     for (int64_t qp = 0; qp < nqp; qp++) {
-        std::vector<double> Px, q, Ax, l, u, xw, q2, l3, u3;
+        std::vector<double> Px, q, Ax, l, u, xw, q2, l3, u3, P4, A4;
         if (!rd(Px, nnzP) || !rd(q, n) || !rd(Ax, nnzA) || !rd(l, m) || !rd(u, m)) return 2;
         if ((flags & 1) && !rd(xw, n)) return 2;
         if ((flags & 2) && (!rd(q2, n) || !rd(l3, m) || !rd(u3, m))) return 2;
-        Eigen::SparseMatrix<double> P((Eigen::Index)n, (Eigen::Index)n), A((Eigen::Index)m, (Eigen::Index)n);
-        for (int64_t j = 0; j < n; j++) {
-            for (int64_t k = Pp[j]; k < Pp[j + 1]; k++) {
-                P.insert(Pi[k], j) = Px[k];
-                if (Pi[k] != j) P.insert(j, Pi[k]) = Px[k];
+        if ((flags & 4) && (!rd(P4, nnzP) || !rd(A4, nnzA))) return 2;
+        // the Eigen matrices a user holds: P with both triangles, A full
+        auto mats = [&](const std::vector<double> &pv, const std::vector<double> &av, Eigen::SparseMatrix<double> &P,
+                        Eigen::SparseMatrix<double> &A) {
+            for (int64_t j = 0; j < n; j++) {
+                for (int64_t k = Pp[j]; k < Pp[j + 1]; k++) {
+                    P.insert(Pi[k], j) = pv[k];
+                    if (Pi[k] != j) P.insert(j, Pi[k]) = pv[k];
+                }
+                for (int64_t k = Ap[j]; k < Ap[j + 1]; k++) A.insert(Ai[k], j) = av[k];
             }
-            for (int64_t k = Ap[j]; k < Ap[j + 1]; k++) A.insert(Ai[k], j) = Ax[k];
-        }
+        };
+        Eigen::SparseMatrix<double> P((Eigen::Index)n, (Eigen::Index)n), A((Eigen::Index)m, (Eigen::Index)n);
+        mats(Px, Ax, P, A);
         OsqpEigen::Solver solver;  // mpcPlanner.cpp:436-527
         solver.settings()->setVerbosity(false);
         solver.settings()->setWarmStart(true);
@@ -191,10 +198,16 @@ static int replay(const char *in, const char *out) {
             y0.setZero((Eigen::Index)m);
             CHECK(solver.setWarmStart(x0, y0));
         }
-        const int steps = (flags & 2) ? 3 : 1;
+        const int steps = (flags & 2) ? ((flags & 4) ? 5 : 3) : 1;
         for (int step = 0; step < steps; step++) {
             if (step == 1) CHECK(solver.updateGradient(vec(q2)));
             if (step == 2) CHECK(solver.updateBounds(vec(l3), vec(u3)));
+            if (step >= 3) {  // Solver.tpp:15-212, same sparsity pattern
+                Eigen::SparseMatrix<double> P4m((Eigen::Index)n, (Eigen::Index)n), A4m((Eigen::Index)m, (Eigen::Index)n);
+                mats(P4, A4, P4m, A4m);
+                if (step == 3) CHECK(solver.updateHessianMatrix(P4m));
+                if (step == 4) CHECK(solver.updateLinearConstraintsMatrix(A4m));
+            }
             CHECK(solver.solveProblem() == OsqpEigen::ErrorExitFlag::NoError);
             double hdr[3] = {(double)solver.getStatus(), (double)solver.getIterations(), solver.getObjValue()};
             std::fwrite(hdr, sizeof(double), 3, o);

@@ -51,9 +51,12 @@ def test_live_loop_thirty_replans_on_the_benchmark_path(ctx):
             np.testing.assert_array_equal(pos_d.get(), pos)               # x0 replayed on the host
             exp_xref = np.array([refs[i].xref(pos[i]) for i in range(I)])
             np.testing.assert_array_equal(xref, exp_xref, err_msg=f"replan {r}: getXRef")
-            expect, expect_first = _check_replan(out, (plan_x, ft, None, None), pos, vel, xref, sc["dyn_cur"][r],
-                                                 sc["pred_pos"][r], sc["pred_size"], sc["prob"], np.ones(I, bool),
-                                                 None, np.zeros(I, np.int32), pd, s)
+            try:
+                expect, expect_first = _check_replan(out, (plan_x, ft, None, None), pos, vel, xref, sc["dyn_cur"][r],
+                                                     sc["pred_pos"][r], sc["pred_size"], sc["prob"], np.ones(I, bool),
+                                                     None, np.zeros(I, np.int32), pd, s)
+            except AssertionError as e:
+                raise AssertionError(f"replan {r}: {e}") from e
             plan_x, ft_new, _, valid = rp.plans()
             np.testing.assert_array_equal(plan_x, expect, err_msg=f"replan {r}: committed plans")
             np.testing.assert_array_equal(ft_new, expect_first)

@@ -123,7 +123,7 @@ def test_explicit_warm_start_between_updates(ctx, kernel):
         w.close()
 
 
-@pytest.mark.parametrize("which", ["P", "A", "PA"])
+@pytest.mark.parametrize("which", ["P", "A", "PA", "A+q"])
 def test_matrix_update_matches_osqp_update_P_A(ctx, which):
     """impc_batch_update_matrices on a persistent structured workspace against the oracle's
     osqp_update_P / _A / _P_A (ora_update_P_A: unscale_data, new values, scale_data, refactor, the
@@ -138,6 +138,7 @@ def test_matrix_update_matches_osqp_update_P_A(ctx, which):
     q2 = v["q"] * (1 + 0.05 * rng.standard_normal(v["q"].shape))
     P3 = v["Px"] * (1.0 + 0.5 * rng.uniform(size=v["Px"].shape)) if "P" in which else None
     A3 = v["Ax"] * (1.0 + 0.02 * rng.standard_normal(v["Ax"].shape)) if "A" in which else None
+    q5 = v["q"] * (1 + 0.3 * rng.standard_normal(v["q"].shape))
     l4, u4 = v["l"].copy(), v["u"].copy()
     fin = np.isfinite(l4) & np.isfinite(u4) & (u4 - l4 > 1e-3)
     l4[fin] -= 0.05
@@ -156,6 +157,8 @@ def test_matrix_update_matches_osqp_update_P_A(ctx, which):
         b.solve()
         r2 = b.get()
         b.update_matrices(P3, A3)
+        if which == "A+q":  # q after the matrices: OSQP scaled the cost with the q held at the update
+            b.update_lin_cost(q5)
         b.solve()
         r3 = b.get()
         b.update_bounds(l4, u4)
@@ -170,6 +173,8 @@ def test_matrix_update_matches_osqp_update_P_A(ctx, which):
         w.update_lin_cost(q2[i])
         check(r2[0][i], r2[2][i], w.solve())
         w.update_matrices(None if P3 is None else P3[i], None if A3 is None else A3[i])
+        if which == "A+q":
+            w.update_lin_cost(q5[i])
         check(r3[0][i], r3[2][i], w.solve())
         w.update_bounds(l4[i], u4[i])
         check(r4[0][i], r4[2][i], w.solve())

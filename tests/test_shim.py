@@ -31,14 +31,14 @@ def test_shim_solves_on_gpu():
     assert rc == 0, out
 
 
-def _replay(tmp_path, cfg, updates=None):
+def _replay(tmp_path, cfg, updates=None, matrices=None):
     """Run the QPs of cfg through the shim's solveTraj call sequence (shim_test replay) and read
     back status / iterations / objective / x / y per solve step."""
     pat, v = cfg["pattern"], cfg["values"]
     n, m = int(pat["n"]), int(pat["m"])
     B = v["q"].shape[0]
     xw = cfg.get("x_ws")
-    flags = (1 if xw is not None else 0) | (2 if updates is not None else 0)
+    flags = (1 if xw is not None else 0) | (2 if updates is not None else 0) | (4 if matrices is not None else 0)
     fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
     with open(fin, "wb") as f:
         np.array([n, m, len(pat["Pi"]), len(pat["Ai"]), B, flags], np.int64).tofile(f)
@@ -52,9 +52,12 @@ def _replay(tmp_path, cfg, updates=None):
             if updates is not None:
                 for a in updates:
                     np.ascontiguousarray(a[i], float).tofile(f)
+            if matrices is not None:
+                for a in matrices:
+                    np.ascontiguousarray(a[i], float).tofile(f)
     p = subprocess.run([EXE, "replay", str(fin), str(fout)], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
-    steps = 3 if updates is not None else 1
+    steps = (5 if matrices is not None else 3) if updates is not None else 1
     raw = np.fromfile(fout, float).reshape(B, steps, 3 + n + m)
     return [(raw[:, s, 3:3 + n], raw[:, s, 3 + n:], raw[:, s, 0].astype(int), raw[:, s, 1].astype(int),
              raw[:, s, 2]) for s in range(steps)]
@@ -125,6 +128,47 @@ def test_shim_update_sequence_vs_persistent_oracle(tmp_path):
         w.update_lin_cost(q2[i])
         refs.append(w.solve())
         w.update_bounds(l3[i], u3[i])
+        refs.append(w.solve())
+        w.close()
+        for s, (xo, yo, io) in enumerate(refs):
+            got = tuple(a[i:i + 1] for a in steps[s])
+            _check(got, (xo[None], yo[None], np.array([io["status_val"]]), np.array([io["iter"]]),
+                         np.array([io["obj_val"]])))
+
+
+@pytest.mark.gpu
+def test_shim_matrix_updates_vs_osqp_update_P_A(tmp_path):
+    """updateHessianMatrix / updateLinearConstraintsMatrix on an unchanged pattern through the shim
+    (Solver.tpp:15-212 -> osqp_update_P / osqp_update_A) against the oracle's persistent workspace:
+    solve -> updateGradient -> solve -> updateBounds -> solve -> new P -> solve -> new A -> solve,
+    identical statuses and iterations, x / y / objective within 1e-5."""
+    import impc
+    from impc import scenarios
+    from oracle import osqp_oracle as ora
+    os_ = ora.settings_from(impc.default_settings(verbose=0, warm_start=1))
+    bk = scenarios.intent_config(instances=1, hyps=8, seed=815)[8]
+    v = bk["values"]
+    B, m = v["q"].shape[0], int(bk["pattern"]["m"])
+    rng = np.random.default_rng(816)
+    q2 = v["q"] * (1 + 0.05 * rng.standard_normal(v["q"].shape))
+    l3, u3 = v["l"].copy(), v["u"].copy()
+    fin = np.isfinite(l3) & np.isfinite(u3) & (u3 - l3 > 0.1)
+    l3[fin] += 0.01
+    u3[fin] -= 0.01
+    P4 = v["Px"] * (1.0 + 0.5 * rng.uniform(size=v["Px"].shape))
+    A4 = v["Ax"] * (1.0 + 0.02 * rng.standard_normal(v["Ax"].shape))
+    steps = _replay(tmp_path, bk, updates=(q2, l3, u3), matrices=(P4, A4))
+    for i in range(B):
+        w = ora.Workspace(bk["pattern"], v["Px"][i], v["q"][i], v["Ax"][i], v["l"][i], v["u"][i], os_)
+        w.warm_start(bk["x_ws"][i], np.zeros(m))
+        refs = [w.solve()]
+        w.update_lin_cost(q2[i])
+        refs.append(w.solve())
+        w.update_bounds(l3[i], u3[i])
+        refs.append(w.solve())
+        w.update_matrices(P4[i], None)
+        refs.append(w.solve())
+        w.update_matrices(None, A4[i])
         refs.append(w.solve())
         w.close()
         for s, (xo, yo, io) in enumerate(refs):
