@@ -64,6 +64,12 @@ namespace impc {
 #ifndef IMPC_CHUNK19
 #define IMPC_CHUNK19 0
 #endif
+// The long shape's sweeps in five chunks on the four wavefronts (CL = 2 ceil(W/10): W = 39 -> 8, 8,
+// 8, 8, 7; the product since round 5).  IMPC_CHUNK5=0 (A/B variants only): the round-4 four-chunk
+// form (W = 39 -> 10, 10, 10, 9), measured 1251.6 vs 1209.6 ms per config-5 launch
+#ifndef IMPC_CHUNK5
+#define IMPC_CHUNK5 1
+#endif
 #define IMPC_REP(X) for (int rep_ = 0; rep_ < (IMPC_DUP == (X) ? 2 : 1); rep_++)
 // Branch counters of the CPU emulation's instrumented builds (tools only; nothing in the product)
 #ifndef IMPC_COUNT
@@ -359,13 +365,27 @@ struct WaveQP {
     // reduction and runs its chunk again.  Dependent chain per sweep: W steps -> 2 CL steps and one
     // reduction.  Operators and ends live in the F region's tail (blocks >= W + 3, never read).
     // CL is even, so every chunk starts on an even stage (the sweeps' index parity).
+    //
+    // Five chunks (NCH = 5, the long shape's form since round 5; four: IMPC_CHUNK5=0 and the
+    // default horizon's IMPC_CHUNK19 variant): CL = 2 ceil(W/10) and W - 4 CL in the
+    // last (W = 39: 8, 8, 8, 8, 7; W = 29: 6, 6, 6, 6, 5).  Round 1: wave 0 the first chunk from the
+    // true start, waves 1..3 chunks 1..3 from zero; round 2: waves 1..3 chunks 1..3 again from their
+    // true starts and wave 0 the fifth, whose start a_4CL = a^_4CL + P3 a^_3CL + P3P2 a^_2CL +
+    // P3P2P1 a_CL is still one 8-lane reduction.  Chain per sweep: 2 CL steps and one reduction
+    // (W = 39: 16 instead of 20).
+    static constexpr int NCH = (WF > 0 && VS == 3 && IMPC_CHUNK5) ? 5 : 4;
     static constexpr bool CHUNK = WF > 0 && NL == 256 && (VS == 3 || (VS == 1 && IMPC_CHUNK19 != 0));
-    static constexpr int CL = WF > 0 ? 2 * ((WF + 7) / 8) : 2;
-    static constexpr int CLAST = WF - 3 * CL;
+    static constexpr int CL = WF > 0 ? (NCH == 5 ? 2 * ((WF + 9) / 10) : 2 * ((WF + 7) / 8)) : 2;
+    static constexpr int CLAST = WF - (NCH - 1) * CL;
     static constexpr int CH_OFF = LD::F_OFF + 64 * (WF + 3);
-    enum { kChFP1 = 0, kChFP2 = 64, kChFP21 = 128, kChBT1 = 192, kChBT2 = 256, kChBT21 = 320, kChEnd = 384 };
-    static_assert(!CHUNK || VS == 1 || CH_OFF + kChEnd + 32 <= LD::R_OFF, "chunk operators do not fit the F region");
-    static_assert(!CHUNK || VS != 1 || LD::CHX >= kChEnd + 32, "chunk operator region");
+    enum { kChFP1 = 0, kChFP2 = 64, kChFP21 = 128, kChBT1 = 192, kChBT2 = 256, kChBT21 = 320 };
+    // five chunks: forward P1 P2 P3 P2P1 P3P2 P3P2P1, then the same backward (+kCh5B), then the ends
+    enum { kCh5P1 = 0, kCh5P2 = 64, kCh5P3 = 128, kCh5P21 = 192, kCh5P32 = 256, kCh5P321 = 320, kCh5B = 384 };
+    static constexpr int kChEnd = NCH == 5 ? 768 : 384;
+    static constexpr int kChEnds = NCH == 5 ? 24 : 16;  // chunk-end values per direction
+    static_assert(!CHUNK || VS == 1 || CH_OFF + kChEnd + 2 * kChEnds <= LD::R_OFF,
+                  "chunk operators do not fit the F region");
+    static_assert(!CHUNK || VS != 1 || LD::CHX >= kChEnd + 2 * kChEnds, "chunk operator region");
     IMPC_WF double *chbuf() const { return lds + (VS == 1 ? LD::ch_off(T) : CH_OFF); }
     static_assert(!CHUNK || (CLAST >= 1 && CLAST <= CL), "chunk lengths");
 
@@ -796,6 +816,10 @@ struct WaveQP {
     // 3CL-1..2CL / 2CL-1..CL, P <- -F_k^T P with k descending); lane (i, j) holds P[i][j].  Then the
     // two-chunk operators of the last chunk's start, P2 P1, forward and backward.
     IMPC_WF void chunk_ops() {
+        if constexpr (NCH == 5) {
+            chunk_ops5();
+            return;
+        }
         const double *Fm = F();
         double *C = chbuf();
         const int w = L >> 6, l = L & 63, i = l >> 3, j = l & 7;
@@ -820,6 +844,54 @@ struct WaveQP {
             double v = 0.0;
             _Pragma("unroll") for (int m = 0; m < 8; m++) v += P2[8 * i + m] * P1[8 * m + j];
             C[(w == 0 ? kChFP21 : kChBT21) + l] = v;
+        }
+        wv.sync();
+    }
+
+    // P = the product of one chunk's step operators on one wavefront (lane (i, j) holds P[i][j]):
+    // forward steps o..o+CL-1, P <- -F_k P with k ascending; backward steps o+CL-1..o, P <- -F_k^T P
+    // with k descending
+    IMPC_WF void chunk_prod(bool fwd, int o, double *P, int l) {
+        const double *Fm = F();
+        const int i = l >> 3, j = l & 7;
+        P[l] = i == j ? 1.0 : 0.0;
+        wv.wsync();
+        for (int s = 0; s < CL; s++) {
+            const int k = fwd ? o + s : o + CL - 1 - s;
+            double pc[8];
+            _Pragma("unroll") for (int m = 0; m < 8; m++) pc[m] = P[8 * m + j];
+            double v = 0.0;
+            _Pragma("unroll") for (int m = 0; m < 8; m++) v -= (fwd ? f_el(Fm, k, i, m) : f_el(Fm, k, m, i)) * pc[m];
+            wv.wsync();
+            P[l] = v;
+            wv.wsync();
+        }
+    }
+    IMPC_WF static void mat8(const double *A, const double *B, double *out, int l) {  // out = A B
+        const int i = l >> 3, j = l & 7;
+        double v = 0.0;
+        _Pragma("unroll") for (int m = 0; m < 8; m++) v += A[8 * i + m] * B[8 * m + j];
+        out[l] = v;
+    }
+    // The five-chunk operators: forward chunks c = 1..3 start at c CL; backward chunks c = 1..3 (in
+    // sweep order) cover steps (5 - c) CL - 1 .. (4 - c) CL.  Six chunk products on four wavefronts,
+    // then the two-chunk products, then the three-chunk ones.
+    IMPC_WF void chunk_ops5() {
+        double *C = chbuf(), *Bk = C + kCh5B;
+        const int w = L >> 6, l = L & 63;
+        if (w < 3)
+            chunk_prod(true, (w + 1) * CL, C + kCh5P1 + 64 * w, l);
+        else
+            chunk_prod(false, 3 * CL, Bk + kCh5P1, l);
+        if (w < 2) chunk_prod(false, (2 - w) * CL, Bk + kCh5P2 + 64 * w, l);
+        wv.sync();
+        // w 0 / 1: forward P2 P1 / P3 P2; w 2 / 3: backward P2 P1 / P3 P2
+        double *X = w < 2 ? C : Bk;
+        mat8(X + kCh5P2 + 64 * (w & 1), X + kCh5P1 + 64 * (w & 1), X + kCh5P21 + 64 * (w & 1), l);
+        wv.sync();
+        if (w < 2) {  // w 0: forward P3 P2 P1, w 1: backward
+            double *Y = w ? Bk : C;
+            mat8(Y + kCh5P3, Y + kCh5P21, Y + kCh5P321, l);
         }
         wv.sync();
     }
@@ -1073,7 +1145,7 @@ struct WaveQP {
     // x_3CL / x_2CL / x_CL (x_2CL = x^_2CL + P1 x_3CL, x_CL = x^_CL + P2 x^_2CL + P2 P1 x_3CL).
     IMPC_WF void bwd_chunked(const double *eb, double *xb) {
         const double *C = chbuf();
-        double *ends = chbuf() + kChEnd + 16;
+        double *ends = chbuf() + kChEnd + kChEnds;
         const int w = L >> 6, l = lane_o() & 63, i = l >> 3, j = l & 7;
         constexpr int X3 = 13 * 3 * CL;     // x_3CL in xb (even stage: index i)
         constexpr bool LODD = (WF - 1) & 1;  // parity of the last chunk's first step W - 1
@@ -1098,6 +1170,69 @@ struct WaveQP {
         } else if (w == 3) {
             const double p = __builtin_fma(C[kChBT2 + l], ends[j],
                                            __builtin_fma(C[kChBT21 + l], xb[X3 + j], 0.125 * ends[8 + i]));
+            (void)bwd_run<true, CL, true>(eb, xb, 0, wv.sum_contig8(p));
+        }
+    }
+
+    // S2 in five chunks (NCH = 5): steps c CL .. c CL + CL - 1 (c = 0..3) and 4 CL .. W - 1; waves
+    // 1..3 run chunks 1..3 twice, wave 0 chunk 0 in round 1 and chunk 4 in round 2.
+    IMPC_WF void fwd_chunked5(const double *tb, double *rb) {
+        const double *C = chbuf();
+        double *ends = chbuf() + kChEnd;
+        const int w = L >> 6, l = lane_o() & 63, i = l >> 3, j = l & 7;
+        constexpr int A1 = 13 * CL;  // a_CL in rb (even stage: index i)
+        if (w == 0) {
+            (void)fwd_run<CL, true>(tb, rb, 0, 8.0 * tb[i]);  // a_0 = t_0 (tb holds t / 8)
+        } else {
+            const double e = fwd_run<CL, false>(tb, rb, w * CL, 0.0);
+            if (j == 0) ends[8 * (w - 1) + i] = e;
+        }
+        wv.lsync();
+        if (w == 1) {
+            (void)fwd_run<CL, true>(tb, rb, CL, rb[A1 + i]);
+        } else if (w == 2) {
+            const double a = wv.sum_contig8(__builtin_fma(C[kCh5P1 + l], rb[A1 + j], 0.125 * ends[i]));
+            (void)fwd_run<CL, true>(tb, rb, 2 * CL, a);
+        } else if (w == 3) {
+            const double p = __builtin_fma(C[kCh5P2 + l], ends[j],
+                                           __builtin_fma(C[kCh5P21 + l], rb[A1 + j], 0.125 * ends[8 + i]));
+            (void)fwd_run<CL, true>(tb, rb, 3 * CL, wv.sum_contig8(p));
+        } else {
+            const double p = __builtin_fma(
+                C[kCh5P3 + l], ends[8 + j],
+                __builtin_fma(C[kCh5P32 + l], ends[j], __builtin_fma(C[kCh5P321 + l], rb[A1 + j], 0.125 * ends[16 + i])));
+            (void)fwd_run<CLAST, true>(tb, rb, 4 * CL, wv.sum_contig8(p));
+        }
+    }
+
+    // S4 in five chunks: steps W-1..4CL (wave 0, round 1, from x_W), 4CL-1..3CL / 3CL-1..2CL /
+    // 2CL-1..CL (waves 1..3, both rounds), CL-1..0 (wave 0, round 2).
+    IMPC_WF void bwd_chunked5(const double *eb, double *xb) {
+        const double *C = chbuf() + kCh5B;
+        double *ends = chbuf() + kChEnd + kChEnds;
+        const int w = L >> 6, l = lane_o() & 63, i = l >> 3, j = l & 7;
+        constexpr int X4 = 13 * 4 * CL;      // x_4CL in xb (even stage: index i)
+        constexpr bool LODD = (WF - 1) & 1;  // parity of the first chunk's first step W - 1
+        if (w == 0) {
+            (void)bwd_run<LODD, CLAST, true>(eb, xb, 4 * CL, 8.0 * eb[13 * WF + (LODD ? i : j)]);
+        } else {
+            const double e = bwd_run<true, CL, false>(eb, xb, (4 - w) * CL, 0.0);
+            if (j == 0) ends[8 * (w - 1) + i] = e;
+        }
+        wv.lsync();
+        if (w == 1) {
+            (void)bwd_run<true, CL, true>(eb, xb, 3 * CL, xb[X4 + i]);
+        } else if (w == 2) {
+            const double x = wv.sum_contig8(__builtin_fma(C[kCh5P1 + l], xb[X4 + j], 0.125 * ends[i]));
+            (void)bwd_run<true, CL, true>(eb, xb, 2 * CL, x);
+        } else if (w == 3) {
+            const double p = __builtin_fma(C[kCh5P2 + l], ends[j],
+                                           __builtin_fma(C[kCh5P21 + l], xb[X4 + j], 0.125 * ends[8 + i]));
+            (void)bwd_run<true, CL, true>(eb, xb, CL, wv.sum_contig8(p));
+        } else {
+            const double p = __builtin_fma(
+                C[kCh5P3 + l], ends[8 + j],
+                __builtin_fma(C[kCh5P32 + l], ends[j], __builtin_fma(C[kCh5P321 + l], xb[X4 + j], 0.125 * ends[16 + i])));
             (void)bwd_run<true, CL, true>(eb, xb, 0, wv.sum_contig8(p));
         }
     }
@@ -1161,7 +1296,9 @@ struct WaveQP {
             // leave their SIMD's issue slots to the co-resident team.
             // (a_0 = t_0 = r_0[:8] is already in rb: stage 0 has no coupling, so S1 left it as is)
             // The long horizon's W = 39 instance runs it in chunks on all four wavefronts (CHUNK).
-            if constexpr (CHUNK) {
+            if constexpr (CHUNK && NCH == 5) {
+                fwd_chunked5(tb, rb);
+            } else if constexpr (CHUNK) {
                 fwd_chunked(tb, rb);
             } else if ((L >> 6) == rw) {
                 if (W == LD::WSPEC)
@@ -1191,7 +1328,9 @@ struct WaveQP {
             // S4: backward 8-dim recursion x_k[:8] = e_k[:8] - F_k' x_{k+1}[:8] on the same grid and
             // stored layout: even steps reduce over j (contiguous), odd steps over i (strided).
             if (L < 8) xb[13 * W + L] = 8.0 * eb[13 * W + L];
-            if constexpr (CHUNK) {
+            if constexpr (CHUNK && NCH == 5) {
+                bwd_chunked5(eb, xb);
+            } else if constexpr (CHUNK) {
                 bwd_chunked(eb, xb);
             } else if ((L >> 6) == rw) {
                 if (W == LD::WSPEC)
