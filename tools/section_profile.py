@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Per-section cycle breakdown of the structured kernel (profiling build, `make prof`).
 
-usage: IMPC_SECTION_PROF=1 python tools/section_profile.py [instances]
-Runs the bench workload (intent_config, N=20) once and prints, per section, the time (100 MHz
+usage: IMPC_SECTION_PROF=1 python tools/section_profile.py [instances [N [K]]]
+Runs the bench workload (intent_config, N=20, K=8/9; or horizon N with K/K+1 obstacles) once and prints, per section, the time (100 MHz
 s_memrealtime ticks -> ns) seen by lane 0 of each team, summed over QPs, normalised per QP and per
 ADMM iteration.
 """
@@ -24,9 +24,11 @@ NAMES = ["setup", "factor", "warm", "rhs", "S1", "fwd", "S3", "bwd", "S5", "upda
 
 def main():
     inst = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    kw = dict(N=N, K=int(sys.argv[3])) if len(sys.argv) > 3 else (dict(N=N) if N != 20 else {})
     assert "prof" in os.path.basename(impc.LIB_PATH)
     impc.lib.impc_debug_sections.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
-    buckets = scenarios.intent_config(instances=inst, seed=3000)
+    buckets = scenarios.intent_config(instances=inst, seed=3000, **kw)
     ctx = impc.Context(0)
     s = impc.default_settings(verbose=0)
     for K, bk in sorted(buckets.items()):
