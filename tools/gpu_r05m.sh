@@ -10,3 +10,6 @@ timeout -k 10 300 python -u tools/section_profile.py 1024 30 8 > $O/sec_n30.txt 
 cat $O/sec_n30.txt
 timeout -k 10 300 python -u tools/section_profile.py 2048 > $O/sec_n20.txt 2>&1 || { tail -20 $O/sec_n20.txt; exit 1; }
 cat $O/sec_n20.txt
+unset IMPC_SECTION_PROF
+timeout -k 10 600 python -u tools/live_loop.py > $O/live_loop.json 2> $O/live_loop.err || { tail -20 $O/live_loop.err; exit 1; }
+cat $O/live_loop.json
