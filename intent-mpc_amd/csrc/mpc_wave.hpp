@@ -70,6 +70,14 @@ namespace impc {
 #ifndef IMPC_CHUNK5
 #define IMPC_CHUNK5 1
 #endif
+// The factorisation's latency form (round 5; IMPC_FACT2=0: the round-4 loops, A/B variants only):
+// assembly codes loaded four at a time with the next stage's ranges prefetched, the Gauss-Jordan
+// steps' operands read at once, the 13-term products unrolled.  The long shape's setup runs one
+// team per CU, so these latencies are exposed: setup 0.440 -> 0.358 ms per N = 40 QP, config 5's
+// closed loop 626 -> 608 ms per step (profiles/r05/exp_phase/README.md)
+#ifndef IMPC_FACT2
+#define IMPC_FACT2 1
+#endif
 #define IMPC_REP(X) for (int rep_ = 0; rep_ < (IMPC_DUP == (X) ? 2 : 1); rep_++)
 // Branch counters of the CPU emulation's instrumented builds (tools only; nothing in the product)
 #ifndef IMPC_COUNT
@@ -675,16 +683,58 @@ struct WaveQP {
         }
         wv.sync();
         int bad = 0;
+#if IMPC_FACT2
+        // the assembly program's range of each of this lane's destinations, one stage ahead (a
+        // global load; the long shape runs one team per CU, so nothing hides its latency)
+        constexpr int ND = (kStageDests + NL - 1) / NL;
+        int32_t tp[ND][2];
+        auto load_tp = [&](int k) {
+            _Pragma("unroll") for (int u = 0; u < ND; u++) {
+                const int d = L + NL * u;
+                const bool ok = d < kStageDests && k < N;
+                tp[u][0] = ok ? T.term_ptr[(int64_t)k * kStageDests + d] : 0;
+                tp[u][1] = ok ? T.term_ptr[(int64_t)k * kStageDests + d + 1] : 0;
+            }
+        };
+        load_tp(0);
+#endif
         for (int k = 0; k < N; k++) {
             const int sz = k < W ? 13 : 8;
             // assemble M_kk and Bbar_k
+#if IMPC_FACT2
+            int32_t tc[ND][2];
+            _Pragma("unroll") for (int u = 0; u < ND; u++) tc[u][0] = tp[u][0], tc[u][1] = tp[u][1];
+            load_tp(k + 1);
+            _Pragma("unroll") for (int u = 0; u < ND; u++) {
+                const int d = L + NL * u;
+                if (d >= kStageDests) continue;
+#else
             for (int d = L; d < kStageDests; d += NL) {
+#endif
                 const bool isB = d >= 169;
                 if (isB && k == W) continue;
                 const int dd = isB ? d - 169 : d;
                 const int r = dd / 13, cc = dd % 13;
                 double val = 0.0;
                 if (isB || (r < sz && cc < sz)) {
+#if IMPC_FACT2
+                    // the codes four at a time, their LDS operands before the products (the sum
+                    // keeps its term order)
+                    const int32_t t0 = tc[u][0], t1 = tc[u][1];
+                    for (int32_t t = t0; t < t1; t += 4) {
+                        int32_t cd[4];
+                        _Pragma("unroll") for (int v = 0; v < 4; v++) cd[v] = t + v < t1 ? T.term[t + v] : 0;
+                        double rg[4], we[4], wf[4];
+                        _Pragma("unroll") for (int v = 0; v < 4; v++) {
+                            const int32_t g = cd[v] >> 4, e = (cd[v] >> 2) & 3, f = cd[v] & 3;
+                            rg[v] = rhog[g];
+                            we[v] = w[4 * g + e];
+                            wf[v] = w[4 * g + f];
+                        }
+                        _Pragma("unroll") for (int v = 0; v < 4; v++)
+                            if (t + v < t1) val += rg[v] * we[v] * wf[v];
+                    }
+#else
                     const int32_t t0 = T.term_ptr[(int64_t)k * kStageDests + d];
                     const int32_t t1 = T.term_ptr[(int64_t)k * kStageDests + d + 1];
                     for (int32_t t = t0; t < t1; t++) {
@@ -692,6 +742,7 @@ struct WaveQP {
                         int32_t g = code >> 4, e = (code >> 2) & 3, f = code & 3;
                         val += rhog[g] * w[4 * g + e] * w[4 * g + f];
                     }
+#endif
                     if (!isB && r == cc) val += diagx[13 * k + r];
                     if (!isB && k > 0 && r < 8 && cc < 8) val -= E[8 * r + cc];  // Schur complement
                 }
@@ -721,6 +772,33 @@ struct WaveQP {
                         if (gi >= sz || gc >= sz) continue;
                         const int i = last && gc > gi ? gc : gi, c = last && gc > gi ? gi : gc;
                         double v;
+#if IMPC_FACT2
+                        // every operand read at once (one LDS round trip per step), the lane's
+                        // case selected after: the same expressions as below
+                        const double p00 = src[13 * j + j], p01 = src[13 * j + (two ? j + 1 : j)];
+                        const double p10 = src[13 * (two ? j + 1 : j) + j], p11 = src[13 * (two ? j + 1 : j) + (two ? j + 1 : j)];
+                        const double s0 = src[13 * j + c], s1 = src[13 * (two ? j + 1 : j) + c];
+                        const double a0 = src[13 * i + j], a1 = src[13 * i + (two ? j + 1 : j)];
+                        const double sic = src[13 * i + c];
+                        if (two) {
+                            const double det = p00 * p11 - p01 * p10;
+                            if (!(p00 > 0.0) || !(det > 0.0)) bad = 1;
+                            const double rd = 1.0 / det;
+                            const double q00 = p11 * rd, q01 = -(p01 * rd), q10 = -(p10 * rd), q11 = p00 * rd;
+                            const int ri = i - j, ci = c - j;
+                            const bool iJ = ri == 0 || ri == 1, cJ = ci == 0 || ci == 1;
+                            const double vq = ri == 0 ? (ci == 0 ? q00 : q01) : (ci == 0 ? q10 : q11);
+                            const double vr = ri == 0 ? q00 * s0 + q01 * s1 : q10 * s0 + q11 * s1;
+                            const double u0 = a0 * q00 + a1 * q10, u1 = a0 * q01 + a1 * q11;
+                            const double vc = -(ci == 0 ? u0 : u1);
+                            const double vi = sic - (u0 * s0 + u1 * s1);
+                            v = iJ ? (cJ ? vq : vr) : (cJ ? vc : vi);
+                        } else {
+                            if (!(p00 > 0.0)) bad = 1;
+                            const double r = 1.0 / p00;
+                            v = i == j ? (c == j ? r : s0 * r) : (c == j ? -(a0 * r) : sic - (a0 * r) * s0);
+                        }
+#else
                         if (two) {
                             const double p00 = src[13 * j + j], p01 = src[13 * j + j + 1];
                             const double p10 = src[13 * (j + 1) + j], p11 = src[13 * (j + 1) + j + 1];
@@ -756,6 +834,7 @@ struct WaveQP {
                             else
                                 v = src[13 * i + c] - (src[13 * i + j] * r) * src[13 * j + c];
                         }
+#endif
                         (last ? Ai : dst)[13 * gi + gc] = v;
                     }
                     wv.sync();
@@ -771,6 +850,9 @@ struct WaveQP {
                 for (int p = L; p < 104; p += NL) {
                     int i = p / 13, cc = p % 13;
                     double s = 0.0;
+#if IMPC_FACT2
+                    _Pragma("unroll")
+#endif
                     for (int t = 0; t < 13; t++) s += Bb[13 * i + t] * Ai[13 * t + cc];
                     G[p] = s;
                 }
@@ -778,6 +860,9 @@ struct WaveQP {
                 if (L < 64) {
                     int i = L >> 3, j = L & 7;
                     double s = 0.0;
+#if IMPC_FACT2
+                    _Pragma("unroll")
+#endif
                     for (int t = 0; t < 13; t++) s += G[13 * i + t] * Bb[13 * j + t];
                     E[8 * i + j] = s;
                     // recursion layout: lane (i,j) of step k reads F_k[j][i] when the column index

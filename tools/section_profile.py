@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-section cycle breakdown of the structured kernel (profiling build, `make prof`).
 
-usage: IMPC_SECTION_PROF=1 python tools/section_profile.py [instances [N [K]]]
+usage: IMPC_SECTION_PROF=1 python tools/section_profile.py [instances [N [K [max_iter]]]]
 Runs the bench workload (intent_config, N=20, K=8/9; or horizon N with K/K+1 obstacles) once and prints, per section, the time (100 MHz
 s_memrealtime ticks -> ns) seen by lane 0 of each team, summed over QPs, normalised per QP and per
 ADMM iteration.
@@ -26,11 +26,12 @@ def main():
     inst = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
     N = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     kw = dict(N=N, K=int(sys.argv[3])) if len(sys.argv) > 3 else (dict(N=N) if N != 20 else {})
+    mi = int(sys.argv[4]) if len(sys.argv) > 4 else 4000  # max_iter = 1: the setup's sections alone
     assert "prof" in os.path.basename(impc.LIB_PATH)
     impc.lib.impc_debug_sections.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
     buckets = scenarios.intent_config(instances=inst, seed=3000, **kw)
     ctx = impc.Context(0)
-    s = impc.default_settings(verbose=0)
+    s = impc.default_settings(verbose=0, max_iter=mi)
     for K, bk in sorted(buckets.items()):
         pat, v = bk["pattern"], bk["values"]
         B = v["q"].shape[0]
@@ -50,7 +51,7 @@ def main():
         print(f"K={K} B={B} kernel {b.timings()[1]:.1f} ms, mean iter {iters / B:.1f}, "
               f"us/QP {tot_ns / B / 1e3:.1f}, ns/iter {tot_ns / iters:.0f}")
         for i, nm in enumerate(NAMES):
-            print(f"  {nm:9s} {100 * sec[i] / tot:5.1f}%  per-iter {per_ns[i] / iters:8.0f} ns")
+            print(f"  {nm:9s} {100 * sec[i] / tot:5.1f}%  per-iter {per_ns[i] / iters:8.0f} ns  per-QP {per_ns[i] / B / 1e3:8.2f} us")
         b.close()
     ctx.close()
 
