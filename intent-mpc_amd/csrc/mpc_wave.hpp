@@ -618,8 +618,16 @@ struct WaveQP {
                     qn = dmax(fabs(q[s]), qn);
                 }
             }
+#if IMPC_FACT2
+            // both cost norms in one team reduction (the same combine orders as sum / max)
+            double mx1[1] = {qn}, sm1[1] = {psum};
+            wv.max_sum_n(mx1, sm1);
+            double ct = sm1[0] / (double)n;
+            qn = mx1[0];
+#else
             double ct = wv.sum(psum) / (double)n;
             qn = wv.max(qn);
+#endif
             qn = qn < kMinScaling ? 1.0 : qn;
             qn = qn > kMaxScaling ? kMaxScaling : qn;
             ct = dmax(ct, qn);
@@ -637,7 +645,10 @@ struct WaveQP {
                 q[s] *= ct;
             }
             c *= ct;
-            wv.sync();
+#if !IMPC_FACT2
+            wv.sync();  // (redundant: the team reduction's barriers already order this pass's reads
+                        // of pb / xb before the next pass's writes)
+#endif
         }
         c = wv.uniform(c);
         cinv = 1. / c;
