@@ -26,6 +26,30 @@ from test_replan_branches import _check_replan
 pytestmark = pytest.mark.gpu
 
 
+def _dump_failure(rp, r, out, plan_x_before, ft_before, pos, vel, xref, sc):
+    """A failed replan's inputs and device outputs, for offline analysis: the state the host checked
+    against (plan_x before the replan), the device's state and linearisation points now, every
+    assembled value and solution of the replan (gpurun_out/live_loop_failure_r<r>.npz)."""
+    import os
+    from impc.replan import _get
+    try:
+        v = rp.view()
+        states = _get(rp.ctx, v.plan_states, (rp.I + 1, rp.N * 8), np.float64)
+        px, ft, pc, valid = rp.plans()
+        arrs = {k: np.asarray(val) for k, val in out.items()
+                if isinstance(val, np.ndarray) and val.dtype != object}
+        for k, val in out.items():
+            if isinstance(val, (list, tuple)) and val and isinstance(val[0], np.ndarray):
+                for j, a in enumerate(val):
+                    arrs[f"{k}_{j}"] = a
+        os.makedirs("gpurun_out", exist_ok=True)
+        np.savez(f"gpurun_out/live_loop_failure_r{r}.npz", plan_x_before=plan_x_before, ft_before=ft_before,
+                 pos=pos, vel=vel, xref=xref, plan_states_now=states, plan_x_now=px, pred_pos=sc["pred_pos"][r],
+                 dyn_cur=sc["dyn_cur"][r], pred_size=sc["pred_size"], prob=sc["prob"], **arrs)
+    except Exception as ex:  # the dump must not mask the assertion
+        print("live-loop failure dump:", ex)
+
+
 def test_live_loop_thirty_replans_on_the_benchmark_path(ctx):
     I, K, R, N = 6, 3, 30, 30
     sc = scenarios.live_loop(I, K, R, N=N, seed=4100)
@@ -56,6 +80,7 @@ def test_live_loop_thirty_replans_on_the_benchmark_path(ctx):
                                                      sc["pred_pos"][r], sc["pred_size"], sc["prob"], np.ones(I, bool),
                                                      None, np.zeros(I, np.int32), pd, s)
             except AssertionError as e:
+                _dump_failure(rp, r, out, plan_x, ft, pos, vel, xref, sc)
                 raise AssertionError(f"replan {r}: {e}") from e
             plan_x, ft_new, _, valid = rp.plans()
             np.testing.assert_array_equal(plan_x, expect, err_msg=f"replan {r}: committed plans")
