@@ -23,7 +23,7 @@ struct Args {
     const double *prev;
     const int32_t *prev_count;
     const double *dyn_cur, *pred_pos, *pred_size, *prob;
-    int32_t *ob_idx, *cand_type, *cand_slot, *max_intent;  // max_intent: scratch [I][K]
+    int32_t *ob_idx, *cand_type, *cand_slot;
     double *closest_prob, *single_pos, *single_size, *pair_pos, *pair_size;
 };
 
@@ -89,13 +89,15 @@ __global__ __launch_bounds__(64) void k_fanout_pick(Args a) {
         a.cand_slot[6 * i + c] = t < 4 ? ns_++ : 4 + np_++;
     }
     for (int q = 0; q < 4; q++) a.closest_prob[4 * i + q] = pr[q];
-    for (int k = 0; k < K; k++) {  // maxCoeff (:762)
-        const double *p = a.prob + (i * K + k) * 4;
-        int m = 0;
-        for (int q = 1; q < 4; q++)
-            if (p[q] > p[m]) m = q;
-        a.max_intent[i * K + k] = m;
-    }
+}
+
+// maxCoeff (:762): the first most probable intent of obstacle k of instance i
+__device__ inline int max_intent(const double *prob, int64_t i, int K, int k) {
+    const double *p = prob + (i * K + k) * 4;
+    int m = 0;
+    for (int q = 1; q < 4; q++)
+        if (p[q] > p[m]) m = q;
+    return m;
 }
 
 __global__ __launch_bounds__(256) void k_fanout_copy(Args a) {
@@ -126,7 +128,7 @@ __global__ __launch_bounds__(256) void k_fanout_copy(Args a) {
         } else {  // other obstacles in index order (:759-768)
             const int q = o - nfirst;
             k = q < ob ? q : q + 1;
-            intent = a.max_intent[i * K + k];
+            intent = max_intent(a.prob, i, K, k);
         }
         const int64_t src = (((i * K + k) * 4 + intent) * (int64_t)L + st) * 3;
         double *dp = pair ? a.pair_pos : a.single_pos, *ds = pair ? a.pair_size : a.single_size;
@@ -216,10 +218,10 @@ extern "C" int impc_intent_fanout_device(impc_ctx ctx, int64_t instances, int32_
         return fail(IMPC_INVALID_ARGUMENT, "fanout: null argument");
     HIP_OK(hipSetDevice(ctx->device));
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
-    int32_t *maxint = nullptr;
-    HIP_OK(hipMallocAsync((void **)&maxint, sizeof(int32_t) * (size_t)instances * num_obstacles, st));
+    // (no scratch: the other obstacles' most probable intents are recomputed where they are used;
+    // a stream-ordered hipMallocAsync scratch for them was read back as zeros on some calls)
     impc_fanout::Args a{instances, num_obstacles, pred_len, prev_len, curr_pos, first_time, prev_states,
-                        prev_count, dyn_cur, pred_pos, pred_size, prob, ob_idx, cand_type, cand_slot, maxint,
+                        prev_count, dyn_cur, pred_pos, pred_size, prob, ob_idx, cand_type, cand_slot,
                         closest_prob, single_pos, single_size, pair_pos, pair_size};
     hipLaunchKernelGGL(impc_fanout::k_fanout_pick, dim3((unsigned)((instances + 63) / 64)), dim3(64), 0, st, a);
     HIP_OK(hipGetLastError());
@@ -227,7 +229,6 @@ extern "C" int impc_intent_fanout_device(impc_ctx ctx, int64_t instances, int32_
     const int64_t blocks = std::min<int64_t>((rows + 255) / 256, (int64_t)ctx->num_cu * 16);
     hipLaunchKernelGGL(impc_fanout::k_fanout_copy, dim3((unsigned)blocks), dim3(256), 0, st, a);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipFreeAsync(maxint, st));
     return IMPC_OK;
 }
 
