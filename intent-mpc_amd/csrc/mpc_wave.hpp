@@ -78,6 +78,25 @@ namespace impc {
 #ifndef IMPC_FACT2
 #define IMPC_FACT2 1
 #endif
+// A/B knobs of that form (variants only): the 13-term products' unroll count (0 = full) and the
+// assembly's codes per batch
+#ifndef IMPC_F2U
+#define IMPC_F2U 0
+#endif
+// The long shape's factorisation (IMPC_FACT3, on for VS = 3 only): the Schur complement E_k kept
+// in the register of the lane that assembles M_k+1's matching entry (the destinations are assigned
+// so that lane 8i + j computes E[i][j] and assembles M[i][j]), B_k double-buffered by stage parity,
+// and the barrier between E_k and the next stage's assembly dropped.  Config 5's closed loop
+// 610.9 -> 604.0 ms; on the default horizon it measured 214.3 -> 215.2 ms, so that shape keeps the
+// barrier (profiles/r05/exp_phase/README.md)
+#ifndef IMPC_FACT3
+#define IMPC_FACT3 1
+#endif
+#define IMPC_PRAGMA_(x) _Pragma(#x)
+#define IMPC_PRAGMA(x) IMPC_PRAGMA_(x)
+#ifndef IMPC_F2B
+#define IMPC_F2B 4
+#endif
 #define IMPC_REP(X) for (int rep_ = 0; rep_ < (IMPC_DUP == (X) ? 2 : 1); rep_++)
 // Branch counters of the CPU emulation's instrumented builds (tools only; nothing in the product)
 #ifndef IMPC_COUNT
@@ -240,6 +259,9 @@ struct WaveLds {
                          DIAGX = FE + 64;
     // general rows' rho during the factorisation: products region + 4 mg
     static_assert(DIAGX + NMAX <= RED_OFF, "factorisation scratch does not fit");
+    // the coupling block of odd stages (IMPC_FACT3: B_k double-buffered by stage parity)
+    static constexpr int FB2 = DIAGX + NMAX;
+    static_assert(VS != 3 || FB2 + 104 <= RED_OFF, "factorisation scratch does not fit");
 };
 
 struct WaveRho {
@@ -381,6 +403,7 @@ struct WaveQP {
     // true starts and wave 0 the fifth, whose start a_4CL = a^_4CL + P3 a^_3CL + P3P2 a^_2CL +
     // P3P2P1 a_CL is still one 8-lane reduction.  Chain per sweep: 2 CL steps and one reduction
     // (W = 39: 16 instead of 20).
+    static constexpr bool F3 = IMPC_FACT2 && IMPC_FACT3 && VS == 3;
     static constexpr int NCH = (WF > 0 && VS == 3 && IMPC_CHUNK5) ? 5 : 4;
     static constexpr bool CHUNK = WF > 0 && NL == 256 && (VS == 3 || (VS == 1 && IMPC_CHUNK19 != 0));
     static constexpr int CL = WF > 0 ? (NCH == 5 ? 2 * ((WF + 9) / 10) : 2 * ((WF + 7) / 8)) : 2;
@@ -566,13 +589,26 @@ struct WaveQP {
         _Pragma("unroll") for (int s = 0; s < GS; s++) Eg[s] = 1.0;
         c = 1.0;
         double *pb = pbuf(), *xb = xbuf();
+#if IMPC_FACT2
+        // |A| entries of the general rows -> products buffer: pass 0's here, each later pass's at
+        // the end of the pass before (after its scaling), ordered by that pass's team reduction
+        if (st.scaling > 0) {
+            _Pragma("unroll") for (int s = 0; s < GS; s++) {
+                if (gok[s])
+                    _Pragma("unroll") for (int e = 0; e < 4; e++) pb[gdst(s, e)] = fabs(a[s][e]);
+            }
+            wv.sync();
+        }
+#endif
         for (int it = 0; it < st.scaling; it++) {
+#if !IMPC_FACT2
             // |A| entries of general rows -> products buffer
             _Pragma("unroll") for (int s = 0; s < GS; s++) {
                 if (gok[s])
                     _Pragma("unroll") for (int e = 0; e < 4; e++) pb[gdst(s, e)] = fabs(a[s][e]);
             }
             wv.sync();
+#endif
             double Dt[VS], Etb[VS], Etg[GS];
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
                 // colnorm_sym(P) (diagonal), max with colnorm(A) = max(box, general entries)
@@ -610,6 +646,14 @@ struct WaveQP {
                 _Pragma("unroll") for (int e = 0; e < 4; e++) a[s][e] = (a[s][e] * Etg[s]) * xb[gcol(s, e)];
                 Eg[s] = Eg[s] * Etg[s];
             }
+#if IMPC_FACT2
+            // the next pass's |A| (every read of this pass's came before the D_temp barrier)
+            if (it + 1 < st.scaling)
+                _Pragma("unroll") for (int s = 0; s < GS; s++) {
+                    if (gok[s])
+                        _Pragma("unroll") for (int e = 0; e < 4; e++) pb[gdst(s, e)] = fabs(a[s][e]);
+                }
+#endif
             // cost normalisation
             double psum = 0.0, qn = 0.0;
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
@@ -674,11 +718,24 @@ struct WaveQP {
 
     // ------------------------------------------------------------ block factorisation
     // Returns 1 if a pivot is not positive (OSQP_NONCVX_ERROR).
+    // the factorisation assembly's destination of slot r = L + NL u (0 <= r < kStageDests): the
+    // identity, or (IMPC_FACT3) slots 0..63 on the 8 x 8 Schur block M[i][j] (13 i + j, lane 8 i + j),
+    // the rest in order over the other 209 (M rows 0..7 columns 8..12, M rows 8..12, then B)
+    IMPC_WF static int stage_dest(int r) {
+        if constexpr (F3) {
+            if (r < 64) return 13 * (r >> 3) + (r & 7);
+            const int c = r - 64;
+            return c < 40 ? 13 * (c / 5) + 8 + c % 5 : 104 + (c - 40);
+        }
+        return r;
+    }
+
     IMPC_WF int factorize() {
         const int n = T.n, W = Wst(), N = W + 1;
         double *w = pbuf(), *rhog = pbuf() + 4 * T.mg, *diagx = lds + LD::DIAGX;
         double *A = lds + LD::FA, *Li = lds + LD::FL, *Ai = lds + LD::FI, *Bb = lds + LD::FB, *G = lds + LD::FG,
                *E = lds + LD::FE, *Fm = F();
+        double e_reg = 0.0;  // F3: E_k-1[L >> 3][L & 7] (lanes < 64)
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
             int g = NL * s + L;
             if (gok[s]) {
@@ -701,7 +758,7 @@ struct WaveQP {
         int32_t tp[ND][2];
         auto load_tp = [&](int k) {
             _Pragma("unroll") for (int u = 0; u < ND; u++) {
-                const int d = L + NL * u;
+                const int d = stage_dest(L + NL * u);
                 const bool ok = d < kStageDests && k < N;
                 tp[u][0] = ok ? T.term_ptr[(int64_t)k * kStageDests + d] : 0;
                 tp[u][1] = ok ? T.term_ptr[(int64_t)k * kStageDests + d + 1] : 0;
@@ -711,14 +768,15 @@ struct WaveQP {
 #endif
         for (int k = 0; k < N; k++) {
             const int sz = k < W ? 13 : 8;
+            if constexpr (F3) Bb = lds + ((k & 1) ? LD::FB2 : LD::FB);
             // assemble M_kk and Bbar_k
 #if IMPC_FACT2
             int32_t tc[ND][2];
             _Pragma("unroll") for (int u = 0; u < ND; u++) tc[u][0] = tp[u][0], tc[u][1] = tp[u][1];
             load_tp(k + 1);
             _Pragma("unroll") for (int u = 0; u < ND; u++) {
-                const int d = L + NL * u;
-                if (d >= kStageDests) continue;
+                if (L + NL * u >= kStageDests) continue;
+                const int d = stage_dest(L + NL * u);
 #else
             for (int d = L; d < kStageDests; d += NL) {
 #endif
@@ -732,17 +790,17 @@ struct WaveQP {
                     // the codes four at a time, their LDS operands before the products (the sum
                     // keeps its term order)
                     const int32_t t0 = tc[u][0], t1 = tc[u][1];
-                    for (int32_t t = t0; t < t1; t += 4) {
-                        int32_t cd[4];
-                        _Pragma("unroll") for (int v = 0; v < 4; v++) cd[v] = t + v < t1 ? T.term[t + v] : 0;
-                        double rg[4], we[4], wf[4];
-                        _Pragma("unroll") for (int v = 0; v < 4; v++) {
+                    for (int32_t t = t0; t < t1; t += IMPC_F2B) {
+                        int32_t cd[IMPC_F2B];
+                        _Pragma("unroll") for (int v = 0; v < IMPC_F2B; v++) cd[v] = t + v < t1 ? T.term[t + v] : 0;
+                        double rg[IMPC_F2B], we[IMPC_F2B], wf[IMPC_F2B];
+                        _Pragma("unroll") for (int v = 0; v < IMPC_F2B; v++) {
                             const int32_t g = cd[v] >> 4, e = (cd[v] >> 2) & 3, f = cd[v] & 3;
                             rg[v] = rhog[g];
                             we[v] = w[4 * g + e];
                             wf[v] = w[4 * g + f];
                         }
-                        _Pragma("unroll") for (int v = 0; v < 4; v++)
+                        _Pragma("unroll") for (int v = 0; v < IMPC_F2B; v++)
                             if (t + v < t1) val += rg[v] * we[v] * wf[v];
                     }
 #else
@@ -755,7 +813,8 @@ struct WaveQP {
                     }
 #endif
                     if (!isB && r == cc) val += diagx[13 * k + r];
-                    if (!isB && k > 0 && r < 8 && cc < 8) val -= E[8 * r + cc];  // Schur complement
+                    if (!isB && k > 0 && r < 8 && cc < 8)  // Schur complement (F3: this lane's E)
+                        val -= F3 ? e_reg : E[8 * r + cc];
                 }
                 if (isB)
                     Bb[dd] = val;
@@ -861,8 +920,10 @@ struct WaveQP {
                 for (int p = L; p < 104; p += NL) {
                     int i = p / 13, cc = p % 13;
                     double s = 0.0;
-#if IMPC_FACT2
+#if IMPC_FACT2 && IMPC_F2U == 0
                     _Pragma("unroll")
+#elif IMPC_FACT2
+                    IMPC_PRAGMA(unroll IMPC_F2U)
 #endif
                     for (int t = 0; t < 13; t++) s += Bb[13 * i + t] * Ai[13 * t + cc];
                     G[p] = s;
@@ -871,11 +932,16 @@ struct WaveQP {
                 if (L < 64) {
                     int i = L >> 3, j = L & 7;
                     double s = 0.0;
-#if IMPC_FACT2
+#if IMPC_FACT2 && IMPC_F2U == 0
                     _Pragma("unroll")
+#elif IMPC_FACT2
+                    IMPC_PRAGMA(unroll IMPC_F2U)
 #endif
                     for (int t = 0; t < 13; t++) s += G[13 * i + t] * Bb[13 * j + t];
-                    E[8 * i + j] = s;
+                    if constexpr (F3)
+                        e_reg = s;
+                    else
+                        E[8 * i + j] = s;
                     // recursion layout: lane (i,j) of step k reads F_k[j][i] when the column index
                     // sits on i (k even), F_k[i][j] otherwise
                     Fm[64 * k + 8 * i + j] = !(k & 1) ? G[13 * j + i] : G[13 * i + j];
@@ -887,7 +953,7 @@ struct WaveQP {
                     if (vs_[s] == k + 1 && vr_[s] < 8)
                         _Pragma("unroll") for (int j = 0; j < 8; j++) cp[s][j] = j < 5 ? G[13 * vr_[s] + 8 + j] : 0.0;
                 }
-                wv.sync();
+                if constexpr (!F3) wv.sync();
             }
             IMPC_SEC(kSecFDense);
         }
