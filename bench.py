@@ -440,7 +440,9 @@ def main():
     values_mode = "shared" if len(nvar) == len(batches) else "full"
     nvar_desc = {str(bk["K"]): nv for (bk, _), nv in zip(batches, nvar)} if values_mode == "shared" else None
     build_id = impc.lib.impc_build_id().decode()
-    traffic, traffic_src = measured_traffic(build_id, total_qps, kernel_name, values_mode, args.workload)
+    # the PMC summary is keyed on the workload as timed: config 5's full-setup study is another workload
+    pmc_workload = "config5_fullsetup" if (args.workload == "config5" and not args.receding) else args.workload
+    traffic, traffic_src = measured_traffic(build_id, total_qps, kernel_name, values_mode, pmc_workload)
 
     e2e = e2e_serial = None
     if args.e2e_steps > 0 and receding is None:
@@ -456,7 +458,7 @@ def main():
         # equal the timed run's bit for bit), recording every step's iterations / statuses and the
         # CPU sample's per-step q, l, u for the oracle
         k_sample = min(args.cpu_sample, 1024) if (rank == 0 and world == 1) else 0
-        rec = receding.replay(k_sample)
+        rec = receding.replay(k_sample, persist=bool(k_sample))
         per_step = rec["per_step"]
         per_step_det = all(np.array_equal(r[0], x) and np.array_equal(r[2]["iter"], inf["iter"])
                            for r, (x, _, inf) in zip(rec["last"], results))
@@ -464,17 +466,16 @@ def main():
         if k_sample:
             cpu, ref = cpu_baseline_receding(bks, settings, rec, args.cpu_threads)
             # parity: the first closed-loop step (setup + solve, then osqp_update_A / _lin_cost /
-            # _bounds + solve on both sides from identical inputs); later steps resume from each side's
-            # own persistent iterates, which independent implementations carry ~1e-12 apart, so their
-            # agreement is reported per step as information
+            # _bounds + solve on both sides from identical inputs), and every later step from the same
+            # starting point -- the oracle re-synchronised to the device's persisted state (chain)
             got = [[e["got"][t] for e in rec["buckets"]] for t in range(len(rec["per_step"]))]
             parity = parity_vs_oracle(got[0], [r[0] for r in ref])
             parity["what"] = ("the first closed-loop step's x, y, status, iterations for the CPU sample's QPs vs the "
                               "oracle's persistent workspaces after the same setup + update sequence (osqp_update_A, "
-                              "_lin_cost, _bounds; parity unpinned against the real libosqp, DESIGN.md 3)")
-            parity["chain"] = [{k: v for k, v in parity_vs_oracle(got[t], [r[t] for r in ref]).items()
-                                if k in ("qps", "status_equal", "iter_equal", "max_rel_x")}
-                               for t in range(len(got))]
+                              "_lin_cost, _bounds; parity unpinned against the real libosqp, DESIGN.md 3); chain: "
+                              "every step with the oracle re-synchronised to the device's state")
+            parity["chain"] = receding_chain_parity(rec, settings, args.cpu_threads, ref)
+            parity["pass"] = bool(parity["pass"] and parity["chain"]["pass"])
         args.cpu_all_cores = 0
     elif rank == 0 and world == 1 and args.cpu_sample > 0:
         cpu, ref = cpu_baseline(bks, settings, args.cpu_sample, args.cpu_threads)
@@ -509,8 +510,12 @@ def main():
             "workload": ("configs[4]: 65536 N=40 QPs = 8192 instances x 8 intent hypotheses, 10(+1) dynamic obstacles, "
                          "split by instance over the ranks, closed receding window on persistent workspaces (per step, "
                          "on the device: x0 = getPos/getVel(dt) of each QP's last solution, reference and predicted "
-                         "obstacles one step on, q / l / u built, update q + update l, u + solve from the kept "
-                         "scaling / rho / iterates), per-step RCCL all-gather of the cost records (N>1)"),
+                         "obstacles one step on, obstacle rows re-linearised at the last plan, A / q / l / u built, "
+                         "osqp_update_A + update q + update l, u + solve from the kept rho / iterates with the data "
+                         "scaled afresh), per-step RCCL all-gather of the cost records (N>1)")
+            if args.receding else
+            ("configs[4] QPs (65536 N=40, 10(+1) dynamic obstacles), kernel study: full setup + warm start + solve "
+             "of the same QPs every step (--receding 0, not the configs[4] line)"),
             "global_batch": global_batch, "batch_per_gpu": total_qps, "shard_qps": counts,
             "buckets": {str(bk["K"]): int(b.B) for bk, b in batches},
         }
@@ -696,15 +701,21 @@ class RecedingLoop:
             e["b"].update_lin_cost_device(e["q"].ptr)
             e["b"].update_bounds_device(e["l"].ptr, e["u"].ptr)
 
-    def replay(self, k_sample):
+    def replay(self, k_sample, persist=False):
         """The same loop again from the setup, untimed: per step the iterations / statuses of every
         QP and the first k_sample QPs' q, l, u (bucket-proportional) for the oracle; the last step's
-        results per bucket."""
+        results per bucket.  persist: also the sample's persistent workspaces (rho and the scaled
+        iterates, impc_batch_get_persistent) after the first solve and after every step's solve --
+        the state the oracle is re-synchronised to before the next step."""
         total = sum(e["nb"] for e in self.buckets)
         for e in self.buckets:
             e["k"] = min(e["nb"], max(1, int(round(k_sample * e["nb"] / total)))) if k_sample else 0
-            e["ups"], e["got"] = [], []
+            e["ups"], e["got"], e["pst"] = [], [], []
         self.start()
+        if persist:
+            for e in self.buckets:
+                if e["k"]:
+                    e["pst"].append(tuple(a[: e["k"]] for a in e["b"].get_persistent()))
         per_step = []
         for _ in range(self.steps):
             self.advance()
@@ -719,6 +730,8 @@ class RecedingLoop:
                 sts.append(info["status_val"])
                 if e["k"]:  # the sample's results of this step (the oracle's per-step comparison)
                     e["got"].append((x[: e["k"]], y[: e["k"]], info[: e["k"]]))
+                    if persist:
+                        e["pst"].append(tuple(a[: e["k"]] for a in e["b"].get_persistent()))
             it, st = np.concatenate(its), np.concatenate(sts)
             per_step.append({"step": self.t, "mean_iter": float(it.mean()), "p50_iter": float(np.median(it)),
                              "max_iter": int(it.max()),
@@ -742,21 +755,30 @@ def rows_to_host(impc, ctx, darr, k):
     return out
 
 
-def cpu_baseline_receding(bks, settings, rec, threads):
-    """Config 5's CPU path: the oracle's persistent workspaces (osqp_setup, warm start, solve once,
-    then per closed-loop step osqp_update_A + osqp_update_lin_cost + osqp_update_bounds + osqp_solve
-    with the step's A, q, l, u) over a bounded sample, the first QPs of each
-    bucket, on `threads` host threads (one QP's chain per task; the oracle's C calls release the
-    GIL); the timed part is the update + solve steps.  Returns (line object, [(k, x, y, info) per
-    bucket] of the last step, for the parity check)."""
+def oracle_chains(rec, settings, threads, resync=False, q1_perturb=0.0, seed=0):
+    """Config 5's closed loop on the oracle's persistent workspaces (osqp_setup, warm start, solve
+    once, then per closed-loop step osqp_update_A + osqp_update_lin_cost + osqp_update_bounds +
+    osqp_solve with that step's device-built A, q, l, u) for the sample of every bucket, on `threads`
+    host threads (one QP's chain per task; the oracle's C calls release the GIL).
+    resync: before each step the workspace takes the device's persisted rho and scaled iterates
+    after the previous solve (impc_batch_get_persistent -> ora_set_state), so each step starts
+    where the device's did; the oracle's own state at that point is kept for the drift report.
+    q1_perturb: the first closed-loop step's q times (1 + q1_perturb * U(-1, 1)) (seeded) -- the
+    oracle against itself under a perturbation of the size the two implementations differ by.
+    Returns (seconds of the update + solve steps, per bucket [(k, x, y, info) per step],
+    per bucket [per step: (oracle rho, x, z, y) before the resync] or None)."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import osqp_oracle as ora
     s = ora.settings_from(settings)
-    ref, t_all, n_all = [], 0.0, 0
+    out, states, t_all = [], [], 0.0
     for e in rec["buckets"]:
-        bk, k, ups = e["bk"], e["k"], e["ups"]
+        bk, k, ups, pst = e["bk"], e["k"], e["ups"], e.get("pst")
         v = bk["values"]
+        if resync and (not pst or len(pst) < len(ups)):
+            raise ValueError("resync needs the device's persistent states (replay(..., persist=True))")
+        rng = np.random.default_rng(seed)
+        dq = 1.0 + q1_perturb * rng.uniform(-1.0, 1.0, size=ups[0][1].shape) if q1_perturb else None
 
         def setup(i):
             w = ora.Workspace(bk["pattern"], v["Px"][i], v["q"][i], v["Ax"][i], v["l"][i], v["u"][i], s)
@@ -768,31 +790,85 @@ def cpu_baseline_receding(bks, settings, rec, threads):
             ws = list(ex.map(setup, range(k)))
 
         def chain(i):
-            out = []
-            for Ax, q, l, u in ups:
+            res, own = [], []
+            for t, (Ax, q, l, u) in enumerate(ups):
+                if resync:
+                    own.append(ws[i].get_state())
+                    rho, x, z, y = (a[i] for a in pst[t])
+                    ws[i].set_state(rho, x, z, y)
                 ws[i].update_matrices(None, Ax[i])
-                ws[i].update_lin_cost(q[i])
+                ws[i].update_lin_cost(q[i] * dq[i] if (dq is not None and t == 0) else q[i])
                 ws[i].update_bounds(l[i], u[i])
-                out.append(ws[i].solve())
-            return out
+                res.append(ws[i].solve())
+            return res, own
 
         t = time.perf_counter()
         with ThreadPoolExecutor(max_workers=threads) as ex:
             res = list(ex.map(chain, range(k)))
         t_all += time.perf_counter() - t
-        n_all += k * len(ups)
         for w in ws:
             w.close()
-        # per step t: (k, x, y, info) of the sample
-        ref.append([(k, np.array([r[t][0] for r in res]), np.array([r[t][1] for r in res]),
-                     np.array([r[t][2] for r in res], dtype=res[0][t][2].dtype)) for t in range(len(ups))])
+        out.append([(k, np.array([r[0][t][0] for r in res]), np.array([r[0][t][1] for r in res]),
+                     np.array([r[0][t][2] for r in res], dtype=res[0][0][t][2].dtype)) for t in range(len(ups))])
+        states.append([[r[1][t] for r in res] for t in range(len(ups))] if resync else None)
+    return t_all, out, states
+
+
+def cpu_baseline_receding(bks, settings, rec, threads):
+    """Config 5's CPU path: the oracle's persistent workspaces over a bounded sample, the first QPs
+    of each bucket (oracle_chains without resync); the timed part is the update + solve steps.
+    Returns (line object, [(k, x, y, info) per step] per bucket, for the parity check)."""
+    t_all, ref, _ = oracle_chains(rec, settings, threads)
     steps = len(rec["buckets"][0]["ups"])
     n_sample = sum(e["k"] for e in rec["buckets"])
-    return {"value": n_all / t_all, "unit": "QP-solves/s", "cores": threads, "kind": "port",
+    return {"value": n_sample * steps / t_all, "unit": "QP-solves/s", "cores": threads, "kind": "port",
             "host_cpus": os.cpu_count(), "cpu_model": cpu_info(),
             "sample": f"{n_sample} QPs of the workload (first of each bucket) x {steps} closed-loop "
                       f"steps, oracle persistent workspaces (update A, q, l/u, solve) with the device-built values "
                       f"of each step, {threads} threads ({t_all:.1f} s)"}, ref
+
+
+def state_diff(dev, own):
+    """Worst relative differences over a sample between the device's persisted state and the
+    oracle's own at the same point: (scaled iterates x, z, y; rho)."""
+    rho, x, z, y = dev
+    worst = worst_rho = 0.0
+    for i, (orho, ox, oz, oy) in enumerate(own):
+        worst_rho = max(worst_rho, abs(rho[i] - orho) / orho)
+        for a, b in ((x[i], ox), (z[i], oz), (y[i], oy)):
+            if b.size:
+                worst = max(worst, float(np.abs(a - b).max()) / max(float(np.abs(b).max()), 1e-12))
+    return worst, worst_rho
+
+
+def receding_chain_parity(rec, settings, threads, ref_free):
+    """Config 5's chain pinned step by step: (1) the oracle re-synchronised to the
+    device's persisted state before every step -- each step's status, iterations and x compared from
+    the same starting point; (2) the free-running chains' drift, device vs oracle (ref_free) next to
+    the oracle against itself with a 1e-13 relative perturbation of the first step's q."""
+    steps = len(rec["buckets"][0]["ups"])
+    got = [[e["got"][t] for e in rec["buckets"]] for t in range(steps)]
+    _, ref_sync, own = oracle_chains(rec, settings, threads, resync=True)
+    _, ref_pert, _ = oracle_chains(rec, settings, threads, q1_perturb=1e-13, seed=13)
+    table = []
+    for t in range(steps):
+        ps = parity_vs_oracle(got[t], [r[t] for r in ref_sync])
+        fr = parity_vs_oracle(got[t], [r[t] for r in ref_free])
+        # oracle vs oracle: the perturbed chain's results in the "device" slot
+        oo = parity_vs_oracle([(x, y, i) for (_, x, y, i) in (r[t] for r in ref_pert)], [r[t] for r in ref_free])
+        sd = [state_diff(e["pst"][t], own[bi][t]) for bi, e in enumerate(rec["buckets"])]
+        table.append({"step": t + 1, "resync": {k: ps[k] for k in ("qps", "status_equal", "iter_equal", "max_rel_x",
+                                                                      "max_rel_y", "pass")},
+                      "state_before_step": {"max_rel_xzy": max(a for a, _ in sd), "max_rel_rho": max(b for _, b in sd)},
+                      "free": {k: fr[k] for k in ("status_equal", "iter_equal", "max_rel_x")},
+                      "oracle_vs_oracle_1e-13": {k: oo[k] for k in ("status_equal", "iter_equal", "max_rel_x")}})
+    return {"steps": table, "pass": bool(all(r["resync"]["pass"] for r in table)),
+            "what": "resync: the oracle loads the device's persisted rho + scaled iterates before each closed-loop "
+                    "step (ora_set_state), then the same osqp_update_A / _lin_cost / _bounds + solve -- identical "
+                    "status and iterations, x and y within 1e-5 at every step; state_before_step: device vs the "
+                    "oracle's own free-running state at that point; free: the two free-running chains; "
+                    "oracle_vs_oracle_1e-13: the oracle chain against itself with the first step's q perturbed by "
+                    "1e-13 relative (same per-step values)"}
 
 
 def measured_traffic(build_id, qps, kernel, values_mode, workload):

@@ -296,6 +296,13 @@ int impc_batch_get_timings(impc_batch b, double *setup_ms, double *solve_ms, dou
  * Costs 8 (24 + 3 n + 2 m_general) bytes per QP of device memory and that much HBM traffic per
  * solve.  Off by default. */
 int impc_batch_set_persistent(impc_batch b, int on);
+/* Debug read-back of the persistent workspaces after a solve (no reference counterpart: OSQP's
+ * OSQPWorkspace fields work->x, work->z, work->y and settings->rho, types.h:182-289): per QP the
+ * rho and the SCALED iterates in OSQP's variable / row order, host arrays rho [B], x [B][n],
+ * z [B][m], y [B][m] (any may be NULL).  After a solve that ended without a solution the iterates
+ * are zero (store_solution's cold_start).  Synchronises the context.  The parity tests load them
+ * into the oracle's workspace before each step of a chained loop. */
+int impc_batch_get_persistent(impc_batch b, double *rho, double *x, double *z, double *y);
 
 /* Per-QP solve latency (ms) of the last profiled structured-kernel solve: from the moment a
  * workgroup takes the QP off the work queue (the tick its time limit counts from) to its results

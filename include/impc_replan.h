@@ -26,8 +26,10 @@ extern "C" {
  *                   addresses of the candidates' QP solutions, impc_fanout_candidates_device; a
  *                   negative best_cand = no valid candidate, impc_select_best_device), or
  *   single solve    (x_rows != NULL): row r of the QP-major solutions x_rows [count][n], valid
- *                   when solveTraj succeeded, i.e. info_rows[r].status_val != OSQP_NON_CVX
- *                   (:513-518).
+ *                   when solveTraj succeeded: initSolver did (setup_exitflag 0) and solveProblem
+ *                   returned NoError -- osqp_solve's exitflag, 0 for every final status including
+ *                   infeasible and NON_CVX (x = OSQP_NAN), 1 only after a failed adaptive-rho
+ *                   refactorisation (status UNSOLVED) (:475-478, :513-518).
  * State (DEVICE, indexed by instance): plan_x [*][n] (the warm start), plan_states [*][horizon][8]
  * (the linearisation point, = plan_x's first 8 * horizon values), prev_count [*] (horizon once a
  * plan exists), first_time [*] (cleared), valid [*] (1 / 0 for the listed instances).  n must be
@@ -39,30 +41,43 @@ int impc_replan_commit_device(impc_ctx ctx, int32_t horizon, int64_t n, int64_t 
 
 /* ======================================================================================
  * The whole batched makePlanWithPred behind one call (mpcPlanner.cpp:571-661; its C++ caller is
- * mpcNavigation.cpp:316-322).  A replan object holds, for I planning instances with K tracked
- * dynamic obstacles each, the planner state (plan_x / plan_states / prev_count / first_time /
- * valid, as above) and every device buffer and solver batch of a replan, allocated once.
+ * mpcNavigation.cpp:316-322).  A replan object holds, for I planning instances with up to K
+ * tracked dynamic obstacles each (K_i = predPos.size() per instance and per replan,
+ * updatePredObstacles :343-373 -- the detector keeps the obstacles within range and field of view,
+ * onboard_detector fakeDetector.cpp:493, so the count varies), the planner state (plan_x /
+ * plan_states / prev_count / first_time / valid, as above) and every device buffer and solver
+ * batch of a replan, allocated once.
  *
  * impc_replan_run, per instance, as the reference decides (:593-606):
- *   FANOUT          not firstTime_ and predictions present: findClosestObstacle + getIntentComb
- *                   (:663-769), the six candidates' castMPCToQP* (K and K + 1 obstacles), their
- *                   solveTraj with timeLimit, candidate validity (solveProblem NoError = every
- *                   status but NON_CVX, :513-518), getTrajectoryScore + evaluateTraj (:771-887);
+ *   FANOUT          not firstTime_ and predictions present (K_i >= 1): findClosestObstacle +
+ *                   getIntentComb (:663-769), the six candidates' castMPCToQP* (four with K_i and
+ *                   two with K_i + 1 obstacles), their solveTraj with timeLimit, candidate validity
+ *                   (solveTraj's success as for the commit above: OSQP_NAN plans of infeasible or
+ *                   diverged QPs included, :475-478, :513-518),
+ *                   getTrajectoryScore + evaluateTraj (:771-887);
  *   SINGLE_FIRST    firstTime_ (static and dynamic obstacles cleared, :593-602), or no predictions
  *                   and no current obstacles: ONE obstacle-free solveTraj, no time limit, no warm
  *                   start on a first plan;
- *   SINGLE_CURRENT  not firstTime_, no predictions, current dynamic obstacles kept: ONE solveTraj
- *                   with each obstacle's current position / size held over the horizon
+ *   SINGLE_CURRENT  not firstTime_, no predictions, c_i >= 1 current dynamic obstacles kept: ONE
+ *                   solveTraj with each obstacle's current position / size held over the horizon
  *                   (updateDynamicObstacles :316-341);
  * all of it in ONE grouped solve, then every plan committed into the state (:636-639 / :653-657).
- * Everything between the inputs and the committed state stays on the device: the host reads
- * back the three branch counts only (the shapes' QP counts; 16 bytes), nothing else.
+ * The QPs are grouped by obstacle count: shape k (0 .. K + 1) is one solver batch holding every
+ * QP of the replan with k obstacle rows per stage -- first plans (k = 0), current-obstacle solves
+ * (k = c_i), single-intent candidates (k = K_i) and two-intent candidates (k = K_i + 1) -- and the
+ * grouped launch spans all of them.  Which rows exist is decided on the device (a scan over the
+ * instances), and the solver reads each shape's QP count from device memory: the call never
+ * synchronises with the device and nothing returns to the host -- it queues the whole replan and
+ * returns.  Device memory: shape k's batch is sized for its worst case (I rows for k = 0, 4 I for
+ * 1 <= k <= K, 2 I for K + 1), about (4 K + 3) I QPs of storage.
  *
  * The budget (:609-628): candidates are issued only while the replan's elapsed time is below
  * issue_cutoff_s (0.15 s); every candidate carries timeLimit = max(limit - t, limit) (= limit for
  * t >= 0).  All six candidates of every instance are issued at one instant -- the end of the
- * device-side assembly -- so the cut-off is one check: past it no candidate is issued and every
- * fan-out instance selects nothing (validTraj = false).  The single-solve branch has no cut-off.
+ * device-side assembly -- so the cut-off is one check, made on the device: elapsed = elapsed_s +
+ * the device clock from the call's first kernel to the end of the assembly.  Past it no candidate
+ * is issued and every fan-out instance selects nothing (validTraj = false).  The single-solve
+ * branch has no cut-off.
  * ====================================================================================== */
 typedef struct impc_replan_s *impc_replan;
 
@@ -72,7 +87,8 @@ typedef struct impc_replan_s *impc_replan;
 
 typedef struct {
     int64_t instances;         /* I planning instances */
-    int32_t num_obstacles;     /* K >= 1 dynamic obstacles per instance (predicted / current) */
+    int32_t num_obstacles;     /* K, 1 <= K <= 30: the most dynamic obstacles an instance tracks
+                                  (the obstacle slots of every per-instance input array) */
     int32_t pred_len;          /* L prediction steps per obstacle trajectory */
     impc_mpc_params mpc;       /* initParam values; mpc.horizon = N (the selection's safety
                                   distances are mpc.dynamic_safety_dist / static_safety_dist) */
@@ -83,7 +99,8 @@ typedef struct {
     int32_t reserved;
 } impc_replan_config;
 
-/* Per-replan inputs, all DEVICE pointers (K = num_obstacles, L = pred_len, N = horizon). */
+/* Per-replan inputs, all DEVICE pointers (K = num_obstacles, L = pred_len, N = horizon).  An
+ * instance's obstacles are its first K_i (predictions) / c_i (current) slots. */
 typedef struct {
     const double *pos, *vel;       /* [I][3] updateCurrStates */
     const double *xref;            /* [I][N][8] getXRef (e.g. impc_reference_traj_device) */
@@ -94,22 +111,24 @@ typedef struct {
     const int8_t *has_pred;        /* [I] obPredPos_.size() != 0; NULL = every instance */
     const double *cur_size;        /* [I][K][3] dynamicObstaclesSize_ kept without predictions;
                                       NULL = none (updatePredObstacles clears them, :364-371) */
-    const int32_t *cur_count;      /* [I] 0 or K current obstacles; NULL with cur_size = K */
+    const int32_t *cur_count;      /* [I] c_i current obstacles (0 .. K); NULL with cur_size = K */
     double solver_time_limit;      /* solverTimeLimit_ (0.05 s); <= 0: settings.time_limit */
     double elapsed_s;              /* seconds of the replan already spent before this call
                                       (counted against the issue cut-off) */
+    const int32_t *num_pred;       /* [I] K_i = predPos.size() (0 .. K; 0 = no predictions, as
+                                      has_pred = 0); NULL = K for every instance */
 } impc_replan_inputs;
 
-/* What the last impc_replan_run did (host values). */
+/* What the last impc_replan_run did (host values; reading them synchronises the context). */
 typedef struct {
     int64_t fanout, single_first, single_current; /* instances per branch */
     int32_t issued;                                /* candidates issued (cut-off not reached) */
     int32_t reserved;
     double time_limit;                             /* the candidates' time limit (s, 0 = none) */
-    double stage_s;                                /* branch table + assembly, host wall (s) */
-    double total_s;                                /* host wall of the call (s); the solve, the
-                                                      selection and the commit are queued, not
-                                                      waited for */
+    double stage_s;                                /* branch table + assembly on the device clock
+                                                      (s): the elapsed time the cut-off adds */
+    double total_s;                                /* host wall of the call (s); the whole replan
+                                                      is queued, not waited for */
 } impc_replan_stats;
 
 int impc_replan_create(impc_ctx ctx, const impc_replan_config *cfg, impc_replan *out);
@@ -120,7 +139,7 @@ int impc_replan_destroy(impc_replan rp);
  * reference sets firstTime_ = false only together with a full plan, :636-639 / :653-657). */
 int impc_replan_set_state(impc_replan rp, const double *plan_x, const int8_t *first_time);
 /* One batched makePlanWithPred (see above).  Stream-ordered on the context stream; returns once
- * the solve, selection and commit are queued. */
+ * every stage is queued (no host synchronisation inside the call). */
 int impc_replan_run(impc_replan rp, const impc_replan_inputs *in);
 int impc_replan_get_stats(impc_replan rp, impc_replan_stats *out);
 
@@ -128,25 +147,30 @@ int impc_replan_get_stats(impc_replan rp, impc_replan_stats *out);
  * plan_states [I+1][N][8], prev_count [I], first_time [I], valid [I] (the last replan's validTraj).
  * Per instance of the last run: branch [I] (IMPC_REPLAN_*), best_cand [I] (fan-out instances:
  * the selected candidate or -1; -1 otherwise), ob_idx [I] (closest obstacle; -1 for single-solve
- * instances), cand_type / cand_slot [I][6] (getIntentComb order; -1 for single-solve instances). */
+ * instances), cand_type / cand_slot [I][6] (getIntentComb order; -1 for single-solve instances),
+ * num_obs [I] (fan-out: K_i; single solve: the obstacle count of its QP = its shape), slot_row
+ * [I][6] (fan-out: the row of slot s in shape K_i (s < 4) or K_i + 1 (s >= 4); single solve: its
+ * row in shape num_obs at [0]; -1 elsewhere). */
 typedef struct {
     double *plan_x, *plan_states;
     int32_t *prev_count;
     int8_t *first_time, *valid, *branch;
     int32_t *best_cand, *ob_idx, *cand_type, *cand_slot;
+    int32_t *num_obs, *slot_row;
 } impc_replan_view;
 int impc_replan_view_device(impc_replan rp, impc_replan_view *out);
 
-/* Inspection of the last run (tests, tools): the solver batch of one QP shape, its QP count and
- * its instances (DEVICE int64 [count'] in ascending order; count' = count / 4 or count / 2 for
- * the fan-out shapes), and the assembled values (DEVICE, QP-major, `count` rows).  Shapes:
- *   0  fan-out single-intent candidates (K obstacles), row 4 j + slot of fan-out instance j
- *   1  fan-out two-intent candidates (K + 1 obstacles), row 2 j + slot - 4
- *   2  single solve, first plan / no obstacles, row j of inst
- *   3  single solve, current obstacles, row j of inst
- * A shape not run in the last replan reports count 0 (its batch may still be NULL). */
-int impc_replan_shape(impc_replan rp, int32_t shape, impc_batch *batch, int64_t *count, const int64_t **inst,
-                      const double **Px, const double **q, const double **Ax, const double **l, const double **u);
+/* Inspection of the last run (tests, tools; synchronises the context): shape k = the QPs with k
+ * obstacle rows per stage (0 <= k <= K + 1) -- its solver batch, the number of its rows solved in
+ * the last replan, each row's instance and kind (DEVICE int32 row_inst / int8 row_code [count]:
+ * 0..3 single-intent slot, 4..5 two-intent slot, 6 first plan / no obstacles, 7 current obstacles;
+ * single solves first, then the candidates, each in ascending instance order) and the assembled
+ * values (DEVICE, QP-major, `count` rows). */
+#define IMPC_REPLAN_ROW_FIRST 6
+#define IMPC_REPLAN_ROW_CURRENT 7
+int impc_replan_shape(impc_replan rp, int32_t obstacles, impc_batch *batch, int64_t *count, const int32_t **row_inst,
+                      const int8_t **row_code, const double **Px, const double **q, const double **Ax,
+                      const double **l, const double **u);
 
 /* The vehicle following its plan (mpc_node.cpp:216-224: after a successful makePlan, currPos =
  * getPos(dt), currVel = getVel(dt)): for every instance whose last replan produced a plan

@@ -625,9 +625,19 @@ IMPC_HD void qp_solve(const DevSym &sy, const DevWork &wk, const DevSettings &st
             double rn = rho_estimate(inf, rho);
             rho_est = rn;
             if ((rn > rho * st.adaptive_rho_tolerance) || (rn < rho / st.adaptive_rho_tolerance)) {
-                update_rho(sy, wk, st, rn, lane);
+                const int bad = update_rho(sy, wk, st, rn, lane);
                 rho = IMPC_AT(wk.scal, SC_RHO);
                 rho_updates += 1;
+                if (bad) {  // osqp_solve exits with exitflag 1: status UNSOLVED, no stored solution
+                    out.iter = inf.iter;
+                    out.status_val = IMPC_UNSOLVED;
+                    out.rho_updates = rho_updates;
+                    out.setup_exitflag = 0;
+                    out.pri_res = inf.pri_res;
+                    out.dua_res = inf.dua_res;
+                    out.rho_estimate = rho_est;
+                    return;
+                }
             }
         }
     }

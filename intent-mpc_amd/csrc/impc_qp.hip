@@ -432,6 +432,10 @@ struct GroupEntry {
     impc::WaveIO io;
     impc::DevSettings st;
     int64_t first;
+    // the batch's active QP count in device memory (impc_lib::batch_set_active_device), or null:
+    // io.B QPs.  A launch with device counts dequeues through a permutation that puts every
+    // active QP first, and stops after the sum of the counts.
+    const int64_t *dcount;
 };
 
 // Several structured batches in one persistent launch: one work queue over all their QPs, so
@@ -440,12 +444,20 @@ struct GroupEntry {
 template <int NL, int VS, int GS, int WPS, int WF, bool TIER>
 __global__ __launch_bounds__(NL, WPS) void k_mpc_wave_group(const GroupEntry *__restrict__ g, int count,
                                                             int64_t total, unsigned *counter,
-                                                            const uint32_t *__restrict__ ord) {
+                                                            const uint32_t *__restrict__ ord, int devcnt) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     using LD = impc::WaveLds<NL, VS, GS>;
     GpuTeam<NL> wv{smem + LD::RED_OFF};
     __shared__ unsigned next;
     int cur = -1;
+    if (devcnt) {  // device-side active counts: the queue's length is their sum (ord puts them first)
+        int64_t t = 0;
+        for (int e = 0; e < count; e++) {
+            const int64_t c = g[e].dcount ? *g[e].dcount : g[e].io.B;
+            t += c < g[e].io.B ? (c > 0 ? c : 0) : g[e].io.B;
+        }
+        total = t;
+    }
     for (;;) {
         if (threadIdx.x == 0) next = atomicAdd(counter, 1u);
         __syncthreads();
@@ -571,6 +583,9 @@ struct impc_batch_s {
     std::vector<int64_t> Pp, Pi, Ap, Ai;  // pattern (host copy)
     int64_t B = 0, S = 0;
     int64_t Bact = 0;  // QPs the solves take (impc_batch_set_active): the first Bact of B
+    // or the count in device memory (impc_lib::batch_set_active_device; Bact = B while set): the
+    // batch's producer decides it on the device, no host round trip before the solve
+    const int64_t *d_active = nullptr;
     impc_settings settings{};
     impc::DevSettings dst{};
     int kernel_req = IMPC_KERNEL_AUTO;
@@ -938,9 +953,14 @@ int build_queue_csr(impc_batch b) {
 int queue_order(impc_batch *bs, const int64_t *firsts, int count, int64_t total, hipStream_t st,
                 const uint32_t **ord) {
     *ord = nullptr;
-    bool any = false;
-    for (int k = 0; k < count; k++) any = any || bs[k]->queue_mode == IMPC_QUEUE_LONGEST_FIRST;
-    if (!any || total < 2) return IMPC_OK;
+    bool any = false, devcnt = false;
+    for (int k = 0; k < count; k++) {
+        any = any || bs[k]->queue_mode == IMPC_QUEUE_LONGEST_FIRST;
+        devcnt = devcnt || bs[k]->d_active != nullptr;
+    }
+    // device-side active counts: always a permutation, active QPs first (FIFO order among them
+    // unless a batch asks for the longest-first order), the inactive rows' keys -inf
+    if (!devcnt && (!any || total < 2)) return IMPC_OK;
     // the radix sort takes an int item count
     if (total > (int64_t)INT32_MAX) return fail(IMPC_UNSUPPORTED, "queue order: too many QPs in one launch");
     impc_batch h = bs[0];
@@ -976,6 +996,8 @@ int queue_order(impc_batch *bs, const int64_t *firsts, int count, int64_t total,
         a.nvar = b->nvar, a.vmap = b->d_vmap, a.Ax_var = b->d_Axv;
         a.q = b->in_q, a.l = b->in_l, a.u = b->in_u, a.xws = b->in_xws, a.has_ws = b->has_ws ? 1 : 0;
         a.q_weight = b->queue_qw;
+        a.dcount = b->d_active;
+        a.fifo = any ? 0 : 1;
         const unsigned grid = (unsigned)std::min<int64_t>(b->Bact, 4096);
         hipLaunchKernelGGL(impc::k_queue_key, dim3(grid), dim3(256), 0, st, a, key, idx);
         HIP_OK(hipGetLastError());
@@ -1040,25 +1062,27 @@ int structured_solve(impc_batch b, hipStream_t st) {
 
 template <int VS, int GS, int WF, bool TIER>
 int launch_group_w(impc_ctx ctx, hipStream_t st, const GroupEntry *entries, int count, int64_t total, size_t lds,
-                   unsigned *counter, const uint32_t *ord) {
+                   unsigned *counter, const uint32_t *ord, int devcnt) {
     using S = Shape<VS>;
     if (int rc = ensure_lds_attr(k_mpc_wave_group<S::NL, VS, GS, S::WPS, WF, TIER>, lds)) return rc;
     const int64_t groups = resident_groups<VS>(ctx->num_cu, lds, total);
     hipLaunchKernelGGL((k_mpc_wave_group<S::NL, VS, GS, S::WPS, WF, TIER>), dim3((unsigned)groups), dim3(S::NL), lds,
-                       st, entries, count, total, counter, ord);
+                       st, entries, count, total, counter, ord, devcnt);
     HIP_OK(hipGetLastError());
     return IMPC_OK;
 }
 // spec: the compile-time horizon every batch of the launch shares (spec_w), or 0
 template <int VS, int GS, bool TIER = false>
 int launch_group(impc_ctx ctx, hipStream_t st, const GroupEntry *entries, int count, int64_t total, size_t lds,
-                 unsigned *counter, int spec, const uint32_t *ord) {
+                 unsigned *counter, int spec, const uint32_t *ord, int devcnt) {
     using LD = impc::WaveLds<Shape<VS>::NL, VS, GS>;
     constexpr int WS = LD::WSPEC, WS2 = LD::WSPEC2;
-    if (spec && spec == WS) return launch_group_w<VS, GS, WS, TIER>(ctx, st, entries, count, total, lds, counter, ord);
+    if (spec && spec == WS)
+        return launch_group_w<VS, GS, WS, TIER>(ctx, st, entries, count, total, lds, counter, ord, devcnt);
     if constexpr (WS2 != 0)
-        if (spec == WS2) return launch_group_w<VS, GS, WS2, TIER>(ctx, st, entries, count, total, lds, counter, ord);
-    return launch_group_w<VS, GS, 0, TIER>(ctx, st, entries, count, total, lds, counter, ord);
+        if (spec == WS2)
+            return launch_group_w<VS, GS, WS2, TIER>(ctx, st, entries, count, total, lds, counter, ord, devcnt);
+    return launch_group_w<VS, GS, 0, TIER>(ctx, st, entries, count, total, lds, counter, ord, devcnt);
 }
 
 // dynamic LDS bytes of the structured kernel for a shape (team VS, GS) and pattern (CG, n); 0 if
@@ -1738,6 +1762,7 @@ int impc_batch_warm_start_device(impc_batch b, const double *x, const double *y)
 int impc_batch_set_active(impc_batch b, int64_t count) {
     if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
     if (count < 1 || count > b->B) return fail(IMPC_INVALID_ARGUMENT, "active count must be in [1, B]");
+    b->d_active = nullptr;
     if (count != b->Bact) {
         b->Bact = count;
         b->persist_valid = b->q_by_update = b->rescale = b->q_after = false;  // the stored workspaces cover other QPs
@@ -1799,6 +1824,7 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
         size_t lds;
         int spec;  // the launch's compile-time horizon (-1: no batch yet; 0: runtime W)
         unsigned *counter;
+        bool devcnt;  // some batch's active count is in device memory
     };
     std::vector<Launch> launches;
     HIP_OK(hipSetDevice(ctx->device));
@@ -1809,7 +1835,7 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
         impc_batch b = bs[order[(size_t)p]];
         if (launches.empty() || launches.back().vs != b->vs || launches.back().gs != b->gs ||
             launches.back().tier != b->tier)
-            launches.push_back(Launch{b->vs, b->gs, b->tier, p, 0, 0, 0, -1, b->d_counter});
+            launches.push_back(Launch{b->vs, b->gs, b->tier, p, 0, 0, 0, -1, b->d_counter, false});
         Launch &L = launches.back();
         L.count++;
         L.lds = std::max(L.lds, wave_lds_bytes(b->vs, b->gs, b->wt));
@@ -1819,6 +1845,8 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
         e.io = wave_io(b);
         e.st = b->dst;
         e.first = L.total;
+        e.dcount = b->d_active;
+        L.devcnt = L.devcnt || b->d_active != nullptr;
         L.total += b->Bact;
         b->ev_solve = false;
         b->ev_setup = false;
@@ -1871,7 +1899,7 @@ int impc_batch_solve_group(impc_batch *bs, int count, void *stream) {
         IMPC_TRY(queue_order(lb.data(), lf.data(), L.count, L.total, st, &ord));
         const int rc = with_shape(L.vs, L.gs, L.tier, [&](auto vs, auto gs, auto tr) {
             return launch_group<decltype(vs)::value, decltype(gs)::value, decltype(tr)::value>(
-                ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord);
+                ctx, st, E, L.count, L.total, L.lds, L.counter, L.spec, ord, L.devcnt ? 1 : 0);
         });
         if (rc) return rc;
     }
@@ -2171,9 +2199,40 @@ int impc_batch_set_persistent(impc_batch b, int on) {
             return fail(IMPC_MEM_ALLOC_ERROR, "hipMalloc(persistent workspace) failed");
         }
         b->device_bytes += (int64_t)bytes;
+        // defined contents before any solve writes them (rho and iterates of a fresh workspace are
+        // written by the first solve, including one whose factorisation fails)
+        HIP_OK(hipMemsetAsync(b->d_persist, 0, bytes, b->ctx->stream));
     }
     b->persist_on = on != 0;
     b->persist_valid = b->q_by_update = b->rescale = b->q_after = false;  // the next solve sets up from scratch
+    return IMPC_OK;
+}
+
+int impc_batch_get_persistent(impc_batch b, double *rho, double *x, double *z, double *y) {
+    if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
+    if (!b->persist_on || !b->persist_valid || !b->d_persist)
+        return fail(IMPC_WORKSPACE_NOT_INIT_ERROR, "no persistent workspace solved yet (impc_batch_set_persistent + solve)");
+    HIP_OK(hipSetDevice(b->ctx->device));
+    IMPC_TRY(ctx_quiesce(b->ctx));
+    const impc::MpcStructure &ms = *b->ms;
+    const int64_t n = b->n, m = b->m, mg = ms.mg, stride = impc::persist_stride((int)n, (int)mg);
+    std::vector<double> h((size_t)(b->B * stride));
+    HIP_OK(hipMemcpy(h.data(), b->d_persist, sizeof(double) * h.size(), hipMemcpyDeviceToHost));
+    // the kernel's layout (mpc_wave.hpp WaveIO::persist): [hdr | x, z_box, y_box (stage order) |
+    // z_gen, y_gen (general-row order)] -> OSQP's variable and row order
+    for (int64_t k = 0; k < b->B; k++) {
+        const double *p = h.data() + k * stride, *it = p + impc::kPersistHdr;
+        if (rho) rho[k] = p[impc::kPersistHdr - 1];
+        for (int64_t v = 0; v < n; v++) {
+            if (x) x[k * n + ms.var_orig[v]] = it[v];
+            if (z) z[k * m + ms.var_boxrow[v]] = it[n + v];
+            if (y) y[k * m + ms.var_boxrow[v]] = it[2 * n + v];
+        }
+        for (int64_t g = 0; g < mg; g++) {
+            if (z) z[k * m + ms.gen_row[g]] = it[3 * n + g];
+            if (y) y[k * m + ms.gen_row[g]] = it[3 * n + mg + g];
+        }
+    }
     return IMPC_OK;
 }
 
@@ -2430,6 +2489,44 @@ int batch_inputs_view(impc_batch b, BatchInputs *out) {
     out->Px = b->in_Px, out->q = b->in_q, out->Ax = b->in_Ax, out->l = b->in_l, out->u = b->in_u;
     out->xws = b->in_xws;
     out->n = b->n, out->m = b->m, out->nnzP = b->nnzP, out->nnzA = b->nnzA, out->B = b->B;
+    return IMPC_OK;
+}
+int batch_set_active_device(impc_batch b, const int64_t *d_count) {
+    if (!b) return fail(IMPC_INVALID_ARGUMENT, "null batch");
+    if (d_count && !use_structured(b))
+        return fail(IMPC_UNSUPPORTED, "device-side active counts need the structured kernel");
+    b->d_active = d_count;
+    b->Bact = b->B;
+    b->persist_valid = b->q_by_update = b->rescale = b->q_after = false;
+    b->generic_dirty = true;
+    return IMPC_OK;
+}
+int batch_tlim_device(impc_batch b, double **out) {
+    if (!b || !out) return fail(IMPC_INVALID_ARGUMENT, "null batch");
+    HIP_OK(hipSetDevice(b->ctx->device));
+    if (!b->d_tlim) {
+        HIP_OK(hipMalloc((void **)&b->d_tlim, sizeof(double) * (size_t)b->B));
+        b->device_bytes += (int64_t)sizeof(double) * b->B;
+        IMPC_TRY(fill0_sync(b->ctx->stream, b->d_tlim, sizeof(double) * (size_t)b->B));
+    }
+    b->tlim_on = true;
+    *out = b->d_tlim;
+    return IMPC_OK;
+}
+double tick_s(impc_ctx ctx) { return ctx->tick_s; }
+int build_rows(impc_mpc_builder bd, int64_t cap, const int64_t *dcount, const int32_t *row_inst, const int64_t *osrc,
+               const double *pos, const double *vel, const double *xref, const double *lin, const double *pred_pos,
+               const double *pred_size, const double *held_pos, const double *held_size, const BatchInputs &out,
+               hipStream_t st) {
+    if (!bd || cap < 1) return fail(IMPC_INVALID_ARGUMENT, "build_rows: null builder or empty capacity");
+    impc_build::Args a{cap, bd->n, bd->m, bd->nnzP, bd->nnzA, bd->obs_off, bd->N, bd->W, bd->S, bd->Kd, bd->K, bd->L,
+                       bd->p.dynamic_safety_dist, bd->p.static_safety_dist, bd->p.position_weight,
+                       bd->p.velocity_weight, bd->d_tPx, bd->d_tAx, bd->d_tl, bd->d_tu, bd->d_slot, pos, vel, xref,
+                       lin, nullptr, nullptr, nullptr, pred_pos, pred_size, out.Px, out.q, out.Ax, out.l, out.u};
+    a.dcount = dcount, a.row_inst = row_inst, a.osrc = osrc, a.hp = held_pos, a.hs = held_size;
+    const int64_t groups = std::min<int64_t>(cap, (int64_t)bd->ctx->num_cu * 8);
+    hipLaunchKernelGGL(impc_build::k_build, dim3((unsigned)groups), dim3(256), 0, st, a);
+    HIP_OK(hipGetLastError());
     return IMPC_OK;
 }
 int batch_inputs_end(impc_batch b, bool warm_x) {

@@ -5,9 +5,18 @@
 
 #include <string>
 
+#include "../../include/impc_mpc.h"
 #include "../../include/impc_qp.h"
 
 namespace impc_lib {
+// solveTraj's success for one solved QP (mpcPlanner.cpp:475-478, :513-518): initSolver (osqp_setup)
+// succeeded and solveProblem returned NoError.  osqp_solve's exitflag -- what solveProblem returns
+// -- is 0 for every final status, infeasible, max-iter, time limit and a NON_CVX from the residual
+// test included (x = OSQP_NAN then), and 1 only when an adaptive-rho refactorisation fails, which
+// leaves the status UNSOLVED; a failed setup is reported as NON_CVX with setup_exitflag set.
+__host__ __device__ inline bool solve_traj_ok(const impc_info &inf) {
+    return inf.setup_exitflag == 0 && inf.status_val != IMPC_UNSOLVED;
+}
 // record the message of the last error (impc_last_error) and return `code`
 int set_error(int code, const std::string &msg);
 int num_cu(impc_ctx ctx);
@@ -28,4 +37,19 @@ int batch_inputs_begin(impc_batch b, BatchInputs *out);
 int batch_inputs_end(impc_batch b, bool warm_x);
 // the same arrays without ordering (read-only inspection after the caller synchronised)
 int batch_inputs_view(impc_batch b, BatchInputs *out);
+// The batch's active QP count from device memory (structured kernel): every later solve takes the
+// first *d_count of its B QPs, the count read by the kernels themselves -- no host round trip
+// between the producer that decides it and the solve.  NULL returns to B (impc_batch_set_active).
+int batch_set_active_device(impc_batch b, const int64_t *d_count);
+// The batch's per-QP time-limit array [B] on the device (allocated zero = no limit on first use),
+// switched on for the following solves; producers write it in place.
+int batch_tlim_device(impc_batch b, double **out);
+// seconds per tick of the device clock the time limits run on (hipDeviceAttributeWallClockRate)
+double tick_s(impc_ctx ctx);
+// The device builder over replan rows (mpc_build.hpp Args: dcount / row_inst / osrc / held arrays),
+// writing the QP values into a batch's input arrays; asynchronous on `st`.
+int build_rows(impc_mpc_builder bd, int64_t cap, const int64_t *dcount, const int32_t *row_inst, const int64_t *osrc,
+               const double *pos, const double *vel, const double *xref, const double *lin, const double *pred_pos,
+               const double *pred_size, const double *held_pos, const double *held_size, const BatchInputs &out,
+               hipStream_t st);
 }  // namespace impc_lib

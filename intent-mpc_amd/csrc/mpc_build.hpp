@@ -24,6 +24,16 @@ struct Args {
     const int32_t *slot;
     const double *cp, *cv, *xref, *ls, *stc, *sts, *sty, *dp, *ds;
     double *Px, *q, *Ax, *l, *u;
+    // replan rows (impc_lib::build_rows, replan_run.hip): the row count in device memory (rows >=
+    // *dcount are not built), each row's planning instance (x0, reference and linearisation
+    // point are per-instance arrays, indexed by row_inst[b]) and each dynamic obstacle's source:
+    // osrc[b][j] = (offset << 1) | held -- held = 0: the trajectory at dp / ds + offset, step
+    // stride 3 (a prediction); held = 1: the position at hp / hs + offset for every stage (a
+    // current obstacle, updateDynamicObstacles :316-341).  All null: the plain layouts above.
+    const int64_t *dcount = nullptr;
+    const int32_t *row_inst = nullptr;
+    const int64_t *osrc = nullptr;
+    const double *hp = nullptr, *hs = nullptr;
 };
 
 // ((std::pow(v, 2)) with glibc's correctly rounded pow is exactly the rounded product v * v)
@@ -31,8 +41,10 @@ __device__ inline double sq(double v) { return v * v; }
 
 __global__ __launch_bounds__(256) void k_build(Args a) {
 #pragma clang fp contract(off)
-    for (int64_t b = blockIdx.x; b < a.nb; b += gridDim.x) {
+    const int64_t nb = a.dcount ? (*a.dcount < a.nb ? *a.dcount : a.nb) : a.nb;
+    for (int64_t b = blockIdx.x; b < nb; b += gridDim.x) {
         const int t0 = (int)threadIdx.x;
+        const int64_t ib = a.row_inst ? (int64_t)a.row_inst[b] : b;  // per-instance inputs
         double *Px = a.Px + b * a.nnzP, *Ax = a.Ax + b * a.nnzA, *q = a.q + b * a.n, *l = a.l + b * a.m,
                *u = a.u + b * a.m;
         for (int64_t e = t0; e < a.nnzP; e += blockDim.x) Px[e] = a.tPx[e];
@@ -42,7 +54,7 @@ __global__ __launch_bounds__(256) void k_build(Args a) {
             u[r] = a.tu[r];
         }
         // castMPCToQPGradient: q_state = Q * (-xRef), controls 0
-        const double *xr = a.xref + b * (int64_t)a.N * 8;
+        const double *xr = a.xref + ib * (int64_t)a.N * 8;
         for (int64_t k = t0; k < a.n; k += blockDim.x) {
             double v = 0.0;
             if (k < (int64_t)8 * a.N) {
@@ -55,7 +67,7 @@ __global__ __launch_bounds__(256) void k_build(Args a) {
         __syncthreads();
         // x0 rows (:1082-1086): l = u = -x0 on the first 8 rows
         if (t0 < 8) {
-            const double x0 = t0 < 3 ? a.cp[3 * b + t0] : t0 < 6 ? a.cv[3 * b + t0 - 3] : 0.0;
+            const double x0 = t0 < 3 ? a.cp[3 * ib + t0] : t0 < 6 ? a.cv[3 * ib + t0 - 3] : 0.0;
             l[t0] = -x0;
             u[t0] = -x0;
         }
@@ -65,8 +77,15 @@ __global__ __launch_bounds__(256) void k_build(Args a) {
             double ox, oy, oz, sx, sy, sz, yaw;
             if (j < a.Kd) {  // dynamic first (:1153), prediction clamped to .back()
                 const int jj = i < a.L ? i : a.L - 1;
-                const double *pp = a.dp + (((int64_t)b * a.Kd + j) * a.L + jj) * 3;
-                const double *ps = a.ds + (((int64_t)b * a.Kd + j) * a.L + jj) * 3;
+                const double *pp, *ps;
+                if (a.osrc) {
+                    const int64_t o = a.osrc[b * a.Kd + j], off = o >> 1;
+                    pp = (o & 1) ? a.hp + off : a.dp + off + (int64_t)jj * 3;
+                    ps = (o & 1) ? a.hs + off : a.ds + off + (int64_t)jj * 3;
+                } else {
+                    pp = a.dp + (((int64_t)b * a.Kd + j) * a.L + jj) * 3;
+                    ps = a.ds + (((int64_t)b * a.Kd + j) * a.L + jj) * 3;
+                }
                 ox = pp[0], oy = pp[1], oz = pp[2];
                 sx = ps[0] / 2 + a.dsafe, sy = ps[1] / 2 + a.dsafe, sz = ps[2] / 2 + a.dsafe;
                 yaw = 0.0;
@@ -79,10 +98,10 @@ __global__ __launch_bounds__(256) void k_build(Args a) {
             }
             double cx, cy, cz;  // linearisation point (:1042-1051)
             if (a.ls) {
-                const double *ls = a.ls + (b * (int64_t)a.N + i) * 8;
+                const double *ls = a.ls + (ib * (int64_t)a.N + i) * 8;
                 cx = ls[0], cy = ls[1], cz = ls[2];
             } else {
-                cx = a.cp[3 * b], cy = a.cp[3 * b + 1], cz = a.cp[3 * b + 2];
+                cx = a.cp[3 * ib], cy = a.cp[3 * ib + 1], cz = a.cp[3 * ib + 2];
             }
             const double cyw = cos(yaw), syw = sin(yaw);
             const double fxx = 2 * ((cx - ox) * cyw + (cy - oy) * syw) / sq(sx) * cyw +

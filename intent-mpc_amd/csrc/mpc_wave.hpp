@@ -1891,6 +1891,18 @@ struct WaveQP {
                 out->pri_res = out->dua_res = 0.0;
                 out->rho_estimate = R.rho;
             }
+            // a first setup that fails its factorisation leaves a defined workspace: the settings'
+            // rho and zero iterates (osqp_setup's cold_start), so a resume after a matrix update
+            // (impc_batch_update_matrices) starts as a fresh setup would; a failed resume keeps the
+            // workspace it had (OSQP keeps work->x, z, y when osqp_update_P / _A fails to refactor)
+            if (ps && io.resume == 0) {
+                double *it = ps + kPersistHdr;
+                if (L == 0) ps[kPersistHdr - 1] = R.rho;
+                _Pragma("unroll") for (int s = 0; s < VS; s++)
+                    if (vok[s]) it[NL * s + L] = it[n + NL * s + L] = it[2 * n + NL * s + L] = 0.0;
+                _Pragma("unroll") for (int s = 0; s < GS; s++)
+                    if (gok[s]) it[3 * n + NL * s + L] = it[3 * n + T.mg + NL * s + L] = 0.0;
+            }
             wv.sync();
             return;
         }
@@ -1966,12 +1978,15 @@ struct WaveQP {
         // The refactorisation after an adaptive-rho update runs between two passes of the inner
         // iteration loop rather than inside it: the register allocator then places the spills the
         // factorisation's temporaries force around that (rare) call, outside the hot loop.
-        bool refac = false;
+        bool refac = false, refail = false;
         iter = 1;
         for (;;) {
             if (refac) {
                 refac = false;
-                factorize();
+                if (factorize()) {  // osqp_solve: a failed rho update ends the solve with exitflag 1
+                    refail = true;
+                    break;
+                }
                 write_v_products();
                 IMPC_SEC(kSecFactor);
             }
@@ -2047,6 +2062,37 @@ struct WaveQP {
             }
             iter++;  // this iteration is complete; the next pass starts at the next one
         }
+        if (refail) {
+            // OSQP 0.6.2 jumps to exit: no termination check, no stored solution (the outputs keep
+            // the previous solve's), status stays UNSOLVED, info.iter is the last update_info's;
+            // the workspace keeps the new rho and its iterates as they are
+            if (ps) {
+                double *it = ps + kPersistHdr;
+                if (L == 0) ps[kPersistHdr - 1] = R.rho;
+                _Pragma("unroll") for (int s = 0; s < VS; s++)
+                    if (vok[s]) {
+                        it[NL * s + L] = x[s];
+                        it[n + NL * s + L] = zb[s];
+                        it[2 * n + NL * s + L] = yb[s];
+                    }
+                _Pragma("unroll") for (int s = 0; s < GS; s++)
+                    if (gok[s]) {
+                        it[3 * n + NL * s + L] = z[s];
+                        it[3 * n + T.mg + NL * s + L] = y[s];
+                    }
+            }
+            if (L == 0) {
+                out->iter = info_iter;
+                out->status_val = IMPC_UNSOLVED;
+                out->rho_updates = rho_updates;
+                out->setup_exitflag = 0;
+                out->pri_res = inf.pri_res;
+                out->dua_res = inf.dua_res;
+                out->rho_estimate = rho_est;
+            }
+            wv.sync();
+            return;
+        }
         IMPC_SEC_START();
         double D[VS], Eb[VS], Eg[GS];
         load_scal(b, D, Eb, Eg);
@@ -2072,21 +2118,22 @@ struct WaveQP {
         const bool has_sol2 = status != IMPC_PRIMAL_INFEASIBLE && status != IMPC_PRIMAL_INFEASIBLE_INACCURATE &&
                               status != IMPC_DUAL_INFEASIBLE && status != IMPC_DUAL_INFEASIBLE_INACCURATE &&
                               status != IMPC_NON_CVX;
-        if (ps) {  // the workspace after osqp_solve: rho and the scaled iterates
+        if (ps) {  // the workspace after osqp_solve: rho and the scaled iterates -- zero when the
+                   // solve ended without a solution (store_solution's cold_start, auxil.c)
             double *it = ps + kPersistHdr;
             if (L == 0) ps[kPersistHdr - 1] = R.rho;
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
                 if (!vok[s]) continue;
                 const int v = NL * s + L;
-                it[v] = x[s];
-                it[n + v] = zb[s];
-                it[2 * n + v] = yb[s];
+                it[v] = has_sol2 ? x[s] : 0.0;
+                it[n + v] = has_sol2 ? zb[s] : 0.0;
+                it[2 * n + v] = has_sol2 ? yb[s] : 0.0;
             }
             _Pragma("unroll") for (int s = 0; s < GS; s++) {
                 if (!gok[s]) continue;
                 const int g = NL * s + L;
-                it[3 * n + g] = z[s];
-                it[3 * n + T.mg + g] = y[s];
+                it[3 * n + g] = has_sol2 ? z[s] : 0.0;
+                it[3 * n + T.mg + g] = has_sol2 ? y[s] : 0.0;
             }
         }
         const bool scaled = st.scaling > 0;

@@ -38,13 +38,23 @@ struct QueueKeyArgs {
     const double *q, *l, *u, *xws;  // QP-major
     int32_t has_ws;
     double q_weight;
+    const int64_t *dcount;  // active rows in device memory (rows >= *dcount: key -inf, last), or null
+    int32_t fifo;           // key = -(queue index): the FIFO order as a permutation (device counts)
 };
 
 // One 256-thread workgroup per QP (grid-stride): rows of A x_ws against [l, u], |q|, a block max.
 // Writes key[first + b] and the QP's launch-wide queue index first + b.
 __global__ __launch_bounds__(256) void k_queue_key(QueueKeyArgs a, double *key, uint32_t *idx) {
     __shared__ double red[8];
+    const int64_t nact = a.dcount ? *a.dcount : a.B;
     for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+        if (b >= nact || a.fifo) {  // (uniform per workgroup)
+            if (threadIdx.x == 0) {
+                key[a.first + b] = b >= nact ? -INFINITY : -(double)(a.first + b);
+                idx[a.first + b] = (uint32_t)(a.first + b);
+            }
+            continue;
+        }
         double v = 0.0;
         for (int64_t r = threadIdx.x; r < a.m; r += blockDim.x) {
             double ax = 0.0;

@@ -19,7 +19,7 @@ __global__ __launch_bounds__(256) void k_commit(int32_t N, int64_t n, int64_t co
         if (x_cand) {
             const int32_t c = best[r];
             if (c >= 0 && c < ncand) src = (const double *)x_cand[r * ncand + c];
-        } else if (info_rows[r].status_val != IMPC_NON_CVX) {  // solveTraj's successSolve (:513-518)
+        } else if (impc_lib::solve_traj_ok(info_rows[r])) {  // solveTraj's successSolve (:475-478, :513-518)
             src = x_rows + r * n;
         }
         if (src) {
@@ -66,7 +66,9 @@ extern "C" int impc_replan_commit_device(impc_ctx ctx, int32_t horizon, int64_t 
 // ---- a receding window's next initial state from the last solve (impc_batch_follow_plan_device)
 namespace impc_replan_k {
 // mpcPlanner::getPos / getVel (mpcPlanner.cpp:1257-1290) on QP b's own solution, for the QPs
-// whose solve returned one; pos / vel [B][3] updated in place
+// whose solve returned one; pos / vel [B][3] updated in place.  Deliberately narrower than
+// solveTraj's success (impc_lib::solve_traj_ok, which the replan's commit uses): a receding window
+// of raw QPs does not move its x0 to an OSQP_NAN plan (infeasible / diverged QPs), DESIGN.md 2
 __global__ void k_follow(int64_t B, int32_t N, int64_t n, double ts, double t, const double *__restrict__ x,
                          const impc_info *__restrict__ info, double *__restrict__ pos, double *__restrict__ vel,
                          double *__restrict__ lin) {

@@ -5,25 +5,25 @@
 // called per planning instance by mpcNavigation.cpp:316-322.  Per instance it takes one of three
 // branches (:593-606) -- the intent fan-out with six candidate solves and a selection, or ONE
 // solveTraj (first plan, or no predictions) -- and commits the plan it gets into the planner state.
-// Here every instance of a batch goes through one call:
+// Every instance may track a different number of obstacles (predPos.size(), :343-373).  Here every
+// instance of a batch goes through one call, and the call never waits for the device:
 //
-//   k_branch_table       the branch of every instance and the compacted instance lists of each
-//                        branch (ascending), one workgroup; the three counts are the only bytes
-//                        the host reads back (they size the shapes' QP sets)
-//   gathers / repeats    the fan-out instances' inputs compacted (impc_gather_rows_device), each
-//                        candidate's x0 / xRef / linearisation point repeated per candidate
-//                        (impc_repeat_rows_device), the warm starts gathered from the plan state
-//                        straight into the batches' input arrays
-//   fan-out              impc_intent_fanout_device (findClosestObstacle + getIntentComb)
-//   assembly             impc_mpc_build_values_device per shape, written in place into the batches
-//   solve                ONE impc_batch_solve_group over every shape that has QPs
-//   validity             k_cand_valid: solveTraj's success from the candidates' impc_info
-//   selection            impc_fanout_candidates_device + impc_select_best_device
-//   commit               impc_replan_commit_device (fan-out winners, single solves), k_scatter
-//                        (per-instance outputs)
+//   k_plan_rows   one workgroup: the branch of every instance and the rows of every QP shape
+//                 (shape k = the QPs with k obstacle rows per stage), by a scan over the instances;
+//                 the device clock at the start of the replan
+//   k_pick        one thread per instance: findClosestObstacle + getIntentComb's candidate order
+//   k_prep        one wavefront per row: the warm start, the time limit and the obstacle sources
+//                 (which prediction / current obstacle each obstacle row linearises)
+//   build         impc_lib::build_rows per shape: the device builder straight from the per-instance
+//                 inputs, written in place into the shape's solver batch
+//   k_issue       the issue cut-off (:613) on the device clock; each shape's solve count
+//   solve         ONE impc_batch_solve_group over every shape, each batch's QP count read from
+//                 device memory by the solver itself
+//   k_cand        the candidates' validity (solveProblem NoError), solution pointers, obstacle sets
+//   selection     impc_select_best_device over every instance (non-fan-out instances: no candidate)
+//   k_commit      every plan into the planner state
 //
-// No x, y or QP value leaves the device.  The host work per call is the launches, one read of
-// the branch counts and the issue cut-off check (:613), which needs the assembly to have finished.
+// No x, y, QP value or count leaves the device, and nothing on the host waits for it.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -54,100 +54,392 @@
 
 namespace impc_rp {
 
-constexpr int kTableLanes = 1024;
+constexpr int kPlanLanes = 512;
+constexpr int kMaxObstacles = 30;
+constexpr int FORWARD = 0, LEFT = 1, RIGHT = 2, STOP = 3;  // dynamicPredictor's intent enum
 
-// The branch of every instance (:593-606) and the instance lists of each branch in ascending
-// order, by one workgroup: lane t owns a contiguous range of instances, an exclusive scan of the
-// per-lane counts gives each lane its output offsets.  Also resets the per-instance outputs of
-// the run (best_cand, ob_idx, cand_type, cand_slot = -1).
-//   ws_first[r]: the warm-start row of the r-th SINGLE_FIRST instance: row I (zeros) on a first
-//   plan (solveTraj :487-508, firstTime_), else the instance's plan.
-__global__ __launch_bounds__(kTableLanes) void k_branch_table(int64_t I, const int8_t *__restrict__ first_time,
-                                                              const int8_t *__restrict__ has_pred,
-                                                              const int32_t *__restrict__ cur_count, int cur_all,
-                                                              int8_t *__restrict__ branch, int64_t *__restrict__ inst_f,
-                                                              int64_t *__restrict__ inst_0, int64_t *__restrict__ ws_0,
-                                                              int64_t *__restrict__ inst_1, int64_t *__restrict__ counts,
-                                                              int32_t *__restrict__ best, int32_t *__restrict__ ob,
-                                                              int32_t *__restrict__ ctype, int32_t *__restrict__ cslot) {
-    __shared__ int64_t scan[3][kTableLanes];
-    const int t = threadIdx.x;
-    const int64_t per = (I + kTableLanes - 1) / kTableLanes;
-    const int64_t i0 = std::min<int64_t>(I, t * per), i1 = std::min<int64_t>(I, i0 + per);
-    auto decide = [&](int64_t i) -> int {
+// Shape k's rows in the flat row arrays: shape 0 holds the first-plan / obstacle-free single
+// solves (<= I rows); shapes 1..K at most four rows per instance (the four single-intent
+// candidates of an instance with K_i = k, or the two two-intent candidates of one with K_i + 1 =
+// k, or one current-obstacle single solve with c_i = k); shape K + 1 the two-intent candidates of
+// the instances with K_i = K (<= 2 I rows).
+__host__ __device__ inline int64_t shape_base(int64_t I, int k) { return k == 0 ? 0 : I + 4 * I * (int64_t)(k - 1); }
+__host__ __device__ inline int64_t shape_cap(int64_t I, int K, int k) { return k == 0 ? I : k <= K ? 4 * I : 2 * I; }
+__host__ __device__ inline int shape_of(int64_t I, int K, int64_t f) {
+    if (f < I) return 0;
+    const int64_t k = 1 + (f - I) / (4 * I);
+    return (int)(k < K + 1 ? k : K + 1);
+}
+
+// per-shape device pointers, fixed when the replan object is created
+struct ShapeDev {
+    double *xws, *tlim;       // the batch's warm-start input [cap][n] and time limits [cap]
+    const double *x;          // the batch's primal solutions [cap][n]
+    const impc_info *info;    // [cap]
+    int64_t *osrc;            // obstacle sources [cap][k] (build_rows)
+};
+
+// The branch of one instance (:593-606), its predicted-obstacle count K_i and current count c_i.
+struct Decide {
+    const int8_t *first_time, *has_pred;
+    const int32_t *num_pred, *cur_count;
+    int32_t K, cur_all;
+    __device__ void operator()(int64_t i, int &br, int &ki, int &ci) const {
         const bool ft = first_time[i] != 0;
-        const bool hp = has_pred ? has_pred[i] != 0 : true;
-        const bool cur = cur_count ? cur_count[i] > 0 : cur_all != 0;
-        return (!ft && hp) ? IMPC_REPLAN_FANOUT : (!ft && cur) ? IMPC_REPLAN_SINGLE_CURRENT : IMPC_REPLAN_SINGLE_FIRST;
-    };
-    int64_t c[3] = {0, 0, 0};
-    for (int64_t i = i0; i < i1; i++) c[decide(i)]++;
-    for (int k = 0; k < 3; k++) scan[k][t] = c[k];
-    __syncthreads();
-    for (int off = 1; off < kTableLanes; off <<= 1) {  // inclusive Hillis-Steele scan
-        int64_t v[3];
-        for (int k = 0; k < 3; k++) v[k] = t >= off ? scan[k][t - off] : 0;
-        __syncthreads();
-        for (int k = 0; k < 3; k++) scan[k][t] += v[k];
-        __syncthreads();
+        ki = num_pred ? min(max(num_pred[i], 0), K) : K;
+        const bool hp = (has_pred ? has_pred[i] != 0 : true) && ki > 0;  // obPredPos_.size() != 0
+        ci = cur_count ? min(max(cur_count[i], 0), K) : (cur_all ? K : 0);
+        br = (!ft && hp) ? IMPC_REPLAN_FANOUT : (!ft && ci > 0) ? IMPC_REPLAN_SINGLE_CURRENT : IMPC_REPLAN_SINGLE_FIRST;
     }
-    int64_t o[3];
-    for (int k = 0; k < 3; k++) o[k] = scan[k][t] - c[k];
+};
+
+struct PlanArgs {
+    int64_t I;
+    int32_t K, S;
+    Decide decide;
+    int8_t *branch;
+    int32_t *num_obs, *slot_row, *best;
+    int32_t *row_inst;
+    int8_t *row_code;
+    int64_t *cnt;               // [S] single solves per shape, [S .. 2S) rows per shape, [2S .. 2S+3) branches
+    unsigned long long *clk;    // [0] the device clock at the start of the replan
+};
+
+// One workgroup of kPlanLanes lanes, lane t owning a contiguous range of instances.  Counters
+// [R = 2S + 3][kPlanLanes] in LDS (rows 0..S-1: single solves of shape k, S..2S-1: candidate rows
+// of shape k, 2S..2S+2: instances per branch), an exclusive scan over the lanes (a wavefront scan
+// of 64 lanes, then the wavefront totals), and a second pass that writes each instance's rows in
+// ascending order: every shape holds its single solves first, then its candidates.
+__global__ __launch_bounds__(kPlanLanes) void k_plan_rows(PlanArgs a) {
+    extern __shared__ int32_t cl[];  // [R][kPlanLanes], then wave totals [R][kPlanLanes / 64]
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, NW = kPlanLanes / 64;
+    const int S = a.S, R = 2 * S + 3;
+    int32_t *wt = cl + R * kPlanLanes;
+    if (t == 0) a.clk[0] = wall_clock64();
+    const int64_t per = (a.I + kPlanLanes - 1) / kPlanLanes;
+    const int64_t i0 = min(a.I, (int64_t)t * per), i1 = min(a.I, i0 + per);
+    for (int r = 0; r < R; r++) cl[r * kPlanLanes + t] = 0;
     for (int64_t i = i0; i < i1; i++) {
-        const int br = decide(i);
-        branch[i] = (int8_t)br;
+        int br, ki, ci;
+        a.decide(i, br, ki, ci);
+        cl[(2 * S + br) * kPlanLanes + t]++;
         if (br == IMPC_REPLAN_FANOUT) {
-            inst_f[o[0]++] = i;
-        } else if (br == IMPC_REPLAN_SINGLE_FIRST) {
-            ws_0[o[1]] = first_time[i] != 0 ? I : i;
-            inst_0[o[1]++] = i;
+            cl[(S + ki) * kPlanLanes + t] += 4;
+            cl[(S + ki + 1) * kPlanLanes + t] += 2;
         } else {
-            inst_1[o[2]++] = i;
+            cl[(br == IMPC_REPLAN_SINGLE_FIRST ? 0 : ci) * kPlanLanes + t]++;
         }
-        best[i] = -1;
-        ob[i] = -1;
-        for (int k = 0; k < 6; k++) ctype[6 * i + k] = cslot[6 * i + k] = -1;
     }
-    if (t == kTableLanes - 1)
-        for (int k = 0; k < 3; k++) counts[k] = scan[k][t];
+    for (int r = 0; r < R; r++) {  // exclusive scan inside each wavefront
+        const int v = cl[r * kPlanLanes + t];
+        int x = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        cl[r * kPlanLanes + t] = x - v;
+        if (lane == 63) wt[r * NW + w] = x;
+    }
+    __syncthreads();
+    for (int r = 0; r < R; r++) {
+        int add = 0;
+        for (int ww = 0; ww < w; ww++) add += wt[r * NW + ww];
+        cl[r * kPlanLanes + t] += add;
+    }
+    auto total = [&](int r) {
+        int64_t s = 0;
+        for (int ww = 0; ww < NW; ww++) s += wt[r * NW + ww];
+        return s;
+    };
+    for (int64_t i = i0; i < i1; i++) {
+        int br, ki, ci;
+        a.decide(i, br, ki, ci);
+        a.branch[i] = (int8_t)br;
+        a.best[i] = -1;
+        int32_t *sr = a.slot_row + 6 * i;
+        for (int s = 0; s < 6; s++) sr[s] = -1;
+        if (br == IMPC_REPLAN_FANOUT) {
+            a.num_obs[i] = ki;
+            for (int s = 0; s < 6; s++) {
+                const int k = s < 4 ? ki : ki + 1;
+                const int64_t r = total(k) + cl[(S + k) * kPlanLanes + t]++;
+                const int64_t f = shape_base(a.I, k) + r;
+                a.row_inst[f] = (int32_t)i;
+                a.row_code[f] = (int8_t)s;
+                sr[s] = (int32_t)r;
+            }
+        } else {
+            const int k = br == IMPC_REPLAN_SINGLE_FIRST ? 0 : ci;
+            const int64_t r = cl[k * kPlanLanes + t]++;
+            const int64_t f = shape_base(a.I, k) + r;
+            a.row_inst[f] = (int32_t)i;
+            a.row_code[f] = (int8_t)(k == 0 ? IMPC_REPLAN_ROW_FIRST : IMPC_REPLAN_ROW_CURRENT);
+            a.num_obs[i] = k;
+            sr[0] = (int32_t)r;
+        }
+    }
+    if (t == 0) {
+        for (int k = 0; k < S; k++) {
+            a.cnt[k] = total(k);
+            a.cnt[S + k] = total(k) + total(S + k);
+        }
+        for (int b = 0; b < 3; b++) a.cnt[2 * S + b] = total(2 * S + b);
+    }
 }
 
-// updateDynamicObstacles (:316-341): each current obstacle's position / size held over the T
-// prediction steps of the single-solve QP: out[r][k][s][:] = src[inst[r]][k][:]
-__global__ void k_hold(const double *__restrict__ src, const int64_t *__restrict__ inst, int64_t count, int32_t K,
-                       int32_t T, double *__restrict__ out) {
-    const int64_t total = count * K * T * 3;
+__device__ inline double norm3(double a, double b, double c) {
+#pragma clang fp contract(off)
+    return sqrt((a * a + b * b) + c * c);
+}
+
+// maxCoeff (:762): the first most probable intent of one obstacle's [4] probabilities
+__device__ inline int max_intent(const double *p) {
+    int m = 0;
+    for (int q = 1; q < 4; q++)
+        if (p[q] > p[m]) m = q;
+    return m;
+}
+
+struct PickArgs {
+    int64_t I;
+    int32_t K, N;
+    const int8_t *branch;
+    const int32_t *num_obs;
+    const double *pos, *plan_states, *dyn_cur, *prob;
+    const int32_t *prev_count;
+    int32_t *ob, *ctype, *cslot, *slot_type;
+    double *cprob;
+};
+
+// findClosestObstacle (:663-708, over the instance's K_i obstacles; a fan-out instance is never on
+// its first plan) and getIntentComb's order (:719-756: std::sort of (weight, index) pairs, taken
+// from the back); single-solve instances get -1.  As impc_intent_fanout_device (fanout.hpp), with
+// the obstacle count per instance.
+__global__ __launch_bounds__(64) void k_pick(PickArgs a) {
+#pragma clang fp contract(off)
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.I) return;
+    int32_t *ct = a.ctype + 6 * i, *cs = a.cslot + 6 * i, *sty = a.slot_type + 6 * i;
+    if (a.branch[i] != IMPC_REPLAN_FANOUT) {
+        a.ob[i] = -1;
+        for (int c = 0; c < 6; c++) ct[c] = cs[c] = sty[c] = -1;
+        return;
+    }
+    const int K = a.K, Ki = a.num_obs[i];
+    const double *cp = a.pos + 3 * i, *dc = a.dyn_cur + i * K * 3;
+    int ob = -1;
+    double minD = INFINITY;
+    const int pc = a.prev_count[i];
+    if (pc < 2) {  // distance to the current position (:676-686)
+        for (int k = 0; k < Ki; k++) {
+            const double d = norm3(cp[0] - dc[3 * k], cp[1] - dc[3 * k + 1], cp[2] - dc[3 * k + 2]);
+            if (d < minD) {
+                minD = d;
+                ob = k;
+            }
+        }
+    } else {  // direction-weighted, every term at states[0] / states[1] as written (:687-706)
+        const double *s = a.plan_states + i * (int64_t)a.N * 8, *ns = s + 8;
+        const double traj = atan2(ns[1] - s[1], ns[0] - s[0]);
+        for (int k = 0; k < Ki; k++) {
+            const double obs = atan2(dc[3 * k + 1] - s[1], dc[3 * k] - s[0]);
+            const double d = norm3(s[0] - dc[3 * k], s[1] - dc[3 * k + 1], s[2] - dc[3 * k + 2]);
+            double dist = 0.0;
+            for (int j = 0; j < pc / 3; j++) {
+                const double w = exp((double)-j);
+                dist += w * d * (3.0 - cos(traj - obs));
+                if (dist > minD) break;
+            }
+            if (dist < minD) {
+                minD = dist;
+                ob = k;
+            }
+        }
+    }
+    if (ob < 0) ob = 0;  // only with NaN inputs (the reference would index -1)
+    a.ob[i] = ob;
+    const double *pr = a.prob + (i * K + ob) * 4;
+    const double w[6] = {pr[STOP], pr[LEFT], pr[RIGHT], pr[FORWARD], pr[LEFT] < pr[FORWARD] ? pr[FORWARD] : pr[LEFT],
+                         pr[RIGHT] < pr[FORWARD] ? pr[FORWARD] : pr[RIGHT]};
+    int type_at[6];
+    for (int t = 0; t < 6; t++) {
+        int pos = 0;
+        for (int u = 0; u < 6; u++)
+            if (w[t] < w[u] || (!(w[u] < w[t]) && t < u)) pos++;
+        type_at[pos] = t;
+    }
+    int ns_ = 0, np_ = 0;
+    for (int c = 0; c < 6; c++) {
+        const int t = type_at[c];
+        const int s = t < 4 ? ns_++ : 4 + np_++;
+        ct[c] = t;
+        cs[c] = s;
+        sty[s] = t;
+    }
+    for (int q = 0; q < 4; q++) a.cprob[4 * i + q] = pr[q];
+}
+
+// Obstacle o of slot s's candidate (getIntentComb :731-768): the closest obstacle's intents
+// first, then every other obstacle in index order at its most probable intent.
+__device__ inline void cand_obstacle(int ob, int t, bool pair, int o, const double *prob_i, int &k, int &intent) {
+    const int nfirst = pair ? 2 : 1;
+    if (o < nfirst) {
+        k = ob;
+        constexpr int single_intent[4] = {STOP, LEFT, RIGHT, FORWARD};
+        intent = t < 4 ? single_intent[t] : (o == 0 ? (t == 4 ? LEFT : RIGHT) : FORWARD);
+    } else {
+        const int q = o - nfirst;
+        k = q < ob ? q : q + 1;
+        intent = max_intent(prob_i + 4 * k);
+    }
+}
+
+struct PrepArgs {
+    int64_t I, n, total;
+    int32_t K, L, S;
+    const int64_t *cnt;
+    const ShapeDev *sh;
+    const int32_t *row_inst, *ob, *slot_type;
+    const int8_t *row_code, *first_time;
+    const double *plan_x, *prob;
+    double cand_limit;
+};
+
+// One wavefront per row (grid-stride over every shape's capacity; rows past a shape's count are
+// skipped): the warm start (solveTraj :485-509: the plan, or zeros on a first plan -- row I of
+// plan_x), the row's time limit (candidates: timeLimit; single solves: none, :442-444) and the
+// sources of its obstacle rows for the builder.
+__global__ __launch_bounds__(64) void k_prep(PrepArgs a) {
+    for (int64_t f = blockIdx.x; f < a.total; f += gridDim.x) {
+        const int k = shape_of(a.I, a.K, f);
+        const int64_t r = f - shape_base(a.I, k);
+        if (r >= a.cnt[a.S + k]) continue;
+        const ShapeDev sd = a.sh[k];
+        const int64_t i = a.row_inst[f];
+        const int code = a.row_code[f];
+        const double *src = a.plan_x + ((code == IMPC_REPLAN_ROW_FIRST && a.first_time[i]) ? a.I : i) * a.n;
+        double *dst = sd.xws + r * a.n;
+        for (int64_t e = threadIdx.x; e < a.n; e += blockDim.x) dst[e] = src[e];
+        if (threadIdx.x == 0) sd.tlim[r] = code < 6 ? a.cand_limit : 0.0;
+        for (int o = threadIdx.x; o < k; o += blockDim.x) {
+            int64_t off;
+            if (code == IMPC_REPLAN_ROW_CURRENT) {  // held over the horizon
+                off = ((i * a.K + o) * 3) << 1 | 1;
+            } else {
+                int kk, intent;
+                cand_obstacle(a.ob[i], a.slot_type[6 * i + code], code >= 4, o, a.prob + i * a.K * 4, kk, intent);
+                off = ((((i * a.K + kk) * 4 + intent) * (int64_t)a.L) * 3) << 1;
+            }
+            sd.osrc[r * k + o] = off;
+        }
+    }
+}
+
+// The issue cut-off (:612-613) after the assembly, on the device clock; the solve count of each
+// shape (its single solves always, its candidates when issued)
+__global__ void k_issue(int32_t S, int64_t *cnt, int64_t *solve, unsigned long long *clk, int32_t *issued_out,
+                        double elapsed_s, double tick, double cutoff) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const unsigned long long now = wall_clock64();
+    clk[1] = now;
+    const double elapsed = elapsed_s + (double)(now - clk[0]) * tick;
+    const bool issued = !(cutoff > 0.0) || elapsed < cutoff;
+    for (int k = 0; k < S; k++) solve[k] = issued ? cnt[S + k] : cnt[k];
+    *issued_out = issued ? 1 : 0;
+}
+
+struct CandArgs {
+    int64_t I, n;
+    int32_t K, L;
+    const ShapeDev *sh;
+    const int8_t *branch;
+    const int32_t *num_obs, *slot_row, *cslot, *slot_type, *ob;
+    const int32_t *issued;
+    const double *pred_pos, *pred_size, *prob;
+    const double **x_cand;
+    int32_t *dyn_count;
+    int8_t *valid;
+    double *dpos, *dsize;  // [I][6][K + 1][L][3], the selection's padded obstacle sets
+};
+
+// per (instance, candidate): solveTraj's success (impc_lib::solve_traj_ok, :475-478, :513-518) when issued,
+// the pointer to the solution, the obstacle count
+__global__ void k_cand(CandArgs a) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.I * 6; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = e / 6;
+        if (a.branch[i] != IMPC_REPLAN_FANOUT) {
+            a.valid[e] = 0;
+            a.x_cand[e] = nullptr;
+            a.dyn_count[e] = 0;
+            continue;
+        }
+        const int s = a.cslot[e], k = s < 4 ? a.num_obs[i] : a.num_obs[i] + 1;
+        const int64_t r = a.slot_row[6 * i + s];
+        a.valid[e] = (*a.issued && impc_lib::solve_traj_ok(a.sh[k].info[r])) ? 1 : 0;
+        a.x_cand[e] = a.sh[k].x + r * a.n;
+        a.dyn_count[e] = k;
+    }
+}
+
+// the candidates' obstacle sets in the selection's padded layout (entries past a candidate's
+// count are never read by the selection and are not written)
+__global__ void k_sel_sets(CandArgs a) {
+    const int64_t per_c = (int64_t)(a.K + 1) * a.L, total = a.I * 6 * per_c;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t c = e % 3, s = e / 3, k = (s / T) % K, r = s / ((int64_t)T * K);
-        out[e] = src[(inst[r] * K + k) * 3 + c];
+        const int64_t ic = e / per_c, i = ic / 6;
+        if (a.branch[i] != IMPC_REPLAN_FANOUT) continue;
+        const int rr = (int)(e - ic * per_c), o = rr / a.L, st = rr % a.L;
+        const int s = a.cslot[ic];
+        const bool pair = s >= 4;
+        if (o >= a.num_obs[i] + (pair ? 1 : 0)) continue;
+        int kk, intent;
+        cand_obstacle(a.ob[i], a.slot_type[6 * i + s], pair, o, a.prob + i * a.K * 4, kk, intent);
+        const int64_t src = (((i * a.K + kk) * 4 + intent) * (int64_t)a.L + st) * 3;
+        for (int d = 0; d < 3; d++) {
+            a.dpos[e * 3 + d] = a.pred_pos[src + d];
+            a.dsize[e * 3 + d] = a.pred_size[src + d];
+        }
     }
 }
 
-// candidate c of fan-out instance j is valid when it was issued and solveTraj succeeded
-// (solveProblem NoError = every OSQP status but NON_CVX, :513-518); slot s < 4 is row 4 j + s of
-// the single-intent batch, else row 2 j + s - 4 of the two-intent batch (fanout.hpp)
-__global__ void k_cand_valid(int64_t nf, const int32_t *__restrict__ cand_slot, const impc_info *__restrict__ info_s,
-                             const impc_info *__restrict__ info_p, int issued, int8_t *__restrict__ valid) {
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nf * 6; e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t j = e / 6;
-        const int32_t s = cand_slot[e];
-        const impc_info &inf = s < 4 ? info_s[4 * j + s] : info_p[2 * j + (s - 4)];
-        valid[e] = (issued && inf.status_val != IMPC_NON_CVX) ? 1 : 0;
-    }
-}
+struct CommitArgs {
+    int64_t I, n;
+    int32_t N;
+    const ShapeDev *sh;
+    const int8_t *branch;
+    const int32_t *num_obs, *slot_row, *best;
+    const double *const *x_cand;
+    double *plan_x, *plan_states;
+    int32_t *prev_count;
+    int8_t *first_time, *valid;
+};
 
-// the fan-out instances' per-instance outputs, from their compacted rows to instance order
-__global__ void k_scatter(int64_t nf, const int64_t *__restrict__ inst_f, const int32_t *__restrict__ best_f,
-                          const int32_t *__restrict__ ob_f, const int32_t *__restrict__ ctype_f,
-                          const int32_t *__restrict__ cslot_f, int32_t *__restrict__ best, int32_t *__restrict__ ob,
-                          int32_t *__restrict__ ctype, int32_t *__restrict__ cslot) {
-    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nf; j += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = inst_f[j];
-        best[i] = best_f[j];
-        ob[i] = ob_f[j];
-        for (int k = 0; k < 6; k++) {
-            ctype[6 * i + k] = ctype_f[6 * j + k];
-            cslot[6 * i + k] = cslot_f[6 * j + k];
+// every plan into the planner state (:629-639 / :653-657): the selected candidate of a fan-out
+// instance, the single solve when solveTraj succeeded; an instance without a plan keeps its state
+__global__ __launch_bounds__(64) void k_commit(CommitArgs a) {
+    for (int64_t i = blockIdx.x; i < a.I; i += gridDim.x) {
+        const double *src = nullptr;
+        if (a.branch[i] == IMPC_REPLAN_FANOUT) {
+            const int b = a.best[i];
+            if (b >= 0) src = a.x_cand[6 * i + b];
+        } else {
+            const int k = a.num_obs[i];
+            const int64_t r = a.slot_row[6 * i];
+            if (impc_lib::solve_traj_ok(a.sh[k].info[r])) src = a.sh[k].x + r * a.n;
+        }
+        if (src) {
+            for (int64_t e = threadIdx.x; e < a.n; e += blockDim.x) {
+                const double v = src[e];
+                a.plan_x[i * a.n + e] = v;
+                if (e < (int64_t)8 * a.N) a.plan_states[i * (int64_t)a.N * 8 + e] = v;
+            }
+        }
+        if (threadIdx.x == 0) {
+            if (src) {
+                a.prev_count[i] = a.N;
+                a.first_time[i] = 0;
+            }
+            a.valid[i] = src ? 1 : 0;
         }
     }
 }
@@ -187,19 +479,14 @@ struct Arena {
     }
 };
 
-// one QP shape of the replan: its solver batch, its on-device builder, and the per-QP inputs of
-// the assembly (cap rows)
+// one QP shape of the replan (k obstacle rows per stage): its solver batch and on-device builder
 struct Shape {
-    int32_t K = 0, L = 0, rep = 1;
-    int64_t cap = 0, count = 0, ninst = 0;
+    int32_t k = 0;
+    int64_t cap = 0;
     impc_qp_dims dm{};
     impc_batch batch = nullptr;
     impc_mpc_builder bld = nullptr;
-    double *pos = nullptr, *vel = nullptr, *xref = nullptr, *lin = nullptr;
-    double *dpos = nullptr, *dsize = nullptr;  // the current-obstacle shape's held obstacles
-    const int64_t *inst = nullptr;            // instances of the last run (device)
-    bool tlim_known = false;
-    double tlim = 0.0;                        // per-QP time limit uploaded last (< 0: none)
+    ShapeDev dev{};
 };
 
 }  // namespace impc_rp
@@ -209,43 +496,43 @@ using namespace impc_rp;
 struct impc_replan_s {
     impc_ctx ctx = nullptr;
     impc_replan_config cfg{};
-    int64_t I = 0, n = 0;
-    int32_t N = 0, K = 0, L = 0;
+    int64_t I = 0, n = 0, rows = 0;
+    int32_t N = 0, K = 0, L = 0, S = 0;
     Arena mem;
     // planner state
     double *plan_x = nullptr, *plan_states = nullptr;
     int32_t *prev_count = nullptr;
     int8_t *first_time = nullptr, *valid = nullptr, *zeros8 = nullptr;
-    // branch table
-    int8_t *branch = nullptr;
-    int64_t *inst_f = nullptr, *inst_0 = nullptr, *ws_0 = nullptr, *inst_1 = nullptr, *d_counts = nullptr;
-    int64_t *h_counts = nullptr;  // pinned
-    // per-instance outputs
-    int32_t *best = nullptr, *ob = nullptr, *ctype = nullptr, *cslot = nullptr;
-    // fan-out: compacted inputs and outputs
-    double *f_pos = nullptr, *f_vel = nullptr, *f_xref = nullptr, *f_lin = nullptr, *f_dcur = nullptr;
-    double *f_ppos = nullptr, *f_psize = nullptr, *f_prob = nullptr, *f_ws = nullptr;
-    int32_t *f_pc = nullptr;
-    int32_t *f_ob = nullptr, *f_ctype = nullptr, *f_cslot = nullptr;
-    double *f_cprob = nullptr, *s_pos = nullptr, *s_size = nullptr, *p_pos = nullptr, *p_size = nullptr;
+    // rows of the shapes and per-instance outputs
+    int8_t *branch = nullptr, *row_code = nullptr;
+    int32_t *row_inst = nullptr, *num_obs = nullptr, *slot_row = nullptr, *slot_type = nullptr;
+    int32_t *best = nullptr, *ob = nullptr, *ctype = nullptr, *cslot = nullptr, *issued = nullptr;
+    int64_t *cnt = nullptr, *solve = nullptr;
+    unsigned long long *clk = nullptr;
+    double *cprob = nullptr;
+    ShapeDev *d_sh = nullptr;
     // selection
     const double **x_cand = nullptr;
-    int32_t *dyn_count = nullptr, *best_f = nullptr, *best_pos = nullptr;
+    int32_t *dyn_count = nullptr, *best_pos = nullptr;
     double *dyn_pos = nullptr, *dyn_size = nullptr, *scores = nullptr, *weighted = nullptr;
     int8_t *cvalid = nullptr;
-    Shape sh[4];  // 0 single-intent, 1 two-intent, 2 single solve (no obstacles), 3 current obstacles
+    std::vector<Shape> sh;  // S = K + 2 shapes, by obstacle count
+    std::vector<impc_batch> group;
     impc_replan_stats stats{};
+    bool ran = false;
+    double last_limit = 0.0;
+    double last_total_s = 0.0;
 };
 
 namespace {
 
 int fail(int code, const char *msg) { return impc_lib::set_error(code, msg); }
 
-int make_shape(impc_replan rp, Shape &s, int32_t K, int32_t L, int32_t rep, int64_t cap, bool held) {
-    s.K = K, s.L = L, s.rep = rep, s.cap = cap;
-    RP_TRY(impc_mpc_dims(&rp->cfg.mpc, 0, K, &s.dm));
+int make_shape(impc_replan rp, Shape &s, int32_t k, int64_t cap) {
+    s.k = k, s.cap = cap;
+    RP_TRY(impc_mpc_dims(&rp->cfg.mpc, 0, k, &s.dm));
     std::vector<int64_t> Pp(s.dm.n + 1), Pi(std::max<int64_t>(s.dm.nnzP, 1)), Ap(s.dm.n + 1), Ai(s.dm.nnzA);
-    RP_TRY(impc_mpc_build_pattern(&rp->cfg.mpc, 0, K, Pp.data(), Pi.data(), Ap.data(), Ai.data()));
+    RP_TRY(impc_mpc_build_pattern(&rp->cfg.mpc, 0, k, Pp.data(), Pi.data(), Ap.data(), Ai.data()));
     RP_TRY(impc_batch_create(rp->ctx, s.dm.n, s.dm.m, Pp.data(), Pi.data(), Ap.data(), Ai.data(), cap, &s.batch));
     RP_TRY(impc_batch_set_settings(s.batch, &rp->cfg.settings));
     if (rp->cfg.queue_order == IMPC_QUEUE_LONGEST_FIRST) {
@@ -253,18 +540,18 @@ int make_shape(impc_replan rp, Shape &s, int32_t K, int32_t L, int32_t rep, int6
         const double qw = 1.0 / (10.0 * (rp->N - 1) * rp->cfg.mpc.position_weight);
         RP_TRY(impc_batch_set_queue_order(s.batch, IMPC_QUEUE_LONGEST_FIRST, qw));
     }
-    RP_TRY(impc_mpc_builder_create(rp->ctx, &rp->cfg.mpc, 0, K, L, &s.bld));
-    const int64_t N = rp->N;
-    // x0, reference and linearisation point of every QP: per-candidate copies (rep > 1) or the
-    // single solves' gathered rows
-    RP_TRY(rp->mem.get((size_t)(cap * 3), &s.pos));
-    RP_TRY(rp->mem.get((size_t)(cap * 3), &s.vel));
-    RP_TRY(rp->mem.get((size_t)(cap * N * 8), &s.xref));
-    RP_TRY(rp->mem.get((size_t)(cap * N * 8), &s.lin));
-    if (held) {
-        RP_TRY(rp->mem.get((size_t)(cap * K * L * 3), &s.dpos));
-        RP_TRY(rp->mem.get((size_t)(cap * K * L * 3), &s.dsize));
-    }
+    RP_TRY(impc_batch_set_kernel(s.batch, IMPC_KERNEL_STRUCTURED));
+    RP_TRY(impc_mpc_builder_create(rp->ctx, &rp->cfg.mpc, 0, k, rp->L, &s.bld));
+    impc_lib::BatchInputs bi{};
+    RP_TRY(impc_lib::batch_inputs_view(s.batch, &bi));
+    double *x = nullptr;
+    impc_info *info = nullptr;
+    RP_TRY(impc_batch_device_results(s.batch, &x, nullptr, &info));
+    s.dev.xws = bi.xws;
+    s.dev.x = x;
+    s.dev.info = info;
+    RP_TRY(impc_lib::batch_tlim_device(s.batch, &s.dev.tlim));
+    RP_TRY(rp->mem.get((size_t)std::max<int64_t>(1, cap * k), &s.dev.osrc));
     return IMPC_OK;
 }
 
@@ -275,49 +562,8 @@ void free_shape(Shape &s) {
     s.bld = nullptr;
 }
 
-// per-QP time limits of a shape's batch, uploaded only when they change (the upload waits for the
-// launches in flight): `v` for every QP, or none (v == 0 with no limit in the settings)
-int set_limit(impc_replan rp, Shape &s, double v) {
-    if (s.tlim_known && s.tlim == v) return IMPC_OK;
-    if (v == 0.0 && rp->cfg.settings.time_limit == 0.0) {
-        RP_TRY(impc_batch_set_time_limits(s.batch, nullptr));
-    } else {
-        std::vector<double> lim((size_t)s.cap, v);
-        RP_TRY(impc_batch_set_time_limits(s.batch, lim.data()));
-    }
-    s.tlim_known = true;
-    s.tlim = v;
-    return IMPC_OK;
-}
-
-// The assembly of one shape's `ninst` instances into its batch: x0, reference and linearisation
-// point per QP (already in s.pos / vel / xref / lin), the obstacle sets (dyn_pos / dyn_size), the
-// warm start gathered from the plan state by ws_idx and repeated per candidate (ws_tmp: [ninst][n]
-// scratch when rep > 1).
-int assemble(impc_replan rp, Shape &s, int64_t ninst, const double *lin, const double *dyn_pos, const double *dyn_size,
-             const int64_t *ws_idx, double *ws_tmp) {
-    s.ninst = ninst;
-    s.count = ninst * s.rep;
-    if (!s.count) return IMPC_OK;
-    impc_ctx ctx = rp->ctx;
-    impc_lib::BatchInputs in{};
-    RP_TRY(impc_lib::batch_inputs_begin(s.batch, &in));
-    if (in.n != rp->n) return fail(IMPC_INVALID_ARGUMENT, "replan shape: n != 13 N - 5");
-    const int64_t wbytes = 8 * rp->n;
-    if (s.rep == 1) {
-        RP_TRY(impc_gather_rows_device(ctx, rp->plan_x, wbytes, ws_idx, ninst, in.xws, nullptr));
-    } else {
-        RP_TRY(impc_gather_rows_device(ctx, rp->plan_x, wbytes, ws_idx, ninst, ws_tmp, nullptr));
-        RP_TRY(impc_repeat_rows_device(ctx, ws_tmp, ninst, wbytes, s.rep, in.xws, nullptr));
-    }
-    RP_TRY(impc_mpc_build_values_device(s.bld, s.count, s.pos, s.vel, s.xref, lin, nullptr, nullptr, nullptr, dyn_pos,
-                                        dyn_size, in.Px, in.q, in.Ax, in.l, in.u, nullptr));
-    RP_TRY(impc_lib::batch_inputs_end(s.batch, true));
-    return impc_batch_set_active(s.batch, s.count);
-}
-
-unsigned grid_for(impc_replan rp, int64_t work) {
-    return (unsigned)std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, (int64_t)impc_lib::num_cu(rp->ctx) * 8));
+unsigned grid_for(impc_replan rp, int64_t work, int per = 256) {
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>((work + per - 1) / per, (int64_t)impc_lib::num_cu(rp->ctx) * 8));
 }
 
 }  // namespace
@@ -329,8 +575,9 @@ int impc_replan_create(impc_ctx ctx, const impc_replan_config *cfg, impc_replan 
     *out = nullptr;
     const int64_t I = cfg->instances;
     const int32_t N = cfg->mpc.horizon, K = cfg->num_obstacles, L = cfg->pred_len;
-    if (I < 1 || I > ((int64_t)1 << 26) || N < 2 || K < 1 || L < 1)
-        return fail(IMPC_INVALID_ARGUMENT, "replan: instances >= 1, horizon >= 2, num_obstacles >= 1, pred_len >= 1");
+    if (I < 1 || I > ((int64_t)1 << 24) || N < 2 || K < 1 || K > kMaxObstacles || L < 1)
+        return fail(IMPC_INVALID_ARGUMENT,
+                    "replan: 1 <= instances <= 2^24, horizon >= 2, 1 <= num_obstacles <= 30, pred_len >= 1");
     if (cfg->mpc.num_half_space != 0)
         return fail(IMPC_UNSUPPORTED, "replan: the live planner path has no FOV half-spaces (num_half_space = 0)");
     if (cfg->queue_order != IMPC_QUEUE_FIFO && cfg->queue_order != IMPC_QUEUE_LONGEST_FIRST)
@@ -339,14 +586,14 @@ int impc_replan_create(impc_ctx ctx, const impc_replan_config *cfg, impc_replan 
     std::unique_ptr<impc_replan_s> rp(new impc_replan_s());
     rp->ctx = ctx;
     rp->cfg = *cfg;
-    rp->I = I, rp->N = N, rp->K = K, rp->L = L;
+    rp->I = I, rp->N = N, rp->K = K, rp->L = L, rp->S = K + 2;
     rp->n = 13 * (int64_t)N - 5;
-    const int64_t n = rp->n;
+    rp->rows = shape_base(I, K + 1) + shape_cap(I, K, K + 1);
+    const int64_t n = rp->n, S = rp->S;
     Arena &a = rp->mem;
     int rc = IMPC_OK;
     auto cleanup = [&]() {
         for (Shape &s : rp->sh) free_shape(s);
-        if (rp->h_counts) (void)hipHostFree(rp->h_counts);
         rp->mem.release();
     };
 #define RP_CK(expr)       \
@@ -361,58 +608,57 @@ int impc_replan_create(impc_ctx ctx, const impc_replan_config *cfg, impc_replan 
     RP_CK(a.get((size_t)I, &rp->valid));
     RP_CK(a.get((size_t)I, &rp->zeros8));
     RP_CK(a.get((size_t)I, &rp->branch));
-    RP_CK(a.get((size_t)I, &rp->inst_f));
-    RP_CK(a.get((size_t)I, &rp->inst_0));
-    RP_CK(a.get((size_t)I, &rp->ws_0));
-    RP_CK(a.get((size_t)I, &rp->inst_1));
-    RP_CK(a.get((size_t)4, &rp->d_counts));
+    RP_CK(a.get((size_t)rp->rows, &rp->row_inst));
+    RP_CK(a.get((size_t)rp->rows, &rp->row_code));
+    RP_CK(a.get((size_t)I, &rp->num_obs));
+    RP_CK(a.get((size_t)(6 * I), &rp->slot_row));
+    RP_CK(a.get((size_t)(6 * I), &rp->slot_type));
     RP_CK(a.get((size_t)I, &rp->best));
     RP_CK(a.get((size_t)I, &rp->ob));
     RP_CK(a.get((size_t)(6 * I), &rp->ctype));
     RP_CK(a.get((size_t)(6 * I), &rp->cslot));
-    RP_CK(a.get((size_t)(3 * I), &rp->f_pos));
-    RP_CK(a.get((size_t)(3 * I), &rp->f_vel));
-    RP_CK(a.get((size_t)(I * N * 8), &rp->f_xref));
-    RP_CK(a.get((size_t)(I * N * 8), &rp->f_lin));
-    RP_CK(a.get((size_t)(I * K * 3), &rp->f_dcur));
-    RP_CK(a.get((size_t)(I * K * 4 * L * 3), &rp->f_ppos));
-    RP_CK(a.get((size_t)(I * K * 4 * L * 3), &rp->f_psize));
-    RP_CK(a.get((size_t)(I * K * 4), &rp->f_prob));
-    RP_CK(a.get((size_t)(I * n), &rp->f_ws));
-    RP_CK(a.get((size_t)I, &rp->f_pc));
-    RP_CK(a.get((size_t)I, &rp->f_ob));
-    RP_CK(a.get((size_t)(6 * I), &rp->f_ctype));
-    RP_CK(a.get((size_t)(6 * I), &rp->f_cslot));
-    RP_CK(a.get((size_t)(4 * I), &rp->f_cprob));
-    RP_CK(a.get((size_t)(I * 4 * K * L * 3), &rp->s_pos));
-    RP_CK(a.get((size_t)(I * 4 * K * L * 3), &rp->s_size));
-    RP_CK(a.get((size_t)(I * 2 * (K + 1) * L * 3), &rp->p_pos));
-    RP_CK(a.get((size_t)(I * 2 * (K + 1) * L * 3), &rp->p_size));
+    RP_CK(a.get((size_t)1, &rp->issued));
+    RP_CK(a.get((size_t)(2 * S + 3), &rp->cnt));
+    RP_CK(a.get((size_t)S, &rp->solve));
+    RP_CK(a.get((size_t)2, &rp->clk));
+    RP_CK(a.get((size_t)(4 * I), &rp->cprob));
+    RP_CK(a.get((size_t)S, &rp->d_sh));
     RP_CK(a.get((size_t)(6 * I), &rp->x_cand));
     RP_CK(a.get((size_t)(6 * I), &rp->dyn_count));
-    RP_CK(a.get((size_t)I, &rp->best_f));
     RP_CK(a.get((size_t)I, &rp->best_pos));
     RP_CK(a.get((size_t)(I * 6 * (K + 1) * L * 3), &rp->dyn_pos));
     RP_CK(a.get((size_t)(I * 6 * (K + 1) * L * 3), &rp->dyn_size));
     RP_CK(a.get((size_t)(I * 6 * 3), &rp->scores));
     RP_CK(a.get((size_t)(I * 6), &rp->weighted));
     RP_CK(a.get((size_t)(I * 6), &rp->cvalid));
-    if (hipHostMalloc((void **)&rp->h_counts, 4 * sizeof(int64_t), hipHostMallocDefault) != hipSuccess) {
-        rp->h_counts = nullptr;
-        cleanup();
-        return fail(IMPC_MEM_ALLOC_ERROR, "replan: pinned counts");
-    }
     hipStream_t st = impc_lib::stream(ctx);
     if (hipMemsetAsync(rp->zeros8, 0, (size_t)I, st) != hipSuccess ||
-        hipMemsetAsync(rp->valid, 0, (size_t)I, st) != hipSuccess) {
+        hipMemsetAsync(rp->valid, 0, (size_t)I, st) != hipSuccess ||
+        hipMemsetAsync(rp->cnt, 0, sizeof(int64_t) * (size_t)(2 * S + 3), st) != hipSuccess ||
+        hipMemsetAsync(rp->solve, 0, sizeof(int64_t) * (size_t)S, st) != hipSuccess) {
         cleanup();
         return fail(IMPC_DEVICE_ERROR, "replan: memset");
     }
-    // fan-out shapes (single-intent K obstacles, 4 per instance; two-intent K + 1, 2 per instance)
-    // and the obstacle-free single solve; the current-obstacle shape is created on first use
-    RP_CK(make_shape(rp.get(), rp->sh[0], K, L, 4, 4 * I, false));
-    RP_CK(make_shape(rp.get(), rp->sh[1], K + 1, L, 2, 2 * I, false));
-    RP_CK(make_shape(rp.get(), rp->sh[2], 0, 1, 1, I, false));
+    // one solver batch per obstacle count, each reading its QP count from device memory
+    rp->sh.resize((size_t)S);
+    std::vector<ShapeDev> hdev((size_t)S);
+    for (int32_t k = 0; k < S; k++) {
+        Shape &s = rp->sh[(size_t)k];
+        RP_CK(make_shape(rp.get(), s, k, shape_cap(I, K, k)));
+        RP_CK(impc_lib::batch_set_active_device(s.batch, rp->solve + k));
+        hdev[(size_t)k] = s.dev;
+        rp->group.push_back(s.batch);
+    }
+    RP_CK(impc_copy_to_device(ctx, rp->d_sh, hdev.data(), (int64_t)(sizeof(ShapeDev) * hdev.size())));
+    {  // the row scan's counters: (2 S + 3) x (lanes + wave totals) int32 of LDS
+        const size_t lds = sizeof(int32_t) * (size_t)(2 * S + 3) * (kPlanLanes + kPlanLanes / 64);
+        if (lds > 64 * 1024 &&
+            hipFuncSetAttribute((const void *)k_plan_rows, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+                hipSuccess) {
+            cleanup();
+            return fail(IMPC_DEVICE_ERROR, "replan: LDS of the row scan");
+        }
+    }
 #undef RP_CK
     rc = impc_replan_set_state(rp.get(), nullptr, nullptr);
     if (rc) {
@@ -428,7 +674,6 @@ int impc_replan_destroy(impc_replan rp) {
     (void)hipSetDevice(impc_lib::device(rp->ctx));
     (void)impc_ctx_synchronize(rp->ctx);
     for (Shape &s : rp->sh) free_shape(s);
-    if (rp->h_counts) (void)hipHostFree(rp->h_counts);
     rp->mem.release();
     delete rp;
     return IMPC_OK;
@@ -465,145 +710,85 @@ int impc_replan_run(impc_replan rp, const impc_replan_inputs *in) {
     RP_HIP(hipSetDevice(impc_lib::device(ctx)));
     hipStream_t st = impc_lib::stream(ctx);
     RP_TRY(impc_lib::order_after_all(ctx));
-    const int64_t I = rp->I, n = rp->n, N = rp->N, K = rp->K, L = rp->L;
+    const int64_t I = rp->I, n = rp->n;
+    const int32_t N = rp->N, K = rp->K, L = rp->L, S = rp->S;
 
-    // ---- branch table (:593-606); the three counts come back to the host
-    hipLaunchKernelGGL(k_branch_table, dim3(1), dim3(kTableLanes), 0, st, I, rp->first_time, in->has_pred,
-                       in->cur_count, in->cur_size ? 1 : 0, rp->branch, rp->inst_f, rp->inst_0, rp->ws_0, rp->inst_1,
-                       rp->d_counts, rp->best, rp->ob, rp->ctype, rp->cslot);
+    // ---- the branch and the rows of every instance (:593-606)
+    PlanArgs pa{I, K, S, Decide{rp->first_time, in->has_pred, in->num_pred, in->cur_count, K, in->cur_size ? 1 : 0},
+                rp->branch, rp->num_obs, rp->slot_row, rp->best, rp->row_inst, rp->row_code, rp->cnt, rp->clk};
+    const size_t lds = sizeof(int32_t) * (size_t)(2 * S + 3) * (kPlanLanes + kPlanLanes / 64);
+    hipLaunchKernelGGL(k_plan_rows, dim3(1), dim3(kPlanLanes), lds, st, pa);
     RP_HIP(hipGetLastError());
-    RP_HIP(hipMemcpyAsync(rp->h_counts, rp->d_counts, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    RP_HIP(hipStreamSynchronize(st));
-    const int64_t nf = rp->h_counts[0], n0 = rp->h_counts[1], n1 = rp->h_counts[2];
-    Shape &S = rp->sh[0], &P = rp->sh[1], &F0 = rp->sh[2];
-    if (n1 && !rp->sh[3].batch) RP_TRY(make_shape(rp, rp->sh[3], (int32_t)K, (int32_t)N, 1, I, true));
-    Shape &C1 = rp->sh[3];
-
-    // ---- fan-out branch: its instances' inputs compacted, the six candidates, the assembly
-    if (nf) {
-        const int64_t *idx = rp->inst_f;
-        RP_TRY(impc_gather_rows_device(ctx, in->pos, 24, idx, nf, rp->f_pos, nullptr));
-        RP_TRY(impc_gather_rows_device(ctx, in->vel, 24, idx, nf, rp->f_vel, nullptr));
-        RP_TRY(impc_gather_rows_device(ctx, in->xref, 64 * N, idx, nf, rp->f_xref, nullptr));
-        RP_TRY(impc_gather_rows_device(ctx, rp->plan_states, 64 * N, idx, nf, rp->f_lin, nullptr));
-        RP_TRY(impc_gather_rows_device(ctx, rp->prev_count, 4, idx, nf, rp->f_pc, nullptr));
-        RP_TRY(impc_gather_rows_device(ctx, in->dyn_cur, 24 * K, idx, nf, rp->f_dcur, nullptr));
-        RP_TRY(impc_gather_rows_device(ctx, in->pred_pos, 8 * K * 4 * L * 3, idx, nf, rp->f_ppos, nullptr));
-        RP_TRY(impc_gather_rows_device(ctx, in->pred_size, 8 * K * 4 * L * 3, idx, nf, rp->f_psize, nullptr));
-        RP_TRY(impc_gather_rows_device(ctx, in->prob, 32 * K, idx, nf, rp->f_prob, nullptr));
-        // fan-out instances are never on their first plan (the branch's condition)
-        RP_TRY(impc_intent_fanout_device(ctx, nf, (int32_t)K, (int32_t)L, (int32_t)N, rp->f_pos, rp->zeros8, rp->f_lin,
-                                         rp->f_pc, rp->f_dcur, rp->f_ppos, rp->f_psize, rp->f_prob, rp->f_ob,
-                                         rp->f_ctype, rp->f_cslot, rp->f_cprob, rp->s_pos, rp->s_size, rp->p_pos,
-                                         rp->p_size, nullptr));
-        for (Shape *s : {&S, &P}) {
-            RP_TRY(impc_repeat_rows_device(ctx, rp->f_pos, nf, 24, s->rep, s->pos, nullptr));
-            RP_TRY(impc_repeat_rows_device(ctx, rp->f_vel, nf, 24, s->rep, s->vel, nullptr));
-            RP_TRY(impc_repeat_rows_device(ctx, rp->f_xref, nf, 64 * N, s->rep, s->xref, nullptr));
-            RP_TRY(impc_repeat_rows_device(ctx, rp->f_lin, nf, 64 * N, s->rep, s->lin, nullptr));
-            s->inst = rp->inst_f;
-        }
-        RP_TRY(assemble(rp, S, nf, S.lin, rp->s_pos, rp->s_size, idx, rp->f_ws));
-        RP_TRY(assemble(rp, P, nf, P.lin, rp->p_pos, rp->p_size, idx, rp->f_ws));
-    } else {
-        S.count = P.count = S.ninst = P.ninst = 0;
+    // ---- the fan-out's closest obstacle and candidate order
+    PickArgs pk{I, K, N, rp->branch, rp->num_obs, in->pos, rp->plan_states, in->dyn_cur, in->prob, rp->prev_count,
+                rp->ob, rp->ctype, rp->cslot, rp->slot_type, rp->cprob};
+    hipLaunchKernelGGL(k_pick, dim3((unsigned)((I + 63) / 64)), dim3(64), 0, st, pk);
+    RP_HIP(hipGetLastError());
+    // ---- warm starts, time limits, obstacle sources; the assembly of every shape in place
+    // (timeLimit = max(solverTimeLimit_ - t, solverTimeLimit_) = solverTimeLimit_ for t >= 0, :614)
+    const double tl = in->solver_time_limit > 0.0 ? in->solver_time_limit : rp->cfg.settings.time_limit;
+    PrepArgs pp{I, n, rp->rows, K, L, S, rp->cnt, rp->d_sh, rp->row_inst, rp->ob, rp->slot_type, rp->row_code,
+                rp->first_time, rp->plan_x, in->prob, tl};
+    hipLaunchKernelGGL(k_prep, dim3(grid_for(rp, rp->rows, 1)), dim3(64), 0, st, pp);
+    RP_HIP(hipGetLastError());
+    for (int32_t k = 0; k < S; k++) {
+        Shape &s = rp->sh[(size_t)k];
+        impc_lib::BatchInputs bi{};
+        RP_TRY(impc_lib::batch_inputs_begin(s.batch, &bi));
+        RP_TRY(impc_lib::build_rows(s.bld, s.cap, rp->cnt + S + k, rp->row_inst + shape_base(I, k), s.dev.osrc,
+                                    in->pos, in->vel, in->xref, rp->plan_states, in->pred_pos, in->pred_size,
+                                    in->dyn_cur, in->cur_size, bi, st));
+        RP_TRY(impc_lib::batch_inputs_end(s.batch, true));
     }
-    // ---- single solve, first plan / no obstacles: no linearisation point (no obstacle rows)
-    F0.inst = rp->inst_0;
-    if (n0) {
-        RP_TRY(impc_gather_rows_device(ctx, in->pos, 24, rp->inst_0, n0, F0.pos, nullptr));
-        RP_TRY(impc_gather_rows_device(ctx, in->vel, 24, rp->inst_0, n0, F0.vel, nullptr));
-        RP_TRY(impc_gather_rows_device(ctx, in->xref, 64 * N, rp->inst_0, n0, F0.xref, nullptr));
-    }
-    RP_TRY(assemble(rp, F0, n0, nullptr, nullptr, nullptr, rp->ws_0, nullptr));
-    // ---- single solve with the current obstacles held over the horizon
-    if (n1) {
-        C1.inst = rp->inst_1;
-        RP_TRY(impc_gather_rows_device(ctx, in->pos, 24, rp->inst_1, n1, C1.pos, nullptr));
-        RP_TRY(impc_gather_rows_device(ctx, in->vel, 24, rp->inst_1, n1, C1.vel, nullptr));
-        RP_TRY(impc_gather_rows_device(ctx, in->xref, 64 * N, rp->inst_1, n1, C1.xref, nullptr));
-        RP_TRY(impc_gather_rows_device(ctx, rp->plan_states, 64 * N, rp->inst_1, n1, C1.lin, nullptr));
-        const int64_t hw = n1 * K * N * 3;
-        hipLaunchKernelGGL(k_hold, dim3(grid_for(rp, hw)), dim3(256), 0, st, in->dyn_cur, rp->inst_1, n1, (int32_t)K,
-                           (int32_t)N, C1.dpos);
-        hipLaunchKernelGGL(k_hold, dim3(grid_for(rp, hw)), dim3(256), 0, st, in->cur_size, rp->inst_1, n1, (int32_t)K,
-                           (int32_t)N, C1.dsize);
-        RP_HIP(hipGetLastError());
-        RP_TRY(assemble(rp, C1, n1, C1.lin, C1.dpos, C1.dsize, rp->inst_1, nullptr));
-    } else if (C1.batch) {
-        C1.count = C1.ninst = 0;
-    }
-
-    // ---- the issue cut-off (:613) after the assembly; the candidates' time limit (:614)
-    RP_HIP(hipStreamSynchronize(st));
-    const auto t_staged = clk::now();
-    const double elapsed = in->elapsed_s + std::chrono::duration<double>(t_staged - t_entry).count();
-    const bool issued = !(rp->cfg.issue_cutoff_s > 0.0) || elapsed < rp->cfg.issue_cutoff_s;
-    double tl = rp->cfg.settings.time_limit;
-    if (in->solver_time_limit > 0.0) tl = std::max(in->solver_time_limit - elapsed, in->solver_time_limit);
-    std::vector<impc_batch> launch;
-    for (Shape *s : {&S, &P})
-        if (s->count && issued) {
-            RP_TRY(set_limit(rp, *s, tl));
-            launch.push_back(s->batch);
-        }
-    for (Shape *s : {&F0, &C1})  // solveTraj's default (none on a first plan, :442-444)
-        if (s->batch && s->count) {
-            RP_TRY(set_limit(rp, *s, 0.0));
-            launch.push_back(s->batch);
-        }
-    if (!issued) S.count = P.count = 0;  // nothing of the fan-out ran (impc_replan_shape)
-    if (!launch.empty()) RP_TRY(impc_batch_solve_group(launch.data(), (int)launch.size(), nullptr));
-
+    // ---- the issue cut-off on the device clock; ONE grouped solve over every shape
+    hipLaunchKernelGGL(k_issue, dim3(1), dim3(64), 0, st, S, rp->cnt, rp->solve, rp->clk, rp->issued, in->elapsed_s,
+                       impc_lib::tick_s(ctx), rp->cfg.issue_cutoff_s);
+    RP_HIP(hipGetLastError());
+    RP_TRY(impc_batch_solve_group(rp->group.data(), (int)rp->group.size(), nullptr));
     // ---- candidate validity, selection, commit
-    if (nf) {
-        impc_info *info_s = nullptr, *info_p = nullptr;
-        double *x_s = nullptr, *x_p = nullptr;
-        RP_TRY(impc_batch_device_results(S.batch, &x_s, nullptr, &info_s));
-        RP_TRY(impc_batch_device_results(P.batch, &x_p, nullptr, &info_p));
-        hipLaunchKernelGGL(k_cand_valid, dim3(grid_for(rp, 6 * nf)), dim3(256), 0, st, nf, rp->f_cslot, info_s, info_p,
-                           issued ? 1 : 0, rp->cvalid);
-        RP_HIP(hipGetLastError());
-        RP_TRY(impc_fanout_candidates_device(ctx, nf, (int32_t)K, (int32_t)L, rp->f_cslot, rp->s_pos, rp->s_size,
-                                             rp->p_pos, rp->p_size, x_s, S.dm.n, x_p, P.dm.n, rp->x_cand,
-                                             rp->dyn_count, rp->dyn_pos, rp->dyn_size, nullptr));
-        impc_select_params sp{};
-        sp.horizon = (int32_t)N, sp.num_candidates = 6, sp.max_dynamic = (int32_t)K + 1, sp.pred_len = (int32_t)L;
-        sp.num_static = 0, sp.prev_len = (int32_t)N;
-        sp.dynamic_safety_dist = rp->cfg.mpc.dynamic_safety_dist;
-        sp.static_safety_dist = rp->cfg.mpc.static_safety_dist;
-        RP_TRY(impc_select_best_device(ctx, &sp, nf, rp->x_cand, rp->cvalid, rp->zeros8, rp->f_lin, rp->f_pc,
-                                       rp->f_xref, nullptr, nullptr, rp->dyn_count, rp->dyn_pos, rp->dyn_size,
-                                       rp->f_cprob, rp->best_f, rp->best_pos, rp->scores, rp->weighted, nullptr));
-        RP_TRY(impc_replan_commit_device(ctx, (int32_t)N, n, nf, rp->inst_f, (const uint64_t *)rp->x_cand, 6,
-                                         rp->best_f, nullptr, nullptr, rp->plan_x, rp->plan_states, rp->prev_count,
-                                         rp->first_time, rp->valid, nullptr));
-        hipLaunchKernelGGL(k_scatter, dim3(grid_for(rp, nf)), dim3(256), 0, st, nf, rp->inst_f, rp->best_f, rp->f_ob,
-                           rp->f_ctype, rp->f_cslot, rp->best, rp->ob, rp->ctype, rp->cslot);
-        RP_HIP(hipGetLastError());
-    }
-    for (Shape *s : {&F0, &C1}) {
-        if (!s->batch || !s->count) continue;
-        double *x = nullptr;
-        impc_info *info = nullptr;
-        RP_TRY(impc_batch_device_results(s->batch, &x, nullptr, &info));
-        RP_TRY(impc_replan_commit_device(ctx, (int32_t)N, n, s->count, s->inst, nullptr, 0, nullptr, x, info,
-                                         rp->plan_x, rp->plan_states, rp->prev_count, rp->first_time, rp->valid,
-                                         nullptr));
-    }
-    const auto t_end = clk::now();
-    impc_replan_stats &o = rp->stats;
-    o.fanout = nf, o.single_first = n0, o.single_current = n1;
-    o.issued = issued ? 1 : 0;
-    o.time_limit = tl;
-    o.stage_s = std::chrono::duration<double>(t_staged - t_entry).count();
-    o.total_s = std::chrono::duration<double>(t_end - t_entry).count();
+    CandArgs ca{I, n, K, L, rp->d_sh, rp->branch, rp->num_obs, rp->slot_row, rp->cslot, rp->slot_type, rp->ob,
+                rp->issued, in->pred_pos, in->pred_size, in->prob, rp->x_cand, rp->dyn_count, rp->cvalid, rp->dyn_pos,
+                rp->dyn_size};
+    hipLaunchKernelGGL(k_cand, dim3(grid_for(rp, 6 * I)), dim3(256), 0, st, ca);
+    hipLaunchKernelGGL(k_sel_sets, dim3(grid_for(rp, I * 6 * (K + 1) * L)), dim3(256), 0, st, ca);
+    RP_HIP(hipGetLastError());
+    impc_select_params sp{};
+    sp.horizon = N, sp.num_candidates = 6, sp.max_dynamic = K + 1, sp.pred_len = L;
+    sp.num_static = 0, sp.prev_len = N;
+    sp.dynamic_safety_dist = rp->cfg.mpc.dynamic_safety_dist;
+    sp.static_safety_dist = rp->cfg.mpc.static_safety_dist;
+    RP_TRY(impc_select_best_device(ctx, &sp, I, rp->x_cand, rp->cvalid, rp->zeros8, rp->plan_states, rp->prev_count,
+                                   in->xref, nullptr, nullptr, rp->dyn_count, rp->dyn_pos, rp->dyn_size, rp->cprob,
+                                   rp->best, rp->best_pos, rp->scores, rp->weighted, nullptr));
+    CommitArgs cm{I, n, N, rp->d_sh, rp->branch, rp->num_obs, rp->slot_row, rp->best, rp->x_cand, rp->plan_x,
+                  rp->plan_states, rp->prev_count, rp->first_time, rp->valid};
+    hipLaunchKernelGGL(k_commit, dim3(grid_for(rp, I, 1)), dim3(64), 0, st, cm);
+    RP_HIP(hipGetLastError());
+    rp->ran = true;
+    rp->last_limit = tl;
+    rp->last_total_s = std::chrono::duration<double>(clk::now() - t_entry).count();
     return IMPC_OK;
 }
 
 int impc_replan_get_stats(impc_replan rp, impc_replan_stats *out) {
     if (!rp || !out) return fail(IMPC_INVALID_ARGUMENT, "replan: null object or output");
-    *out = rp->stats;
+    std::memset(out, 0, sizeof(*out));
+    if (!rp->ran) return IMPC_OK;
+    RP_TRY(impc_ctx_synchronize(rp->ctx));
+    const int32_t S = rp->S;
+    std::vector<int64_t> c((size_t)(2 * S + 3));
+    unsigned long long ck[2];
+    int32_t iss = 0;
+    RP_TRY(impc_copy_to_host(rp->ctx, c.data(), rp->cnt, (int64_t)(sizeof(int64_t) * c.size())));
+    RP_TRY(impc_copy_to_host(rp->ctx, ck, rp->clk, (int64_t)sizeof(ck)));
+    RP_TRY(impc_copy_to_host(rp->ctx, &iss, rp->issued, (int64_t)sizeof(iss)));
+    out->fanout = c[(size_t)(2 * S + IMPC_REPLAN_FANOUT)];
+    out->single_first = c[(size_t)(2 * S + IMPC_REPLAN_SINGLE_FIRST)];
+    out->single_current = c[(size_t)(2 * S + IMPC_REPLAN_SINGLE_CURRENT)];
+    out->issued = iss;
+    out->time_limit = rp->last_limit;
+    out->stage_s = (double)(ck[1] - ck[0]) * impc_lib::tick_s(rp->ctx);
+    out->total_s = rp->last_total_s;
     return IMPC_OK;
 }
 
@@ -612,20 +797,28 @@ int impc_replan_view_device(impc_replan rp, impc_replan_view *out) {
     out->plan_x = rp->plan_x, out->plan_states = rp->plan_states, out->prev_count = rp->prev_count;
     out->first_time = rp->first_time, out->valid = rp->valid, out->branch = rp->branch;
     out->best_cand = rp->best, out->ob_idx = rp->ob, out->cand_type = rp->ctype, out->cand_slot = rp->cslot;
+    out->num_obs = rp->num_obs, out->slot_row = rp->slot_row;
     return IMPC_OK;
 }
 
-int impc_replan_shape(impc_replan rp, int32_t shape, impc_batch *batch, int64_t *count, const int64_t **inst,
-                      const double **Px, const double **q, const double **Ax, const double **l, const double **u) {
-    if (!rp || shape < 0 || shape > 3) return fail(IMPC_INVALID_ARGUMENT, "replan: shape must be 0..3");
-    const Shape &s = rp->sh[shape];
-    if (batch) *batch = s.batch;
-    if (count) *count = s.batch ? s.count : 0;
-    if (inst) *inst = s.inst;
-    impc_lib::BatchInputs bi{};
-    if (s.batch) {
-        RP_TRY(impc_lib::batch_inputs_view(s.batch, &bi));  // the inputs of the last assembly
+int impc_replan_shape(impc_replan rp, int32_t obstacles, impc_batch *batch, int64_t *count, const int32_t **row_inst,
+                      const int8_t **row_code, const double **Px, const double **q, const double **Ax,
+                      const double **l, const double **u) {
+    if (!rp || obstacles < 0 || obstacles >= rp->S)
+        return fail(IMPC_INVALID_ARGUMENT, "replan: shape (obstacle count) must be in 0 .. num_obstacles + 1");
+    const Shape &s = rp->sh[(size_t)obstacles];
+    int64_t c = 0;
+    if (rp->ran) {
+        RP_TRY(impc_ctx_synchronize(rp->ctx));
+        RP_TRY(impc_copy_to_host(rp->ctx, &c, rp->solve + obstacles, (int64_t)sizeof(c)));
     }
+    if (batch) *batch = s.batch;
+    if (count) *count = c;
+    const int64_t base = shape_base(rp->I, obstacles);
+    if (row_inst) *row_inst = rp->row_inst + base;
+    if (row_code) *row_code = rp->row_code + base;
+    impc_lib::BatchInputs bi{};
+    RP_TRY(impc_lib::batch_inputs_view(s.batch, &bi));  // the inputs of the last assembly
     if (Px) *Px = bi.Px;
     if (q) *q = bi.q;
     if (Ax) *Ax = bi.Ax;

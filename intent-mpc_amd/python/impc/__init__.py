@@ -136,6 +136,7 @@ _sig("impc_batch_set_profiling", C.c_int, _P, C.c_int)
 _sig("impc_batch_get_timings", C.c_int, _P, _dp, _dp, _dp)
 _sig("impc_batch_get_qp_latency", C.c_int, _P, _dp)
 _sig("impc_batch_set_persistent", C.c_int, _P, C.c_int)
+_sig("impc_batch_get_persistent", C.c_int, _P, _dp, _dp, _dp, _dp)
 _sig("impc_batch_set_kernel", C.c_int, _P, C.c_int)
 _sig("impc_batch_solve_group", C.c_int, C.POINTER(_P), C.c_int, _P)
 _sig("impc_device_alloc", C.c_int, _P, C.c_int64, C.POINTER(_P))
@@ -263,6 +264,7 @@ EXPORTED = [
     "impc_replan_create", "impc_replan_destroy", "impc_replan_set_state", "impc_replan_run", "impc_replan_get_stats",
     "impc_replan_view_device", "impc_replan_shape", "impc_replan_advance_device", "impc_batch_follow_plan_device",
     "impc_copy_rows_device", "impc_batch_update_matrices", "impc_batch_update_matrices_device",
+    "impc_batch_get_persistent",
 ]
 
 
@@ -442,6 +444,14 @@ class Batch:
 
     def set_persistent(self, on=True):
         _check(lib.impc_batch_set_persistent(self.h, int(on)), "impc_batch_set_persistent")
+
+    def get_persistent(self):
+        """impc_batch_get_persistent: (rho [B], x [B][n], z [B][m], y [B][m]) of the persistent
+        workspaces -- the SCALED iterates OSQP keeps between solves, in OSQP's variable / row order."""
+        rho, x = np.empty(self.B), np.empty((self.B, self.n))
+        z, y = np.empty((self.B, self.m)), np.empty((self.B, self.m))
+        _check(lib.impc_batch_get_persistent(self.h, _d(rho), _d(x), _d(z), _d(y)), "impc_batch_get_persistent")
+        return rho, x, z, y
 
     def qp_latency(self):
         """Per-QP device solve latency (ms) of the last profiled structured solve."""

@@ -139,6 +139,26 @@ def gather_costs(dist, local, counts):
     return unpad(np.concatenate([o.numpy() for o in out]), counts)
 
 
+REPLAN_FIELDS = ("rank", "inst", "branch", "best_cand", "valid", "plan_sum", "plan_x0", "plan_y0", "plan_z0")
+
+
+def replan_records(rank, inst, branch, best_cand, valid, plan_x):
+    """[I_local, 9] float64 per-instance records of one rank's replan (REPLAN_FIELDS order): the
+    makePlanWithPred branch, the selected candidate, validTraj, and the committed plan (its sum and
+    its first state's position) -- what the multi-GPU replan returns to every rank (the hypothesis
+    selection is local to an instance, so this is the only exchange)."""
+    px = np.asarray(plan_x, np.float64)
+    rec = np.zeros((len(inst), len(REPLAN_FIELDS)))
+    rec[:, 0] = rank
+    rec[:, 1] = inst
+    rec[:, 2] = branch
+    rec[:, 3] = best_cand
+    rec[:, 4] = valid
+    rec[:, 5] = px.sum(axis=1)
+    rec[:, 6:9] = px[:, 0:3]
+    return rec
+
+
 def gather_records(dist, rec):
     """All-gather of every rank's records (equal counts per rank: weak scaling)."""
     if dist is None:

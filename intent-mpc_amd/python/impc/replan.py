@@ -19,26 +19,34 @@ An instance without a plan keeps its state (validTraj = false).
 
 The replan's wall-clock budget (:609-628): candidate i is issued only while `time = now -
 startTime < 0.15 s`, with `timeLimit = max(solverTimeLimit_ - time, solverTimeLimit_)`; a
-candidate enters the selection only when solveTraj succeeded (every OSQP status but NON_CVX,
-:513-518).  The batch issues all six candidates of every fan-out instance at one instant (after
+candidate enters the selection only when solveTraj succeeded (initSolver and solveProblem NoError,
+:475-478, :513-518 -- solve_traj_ok).  The batch issues all six candidates of every fan-out instance at one instant (after
 the device-side assembly), so the cut-off is one check: past it no candidate is issued and every
 fan-out instance selects nothing (best_cand -1, validTraj = false).
 
+Every instance may track its own number of obstacles, K_i = num_pred[i] (0..K; predPos.size(),
+updatePredObstacles :343-373).  The QPs of a replan are grouped by obstacle count: shape k holds
+every QP with k obstacle rows per stage (first plans k = 0, current-obstacle solves k = c_i,
+single-intent candidates K_i, two-intent candidates K_i + 1), one solver batch per shape, all in
+one grouped launch whose per-shape QP counts the device decides and the solver reads from device
+memory -- the library call never waits for the device and reads nothing back.
+
 Everything here beyond impc_replan_run / impc_replan_set_state (input uploads, the per-shape
-results and assembled values of run()'s return dict) is test plumbing: the library call itself
-reads back only the three branch counts.
+results and assembled values of run()'s return dict) is test plumbing.
 """
 import ctypes as C
 import time
 
 import numpy as np
 
-from . import (INFO_DTYPE, NON_CVX, DeviceArray, MpcParams, ReferencePaths, Settings, _check, _P, lib,
+from . import (INFO_DTYPE, DeviceArray, MpcParams, ReferencePaths, Settings, _check, _P, lib,
                QUEUE_FIFO)
 
 ISSUE_CUTOFF_S = 0.15  # makePlanWithPred: no candidate is issued 0.15 s after the replan started (:613)
 FANOUT, SINGLE_FIRST, SINGLE_CURRENT = 0, 1, 2  # IMPC_REPLAN_* (run()["branch"])
-SHAPES = ("single", "pair", "first", "current")  # impc_replan_shape 0..3
+ROW_FIRST, ROW_CURRENT = 6, 7  # impc_replan_shape row codes (0..3 single-intent slot, 4..5 two-intent slot)
+CATEGORIES = ("single", "pair", "first", "current")  # the per-kind views of results()
+UNSOLVED = -10
 
 
 class ReplanConfig(C.Structure):
@@ -52,7 +60,7 @@ class ReplanInputs(C.Structure):
     """impc_replan_inputs: device pointers + the budget."""
     _fields_ = [(k, C.c_void_p) for k in ("pos", "vel", "xref", "dyn_cur", "pred_pos", "pred_size", "prob", "has_pred",
                                           "cur_size", "cur_count")] + \
-               [("solver_time_limit", C.c_double), ("elapsed_s", C.c_double)]
+               [("solver_time_limit", C.c_double), ("elapsed_s", C.c_double), ("num_pred", C.c_void_p)]
 
 
 class ReplanStats(C.Structure):
@@ -63,7 +71,7 @@ class ReplanStats(C.Structure):
 
 class ReplanView(C.Structure):
     _fields_ = [(k, C.c_void_p) for k in ("plan_x", "plan_states", "prev_count", "first_time", "valid", "branch",
-                                          "best_cand", "ob_idx", "cand_type", "cand_slot")]
+                                          "best_cand", "ob_idx", "cand_type", "cand_slot", "num_obs", "slot_row")]
 
 
 def _sig(name, *args):
@@ -80,19 +88,66 @@ _sig("impc_replan_get_stats", _P, C.POINTER(ReplanStats))
 _sig("impc_replan_view_device", _P, C.POINTER(ReplanView))
 _sig("impc_replan_advance_device", _P, C.c_double, _P, _P)
 _sig("impc_replan_shape", _P, C.c_int32, C.POINTER(_P), C.POINTER(C.c_int64), C.POINTER(_P), C.POINTER(_P),
-     C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), C.POINTER(_P))
+     C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), C.POINTER(_P))
 
 
-def candidate_valid(cand_slot, status_single, status_pair):
-    """valid[i][c] of the selection (host restatement of the library's k_cand_valid): candidate c
-    of fan-out instance i was solved without an OSQP error (solveTraj's successSolve,
-    mpcPlanner.cpp:513-518 -- every status but OSQP_NON_CVX).  Candidate c sits at row 4i+slot of
-    the single-intent batch (slot < 4) or 2i+slot-4 of the two-intent batch."""
+def solve_traj_ok(info):
+    """solveTraj's successSolve per solved QP (host restatement of impc_lib::solve_traj_ok,
+    mpcPlanner.cpp:475-478, :513-518): initSolver succeeded (setup_exitflag 0) and solveProblem
+    returned NoError -- osqp_solve's exitflag, 0 for every final status (infeasible and a diverged
+    NON_CVX included, x = OSQP_NAN) and 1 only after a failed adaptive-rho refactorisation (status
+    left UNSOLVED)."""
+    info = np.asarray(info)
+    return (info["setup_exitflag"] == 0) & (info["status_val"] != UNSOLVED)
+
+
+def candidate_valid(cand_slot, info_single, info_pair):
+    """valid[i][c] of the selection (host restatement of the library's k_cand): candidate c of
+    fan-out instance i succeeded (solve_traj_ok).  Candidate c sits at row 4i+slot of the
+    single-intent rows (slot < 4) or 2i+slot-4 of the two-intent rows."""
     slot = np.asarray(cand_slot)
     ii = np.arange(slot.shape[0])[:, None]
-    ok_s = np.asarray(status_single) != NON_CVX
-    ok_p = np.asarray(status_pair) != NON_CVX
+    ok_s, ok_p = solve_traj_ok(info_single), solve_traj_ok(info_pair)
     return np.where(slot < 4, ok_s[4 * ii + np.minimum(slot, 3)], ok_p[2 * ii + np.clip(slot - 4, 0, 1)]).astype(np.int8)
+
+
+def assemble(per_inst, shapes):
+    """The per-kind views of one replan from its per-shape rows (shapes[k] = dict(x, y, info[, vals,
+    lat]) of the rows shape k solved) and the per-instance outputs (branch, num_obs, slot_row):
+    x_<kind>, y_<kind>, info_<kind>, vals_<kind>, lat_<kind> for the kinds single (the single-intent
+    candidates, row 4 j + slot of the j-th fan-out instance), pair (two-intent, 2 j + slot - 4),
+    first and current (row j of the j-th instance on that branch).  x and info are arrays; y and
+    vals are arrays when every row has the same m (one obstacle count), else per-row lists.  A kind
+    with no solved row is None.  Also cand_rows [I][6] = (shape, row) of candidate c (getIntentComb
+    order) and single_rows [I] = (shape, row)."""
+    br, K, R = per_inst["branch"], per_inst["num_obs"], per_inst["slot_row"]
+    I = br.shape[0]
+    out = {"inst_fanout": np.flatnonzero(br == FANOUT), "inst_first": np.flatnonzero(br == SINGLE_FIRST),
+           "inst_current": np.flatnonzero(br == SINGLE_CURRENT)}
+    rows = {"single": [(int(K[i]), int(R[i, s])) for i in out["inst_fanout"] for s in range(4)],
+            "pair": [(int(K[i]) + 1, int(R[i, s])) for i in out["inst_fanout"] for s in (4, 5)],
+            "first": [(int(K[i]), int(R[i, 0])) for i in out["inst_first"]],
+            "current": [(int(K[i]), int(R[i, 0])) for i in out["inst_current"]]}
+    for nm in CATEGORIES:
+        rr = rows[nm]
+        ok = bool(rr) and all(k in shapes and r < shapes[k]["x"].shape[0] for k, r in rr)
+        for key in ("x", "y", "info", "vals", "lat"):
+            if not ok or shapes[rr[0][0]].get(key) is None:
+                out[f"{key}_{nm}"] = None
+                continue
+            if key == "vals":
+                parts = [[v[r] for v in shapes[k]["vals"]] for k, r in rr]
+                same = len({k for k, _ in rr}) == 1
+                out[f"vals_{nm}"] = [np.stack([p[j] for p in parts]) for j in range(5)] if same else parts
+                continue
+            parts = [shapes[k][key][r] for k, r in rr]
+            same = key in ("x", "info", "lat") or len({k for k, _ in rr}) == 1
+            out[f"{key}_{nm}"] = np.stack(parts) if same else parts
+    slot = per_inst.get("cand_slot")
+    out["cand_rows"] = [[((int(K[i]) + (1 if slot[i, c] >= 4 else 0)), int(R[i, slot[i, c]])) for c in range(6)]
+                        if br[i] == FANOUT else None for i in range(I)] if slot is not None else None
+    out["single_rows"] = [(int(K[i]), int(R[i, 0])) if br[i] != FANOUT else None for i in range(I)]
+    return out
 
 
 def branches(first_time, has_pred, cur_count=None):
@@ -157,11 +212,12 @@ class DeviceReplan:
 
     # ---- one replan
     def run_device(self, pos, vel, xref, dyn_cur, pred_pos, pred_size, prob, has_pred=None, cur_size=None,
-                   cur_count=None, solver_time_limit=0.0, elapsed_s=0.0):
+                   cur_count=None, solver_time_limit=0.0, elapsed_s=0.0, num_pred=None):
         """impc_replan_run on device addresses (ints); the product call."""
         inp = ReplanInputs(pos=pos, vel=vel, xref=xref, dyn_cur=dyn_cur, pred_pos=pred_pos, pred_size=pred_size,
                            prob=prob, has_pred=has_pred, cur_size=cur_size, cur_count=cur_count,
-                           solver_time_limit=float(solver_time_limit or 0.0), elapsed_s=float(elapsed_s))
+                           solver_time_limit=float(solver_time_limit or 0.0), elapsed_s=float(elapsed_s),
+                           num_pred=num_pred)
         _check(lib.impc_replan_run(self.h, C.byref(inp)), "impc_replan_run")
 
     def advance_device(self, t, pos_ptr, vel_ptr):
@@ -175,32 +231,36 @@ class DeviceReplan:
         return {f: getattr(s, f) for f, _ in ReplanStats._fields_}
 
     def shape(self, k):
-        """impc_replan_shape k: (batch handle, QP count, instances [count'], device value pointers)."""
-        b, cnt, inst = _P(), C.c_int64(), _P()
+        """impc_replan_shape k (obstacle count 0 .. K + 1): (batch handle, QP count solved, row_inst
+        and row_code device pointers, device value pointers)."""
+        b, cnt, ri, rc = _P(), C.c_int64(), _P(), _P()
         ptrs = [_P() for _ in range(5)]
-        _check(lib.impc_replan_shape(self.h, k, C.byref(b), C.byref(cnt), C.byref(inst), *[C.byref(p) for p in ptrs]),
-               "impc_replan_shape")
-        return b.value, cnt.value, inst.value, [p.value for p in ptrs]
+        _check(lib.impc_replan_shape(self.h, k, C.byref(b), C.byref(cnt), C.byref(ri), C.byref(rc),
+                                     *[C.byref(p) for p in ptrs]), "impc_replan_shape")
+        return b.value, cnt.value, ri.value, rc.value, [p.value for p in ptrs]
 
-    def _shape_results(self, k, with_values):
-        """Host copies of shape k's last results (count rows) -- inspection for tests."""
-        b, cnt, inst, ptrs = self.shape(k)
+    def _shape_results(self, k, with_values, profile=False):
+        """Host copies of shape k's last results (its solved rows) -- inspection for tests."""
+        b, cnt, ri, rc, ptrs = self.shape(k)
         if not cnt:
             return None
-        rep = (4, 2, 1, 1)[k]
-        st = {}
-        for key in ("n", "m", "nnzP", "nnzA", "batch"):
-            st[key] = self._stats_of(b)[key]
+        st = self._stats_of(b)
         n, m = st["n"], st["m"]
         x = np.empty((st["batch"], n))
         y = np.empty((st["batch"], max(m, 1)))
         info = np.empty(st["batch"], INFO_DTYPE)
         _check(lib.impc_batch_get(_P(b), x.ctypes.data_as(C.POINTER(C.c_double)),
                                   y.ctypes.data_as(C.POINTER(C.c_double)), info.ctypes.data_as(_P)), "impc_batch_get")
-        out = dict(x=x[:cnt], y=y[:cnt, :m], info=info[:cnt], inst=_get(self.ctx, inst, cnt // rep, np.int64), batch=b)
+        out = dict(x=x[:cnt], y=y[:cnt, :m], info=info[:cnt], row_inst=_get(self.ctx, ri, cnt, np.int32),
+                   row_code=_get(self.ctx, rc, cnt, np.int8), batch=b)
         if with_values:
             out["vals"] = [_get(self.ctx, p, (cnt, ln), np.float64)
                            for p, ln in zip(ptrs, (st["nnzP"], n, st["nnzA"], m, m))]
+        if profile:
+            ms = np.empty(st["batch"])
+            _check(lib.impc_batch_get_qp_latency(_P(b), ms.ctypes.data_as(C.POINTER(C.c_double))),
+                   "impc_batch_get_qp_latency")
+            out["lat"] = ms[:cnt]
         return out
 
     @staticmethod
@@ -212,20 +272,20 @@ class DeviceReplan:
 
     def run(self, pos, vel, xref, prev=None, first_time=None, prev_count=None, dyn_cur=None, pred_pos=None,
             pred_size=None, prob=None, timings=None, solver_time_limit=None, t_start=None, profile=False,
-            has_pred=None, cur_size=None, cur_count=None, values=True):
+            has_pred=None, cur_size=None, cur_count=None, values=True, num_pred=None):
         """One makePlanWithPred over all instances from host arrays (uploaded here; test plumbing
         around impc_replan_run).  Inputs: pos, vel [I][3]; xref [I][N][8] or an
         impc.ReferencePaths (getXRef on the device, from `pos`); dyn_cur [I][K][3]; pred_pos /
-        pred_size [I][K][4][L][3], prob [I][K][4]; has_pred [I] (default all); cur_size [I][K][3] +
-        cur_count [I] (0 or K): the current dynamic obstacles a no-prediction instance keeps
-        (default none).  prev [I][N][8] / first_time [I]: when given, the planner state is set
+        pred_size [I][K][4][L][3], prob [I][K][4]; has_pred [I] (default all); num_pred [I] (K_i,
+        0..K: each instance's first K_i obstacle slots; default K); cur_size [I][K][3] + cur_count [I]
+        (0..K): the current dynamic obstacles a no-prediction instance keeps (default none).  prev [I][N][8] / first_time [I]: when given, the planner state is set
         from them first (impc_replan_set_state; prev_count is implied -- 0 on a first plan, N
         otherwise -- and checked when passed); else the replan continues from the committed state.
 
-        Returns dict(branch [I], valid [I], best_cand [I], cand_type, cand_slot, ob_idx [I],
-        inst_fanout / inst_first / inst_current, x_* / y_* / info_* / vals_* (lat_* with profile)
-        for the shapes single, pair, first, current (None when a shape did not run), xref,
-        issued, time_limit).  t_start: the replan's startTime (perf_counter seconds)."""
+        Returns dict(branch [I], valid [I], best_cand [I], cand_type, cand_slot, ob_idx [I], num_obs,
+        slot_row, inst_fanout / inst_first / inst_current, x_* / y_* / info_* / vals_* (lat_* with
+        profile) for the kinds single, pair, first, current (assemble(); None when a kind did not
+        run), shapes, cand_rows, single_rows, xref, issued, time_limit).  t_start: the replan's startTime (perf_counter seconds)."""
         I, K, L, N = self.I, self.K, self.L, self.N
         t0 = time.perf_counter()
         if t_start is None:
@@ -261,10 +321,11 @@ class DeviceReplan:
                     has_pred=None if has_pred is None else dev(np.asarray(has_pred).reshape(I), np.int8),
                     cur_size=None if cur_size is None else dev(np.asarray(cur_size).reshape(I, K, 3)),
                     cur_count=None if (cur_size is None or cur_count is None) else dev(np.asarray(cur_count).reshape(I),
-                                                                                      np.int32))
+                                                                                      np.int32),
+                    num_pred=None if num_pred is None else dev(np.asarray(num_pred).reshape(I), np.int32))
         self.ctx.synchronize()
         t_up = time.perf_counter() - t0
-        batches = [self.shape(k)[0] for k in range(4)]
+        batches = [self.shape(k)[0] for k in range(self.K + 2)]
         if profile:
             for b in batches:
                 if b:
@@ -277,7 +338,7 @@ class DeviceReplan:
         out = self.results(values, profile)
         out["xref"] = xd.get() if xd is not None else np.asarray(xref, np.float64).reshape(I, N, 8)
         if profile:
-            for b in [self.shape(k)[0] for k in range(4)]:
+            for b in batches:
                 if b:
                     _check(lib.impc_batch_set_profiling(_P(b), 0), "impc_batch_set_profiling")
         for d in tmp:
@@ -295,21 +356,15 @@ class DeviceReplan:
         out = dict(branch=_get(self.ctx, v.branch, I, np.int8), best_cand=_get(self.ctx, v.best_cand, I, np.int32),
                    ob_idx=_get(self.ctx, v.ob_idx, I, np.int32), cand_type=_get(self.ctx, v.cand_type, (I, 6), np.int32),
                    cand_slot=_get(self.ctx, v.cand_slot, (I, 6), np.int32), valid=_get(self.ctx, v.valid, I, np.int8),
+                   num_obs=_get(self.ctx, v.num_obs, I, np.int32), slot_row=_get(self.ctx, v.slot_row, (I, 6), np.int32),
                    issued=bool(st["issued"]), time_limit=st["time_limit"])
-        br = out["branch"]
-        out["inst_fanout"], out["inst_first"], out["inst_current"] = [np.flatnonzero(br == b) for b in
-                                                                      (FANOUT, SINGLE_FIRST, SINGLE_CURRENT)]
-        for k, nm in enumerate(SHAPES):
-            r = self._shape_results(k, values)
-            out["x_" + nm], out["y_" + nm], out["info_" + nm] = (r["x"], r["y"], r["info"]) if r else (None,) * 3
-            out["lat_" + nm] = None
-            if r and values:
-                out["vals_" + nm] = r["vals"]
-            if r and profile:
-                ms = np.empty(self._stats_of(r["batch"])["batch"])
-                _check(lib.impc_batch_get_qp_latency(_P(r["batch"]), ms.ctypes.data_as(C.POINTER(C.c_double))),
-                       "impc_batch_get_qp_latency")
-                out["lat_" + nm] = ms[: r["x"].shape[0]]
+        shapes = {}
+        for k in range(self.K + 2):
+            r = self._shape_results(k, values, profile)
+            if r:
+                shapes[k] = r
+        out["shapes"] = shapes
+        out.update(assemble(out, shapes))
         self.first_time_h = _get(self.ctx, v.first_time, I, np.int8)
         return out
 

@@ -1246,6 +1246,27 @@ void ora_get_iterates(const ora_ws *w, c_float *x, c_float *y) {
     for (c_int i = 0; i < w->m; i++) y[i] = w->scaled ? w->E[i] * w->y[i] * w->cinv : w->y[i];
 }
 
+/* Test-only state transfer (not an OSQP call): the workspace's SCALED iterates work->x, z, y and
+ * settings->rho (types.h:182-289).  ora_set_state loads another solver's persisted state -- the
+ * device's persistent workspace (impc_batch_get_persistent) -- into this workspace before the next
+ * update / solve, as osqp_update_rho (osqp.h:264) would set rho: rho_vec by constraint type and a
+ * refactorisation.  The closed-loop parity tests re-synchronise the oracle with it at every step,
+ * so each step is compared from the same starting point. */
+void ora_get_state(const ora_ws *w, c_float *rho, c_float *x, c_float *z, c_float *y) {
+    if (rho) *rho = w->st.rho;
+    if (x) memcpy(x, w->x, sizeof(c_float) * (size_t)w->n);
+    if (z) memcpy(z, w->z, sizeof(c_float) * (size_t)w->m);
+    if (y) memcpy(y, w->y, sizeof(c_float) * (size_t)w->m);
+}
+int ora_set_state(ora_ws *w, c_float rho, const c_float *x, const c_float *z, const c_float *y) {
+    if (!w) return OSQP_WORKSPACE_NOT_INIT_ERROR;
+    memcpy(w->x, x, sizeof(c_float) * (size_t)w->n);
+    memcpy(w->z, z, sizeof(c_float) * (size_t)w->m);
+    memcpy(w->y, y, sizeof(c_float) * (size_t)w->m);
+    if (rho != w->st.rho) return update_rho(w, rho) ? OSQP_NONCVX_ERROR : 0;
+    return 0;
+}
+
 /* The state osqp_setup leaves in the workspace (types.h:182-289): rho_vec, constr_type, the
  * scaling vectors D, E and the cost scale c -- compared in tests/test_oracle.py with the facts the
  * survey's probe read from the reference libosqp.so's OSQPWorkspace after osqp_setup (SURVEY.md

@@ -56,6 +56,10 @@ def lib():
         L.ora_update_P_A.argtypes = [C.c_void_p, dp, dp]
         L.ora_rescale_raw.argtypes = [C.c_void_p, dp, dp, dp, dp, dp]
         L.ora_cleanup.argtypes = [C.c_void_p]
+        L.ora_get_state.argtypes = [C.c_void_p, dp, dp, dp, dp]
+        L.ora_get_state.restype = None
+        L.ora_set_state.argtypes = [C.c_void_p, C.c_double, dp, dp, dp]
+        L.ora_set_state.restype = C.c_int
         L.ora_get_setup.argtypes = [C.c_void_p, dp, ip, dp, dp, dp]
         L.ora_cleanup.restype = None
         _lib = L
@@ -149,6 +153,21 @@ class Workspace:
         rc = lib().ora_rescale_raw(self.h, *[_d(v) for v in a])
         if rc:
             raise RuntimeError(f"ora_rescale_raw failed: {rc}")
+
+    def get_state(self):
+        """(rho, x, z, y): settings rho and the SCALED iterates the workspace holds (ora_get_state)."""
+        rho = C.c_double()
+        x, z, y = np.empty(self.n), np.empty(max(self.m, 1)), np.empty(max(self.m, 1))
+        lib().ora_get_state(self.h, C.byref(rho), _d(x), _d(z), _d(y))
+        return rho.value, x, z[: self.m], y[: self.m]
+
+    def set_state(self, rho, x, z, y):
+        """Load another solver's persisted (rho, scaled x, z, y) into this workspace (ora_set_state:
+        rho_vec by constraint type and a refactorisation when rho changes)."""
+        a = [np.ascontiguousarray(v, float) for v in (x, z, y)]
+        rc = lib().ora_set_state(self.h, float(rho), *[_d(v) for v in a])
+        if rc:
+            raise RuntimeError(f"ora_set_state failed: {rc}")
 
     def setup_state(self):
         """rho_vec, constr_type, D, E and c as osqp_setup left them (ora_get_setup)."""

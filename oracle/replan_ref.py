@@ -14,8 +14,10 @@ the horizon as updateDynamicObstacles / updatePredObstacles store them, :326-334
 when updatePredObstacles was handed no predictions, :364-371).
 solveTraj (:375-541): the time limit only when not firstTime_ (:442-444); warm start x = the
 previous plan when not firstTime_, else zeros, y = 0 (:485-509); linearisation point = the previous
-plan's states (currPos_ when there are none, :1042-1051); success = solveProblem NoError, i.e. any
-OSQP status but NON_CVX (:513-518).
+plan's states (currPos_ when there are none, :1042-1051); success = initSolver succeeded and
+solveProblem returned NoError (:475-478, :513-518): osqp_solve's exitflag, 0 for every final status
+(infeasible, max-iter, time limit and a NON_CVX from the residual test too, x = OSQP_NAN), 1 only
+when an adaptive-rho refactorisation fails (status left UNSOLVED) -- solve_traj_ok.
 """
 import numpy as np
 
@@ -24,6 +26,12 @@ from oracle import osqp_oracle as ora
 
 FANOUT, SINGLE_FIRST, SINGLE_CURRENT = 0, 1, 2
 NON_CVX = -7
+UNSOLVED = -10
+
+
+def solve_traj_ok(info):
+    """solveTraj's successSolve from one oracle solve's info record (module docstring)."""
+    return int(info["setup_exitflag"]) == 0 and int(info["status_val"]) != UNSOLVED
 
 
 def branch(first_time, has_pred, cur_count=0):
@@ -82,13 +90,14 @@ def single_qp(params, first_time, plan_x, pos, vel, xref, cur_pos=None, cur_size
     return pat, vals, warm_start(first_time, plan_x, pat["n"])
 
 
-def select(params, pd, first_time, plan_x, xref, fo, cand_x, cand_status, prob_closest):
+def select(params, pd, first_time, plan_x, xref, fo, cand_x, cand_ok, prob_closest):
     """getTrajectoryScore per successful candidate + evaluateTraj (:617-634) on the candidates'
-    solutions cand_x [6][n]: the chosen candidate index, or -1 when none succeeded."""
+    solutions cand_x [6][n] (cand_ok [6]: solve_traj_ok of each): the chosen candidate index, or -1
+    when none succeeded."""
     N = int(params["horizon"])
     prev = _states(plan_x, N)
     states = [[list(x[8 * k: 8 * k + 8]) for k in range(N)] for x in cand_x]
-    valid = [st != NON_CVX for st in cand_status]
+    valid = [bool(ok) for ok in cand_ok]
     best, _, _, _ = select_ref.select_instance(states, valid, prev, first_time, [list(r) for r in xref], [],
                                                [c[0] for c in fo["cands"]], [c[1] for c in fo["cands"]],
                                                prob_closest, pd["dynamic_safety_dist"], pd["static_safety_dist"])
@@ -112,14 +121,14 @@ def make_plan_with_pred(params, pd, settings, state, pos, vel, xref, dyn_cur, pr
     if br == FANOUT:
         fo, qps = fanout_qps(params, ft, px, pos, vel, xref, dyn_cur, pred_pos, pred_size, prob)
         sols = [solve(p, v, w, settings) for p, v, w in qps]
-        best = select(params, pd, ft, px, xref, fo, [s[0] for s in sols], [int(s[2]["status_val"]) for s in sols],
+        best = select(params, pd, ft, px, xref, fo, [s[0] for s in sols], [solve_traj_ok(s[2]) for s in sols],
                       prob[fo["ob_idx"]])
         out = dict(branch=br, valid=best >= 0, best=best, x=sols[best][0] if best >= 0 else None)
     else:
         p, v, w = single_qp(params, ft, px, pos, vel, xref, dyn_cur if br == SINGLE_CURRENT else None,
                             cur_size if br == SINGLE_CURRENT else None)
         x, _, info = solve(p, v, w, settings)
-        ok = int(info["status_val"]) != NON_CVX
+        ok = solve_traj_ok(info)
         out = dict(branch=br, valid=ok, best=-1, x=x if ok else None)
     if out["valid"]:  # currentStatesSol_ / currentControlsSol_ = the plan, firstTime_ = false
         state["plan_x"] = np.array(out["x"])

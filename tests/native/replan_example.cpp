@@ -15,9 +15,10 @@
 // program dumps (outside the timed call) the branch table, the selection, the committed state and
 // each shape's QPs and solutions.
 //   replan_example <inputs.bin> <outputs.bin>
-// inputs.bin: int32 I, K, L, N, R; impc_mpc_params; impc_settings; pos [I][3], vel [I][3],
+// inputs.bin: int32 I, K, L, N, R, P; impc_mpc_params; impc_settings; pos [I][3], vel [I][3],
 // xref [I][N][8], prev [I][N][8], first_time int8 [I], dyn/pred_pos [I][K][4][L][3], pred_size
-// [I][K][4][L][3], prob [I][K][4], cur_size [I][K][3], cur_count int32 [I], has_pred int8 [R][I].
+// [I][K][4][L][3], prob [I][K][4], cur_size [I][K][3], cur_count int32 [I], has_pred int8 [R][I],
+// and when P = 1 num_pred int32 [R][I] (each instance's obstacle count per replan).
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -81,18 +82,18 @@ int main(int argc, char **argv) {
     }
     FILE *f = std::fopen(argv[1], "rb");
     if (!f) return 2;
-    int32_t hdr[5];
+    int32_t hdr[6];
     impc_mpc_params mp{};
     impc_settings st{};
     bool ok = std::fread(hdr, sizeof hdr, 1, f) == 1 && std::fread(&mp, sizeof mp, 1, f) == 1 &&
               std::fread(&st, sizeof st, 1, f) == 1;
-    const int64_t I = hdr[0], K = hdr[1], L = hdr[2], N = hdr[3], R = hdr[4];
+    const int64_t I = hdr[0], K = hdr[1], L = hdr[2], N = hdr[3], R = hdr[4], P = hdr[5];
     std::vector<double> pos, vel, xref, prev, pred, psize, prob, csize;
     std::vector<int8_t> first, has_pred;
-    std::vector<int32_t> ccount;
+    std::vector<int32_t> ccount, npred;
     ok = ok && rd(f, pos, I * 3) && rd(f, vel, I * 3) && rd(f, xref, I * N * 8) && rd(f, prev, I * N * 8) &&
          rd(f, first, I) && rd(f, pred, I * K * 4 * L * 3) && rd(f, psize, I * K * 4 * L * 3) && rd(f, prob, I * K * 4) &&
-         rd(f, csize, I * K * 3) && rd(f, ccount, I) && rd(f, has_pred, R * I);
+         rd(f, csize, I * K * 3) && rd(f, ccount, I) && rd(f, has_pred, R * I) && (!P || rd(f, npred, R * I));
     std::fclose(f);
     if (!ok || mp.horizon != N) {
         std::fprintf(stderr, "short or inconsistent input file\n");
@@ -115,7 +116,7 @@ int main(int argc, char **argv) {
     for (int64_t i = 0; i < I; i++) std::memcpy(&plan[(size_t)(i * n)], &prev[(size_t)(i * N * 8)], 8 * 8 * N);
     CK(impc_replan_set_state(rp, plan.data(), first.data()));
 
-    Dev d_pos, d_vel, d_xref, d_dcur, d_pred, d_psize, d_prob, d_csize, d_ccount, d_hp;
+    Dev d_pos, d_vel, d_xref, d_dcur, d_pred, d_psize, d_prob, d_csize, d_ccount, d_hp, d_np;
     CK(d_pos.upload(ctx, pos));
     CK(d_vel.upload(ctx, vel));
     CK(d_xref.upload(ctx, xref));
@@ -135,11 +136,16 @@ int main(int argc, char **argv) {
         CK(d_pred.upload(ctx, pred));
         std::vector<int8_t> hp(has_pred.begin() + r * I, has_pred.begin() + (r + 1) * I);
         CK(d_hp.upload(ctx, hp));
+        if (P) {
+            std::vector<int32_t> np(npred.begin() + r * I, npred.begin() + (r + 1) * I);
+            CK(d_np.upload(ctx, np));
+        }
         impc_replan_inputs in{};
         in.pos = d_pos.as<double>(), in.vel = d_vel.as<double>(), in.xref = d_xref.as<double>();
         in.dyn_cur = d_dcur.as<double>(), in.pred_pos = d_pred.as<double>(), in.pred_size = d_psize.as<double>();
         in.prob = d_prob.as<double>(), in.has_pred = d_hp.as<int8_t>();
         in.cur_size = d_csize.as<double>(), in.cur_count = d_ccount.as<int32_t>();
+        in.num_pred = P ? d_np.as<int32_t>() : nullptr;
         in.solver_time_limit = 0.0;
         CK(impc_ctx_synchronize(ctx));
         const auto t0 = std::chrono::steady_clock::now();
@@ -159,14 +165,19 @@ int main(int argc, char **argv) {
         put<int8_t>(o, v.first_time, I, ctx);
         put<int32_t>(o, v.prev_count, I, ctx);
         put<int8_t>(o, v.valid, I, ctx);
-        for (int32_t s = 0; s < 4; s++) {
+        put<int32_t>(o, v.num_obs, I, ctx);
+        put<int32_t>(o, v.slot_row, 6 * I, ctx);
+        for (int32_t s = 0; s < (int32_t)K + 2; s++) {  // shape s: the QPs with s obstacle rows per stage
             impc_batch b = nullptr;
             int64_t cnt = 0;
-            const int64_t *inst = nullptr;
+            const int32_t *rinst = nullptr;
+            const int8_t *rcode = nullptr;
             const double *vals[5] = {};
-            CK(impc_replan_shape(rp, s, &b, &cnt, &inst, &vals[0], &vals[1], &vals[2], &vals[3], &vals[4]));
+            CK(impc_replan_shape(rp, s, &b, &cnt, &rinst, &rcode, &vals[0], &vals[1], &vals[2], &vals[3], &vals[4]));
             std::fwrite(&cnt, 8, 1, o);
             if (!cnt) continue;
+            put<int32_t>(o, rinst, cnt, ctx);
+            put<int8_t>(o, rcode, cnt, ctx);
             impc_batch_stats bs{};
             CK(impc_batch_get_stats(b, &bs));
             std::vector<double> x((size_t)(bs.batch * bs.n)), y((size_t)(bs.batch * bs.m));

@@ -358,3 +358,96 @@ def test_two_rank_config5_closed_loop_split_matches_whole_batch():
         for row in g0:
             np.testing.assert_array_equal(row[3:6], ref[(int(row[1]), int(row[2]))])
             assert row[0] == (0 if row[1] < 1 else 1)
+
+
+def _replan_chain(idx, steps=2, seed=6060):
+    """Chained makePlanWithPred replans of the instances `idx` of one fixed mixed-branch scenario on
+    the restatement (oracle/replan_ref.py): per replan the per-instance records (REPLAN_FIELDS
+    without the rank), x0 moving to each plan's next state and the predictions one step on."""
+    import impc
+    from impc import scenarios
+    from oracle import replan_ref as ref
+    I, K, N = 6, 3, 20
+    inst = next(iter(scenarios.intent_config(N=N, K=K, instances=I, hyps=6, seed=seed).values()))["instances"]
+    _, pd = impc.mpc_params(horizon=N)
+    s = impc.default_settings(verbose=0)
+    pred_size = np.broadcast_to(inst["size"], inst["pred"].shape).copy()
+    cur_size = np.broadcast_to(inst["size"], (I, K, 3)).copy()
+    ar = np.arange(I)
+    first = ar % 3 == 0
+    has_pred = [ar % 4 != 1, ar % 5 != 2]
+    cur_count = np.where(ar % 2 == 0, K, 0)
+    n = 13 * N - 5
+    recs = [[] for _ in range(steps)]
+    for i in idx:
+        st = dict(first_time=int(first[i]), plan_x=np.concatenate([inst["prev"][i].reshape(-1), np.zeros(n - 8 * N)]))
+        pos, vel, pred = inst["pos"][i].copy(), inst["vel"][i].copy(), inst["pred"][i].copy()
+        for t in range(steps):
+            o = ref.make_plan_with_pred(pd, pd, s, st, pos, vel, inst["xref"][i], pred[:, 0, 0, :], pred, pred_size[i],
+                                        inst["prob_all"][i], bool(has_pred[t][i]), cur_size[i], int(cur_count[i]))
+            px = st["plan_x"]
+            recs[t].append([i, o["branch"], o["best"], int(o["valid"]), px.sum(), px[0], px[1], px[2]])
+            if o["valid"]:
+                pos, vel = px[8:11].copy(), px[11:14].copy()
+            pred = np.concatenate([pred[:, :, 1:], pred[:, :, -1:]], axis=2)
+    return [np.array(r, np.float64).reshape(-1, 8) for r in recs]
+
+
+def _replan_worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(WORLD))
+    try:
+        import sys
+        here = os.path.dirname(os.path.abspath(__file__))
+        sys.path[:0] = [here, os.path.dirname(here)]
+        r, lr, w = D.env()
+        dist = D.init("gloo", lr)
+        # tools/live_loop.py --gpus N's rank path: the planning instances split in contiguous ranges,
+        # every rank replans its own (no exchange inside a replan: the selection is per instance),
+        # and each replan's per-instance records reach every rank
+        bounds = D.equal_instance_bounds(6, w)
+        mine = list(range(int(bounds[r]), int(bounds[r + 1])))
+        counts = [int(bounds[k + 1] - bounds[k]) for k in range(w)]
+        per_step = _replan_chain(mine)
+        gathered = []
+        for rec in per_step:
+            full = D.replan_records(r, rec[:, 0], rec[:, 1], rec[:, 2], rec[:, 3], np.zeros((rec.shape[0], 3)))
+            full[:, 5:9] = rec[:, 4:8]
+            gathered.append(D.gather_costs(dist, full, counts))
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((r, per_step, gathered, counts))
+    except Exception:  # surface the failure in the parent
+        import traceback
+        q.put((rank, traceback.format_exc(), None, None))
+
+
+def test_two_rank_replan_split_matches_whole_batch():
+    """The batched makePlanWithPred split over two gloo ranks by planning instance (the multi-GPU
+    replan / live loop): first plans, fan-outs and current-obstacle solves on both ranks over two
+    chained replans; every rank ends each replan with every instance's record, equal to the whole
+    batch replanned in one process."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_replan_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(WORLD):
+        r, per_step, gathered, counts = q.get(timeout=600)
+        assert gathered is not None, per_step
+        out[r] = (per_step, gathered, counts)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out[0][2] == [3, 3]
+    whole = _replan_chain(range(6))
+    branches = set()
+    for t in range(2):
+        g0, g1 = out[0][1][t], out[1][1][t]
+        np.testing.assert_array_equal(g0, g1)
+        np.testing.assert_array_equal(g0[:, 1:], whole[t])
+        np.testing.assert_array_equal(g0[:, 0], [0, 0, 0, 1, 1, 1])
+        branches.update(int(b) for b in g0[:, 2])
+    assert branches == {0, 1, 2}

@@ -94,8 +94,8 @@ def test_structured_emulation_long_horizon():
 
 def test_structured_emulation_live_horizon():
     """N=30 (n=385, the reference's live planner horizon, planner_param.yaml:25): the three-slot
-    shape's W = 29 instance, chunked recursions of 8 / 8 / 8 / 5 steps, with adaptive-rho
-    refactorisations."""
+    shape's W = 29 instance, chunked recursions of 6 / 6 / 6 / 6 / 5 steps (five chunks on four
+    wavefronts, IMPC_CHUNK5, the product form), with adaptive-rho refactorisations."""
     cfg = take(scenarios.intent_config(N=30, K=8, instances=1, seed=3030)[8], 1)
     s = impc.default_settings(**S25)
     compare(emulate(cfg, s), oracle(cfg, s))

@@ -204,3 +204,36 @@ def test_reachable_reference_needs_fewer_iterations():
                                      ora.settings_from(s), threads=4)
         it[step] = float(info["iter"].mean())
     assert it[0.3] <= 200 and it[2.5] >= 1.5 * it[0.3], it
+
+
+def test_set_state_reproduces_the_workspace_it_was_taken_from():
+    """ora_set_state (the closed-loop tests' re-synchronisation): a second workspace of the same QP
+    loaded with the first's rho and scaled iterates continues bitwise like the first through an
+    osqp_update_A + _lin_cost + _bounds + solve step; an unchanged rho leaves the factor alone."""
+    import impc
+    from impc import scenarios
+    cfg = scenarios.static_config(N=20, K=4, batch=1, identical=False, seed=531)
+    pat, v = cfg["pattern"], cfg["values"]
+    s = ora.settings_from(impc.default_settings(verbose=0, adaptive_rho_interval=25))
+    a = ora.Workspace(pat, v["Px"][0], v["q"][0], v["Ax"][0], v["l"][0], v["u"][0], s)
+    b = ora.Workspace(pat, v["Px"][0], v["q"][0], v["Ax"][0], v["l"][0], v["u"][0], s)
+    a.solve()
+    rho, x, z, y = a.get_state()
+    b.set_state(rho, x, z, y)
+    rb, xb, zb, yb = b.get_state()
+    assert rb == rho and np.array_equal(xb, x) and np.array_equal(zb, z) and np.array_equal(yb, y)
+    rng = np.random.default_rng(3)
+    A2 = v["Ax"][0] * (1 + 0.01 * rng.standard_normal(v["Ax"][0].shape))
+    q2 = v["q"][0] * 1.05
+    out = []
+    for w in (a, b):
+        w.update_matrices(None, A2)
+        w.update_lin_cost(q2)
+        w.update_bounds(v["l"][0], v["u"][0])
+        out.append(w.solve())
+    (xa, ya, ia), (xb2, yb2, ib) = out
+    assert ia["iter"] == ib["iter"] and ia["status_val"] == ib["status_val"]
+    np.testing.assert_array_equal(xa, xb2)
+    np.testing.assert_array_equal(ya, yb2)
+    a.close()
+    b.close()

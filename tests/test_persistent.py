@@ -123,14 +123,16 @@ def test_explicit_warm_start_between_updates(ctx, kernel):
         w.close()
 
 
-@pytest.mark.parametrize("which", ["P", "A", "PA", "A+q"])
-def test_matrix_update_matches_osqp_update_P_A(ctx, which):
+@pytest.mark.parametrize("N,which", [(20, "P"), (20, "A"), (20, "PA"), (20, "A+q"), (30, "A"), (30, "A+q"),
+                                     (40, "P"), (40, "A"), (40, "PA"), (40, "A+q")])
+def test_matrix_update_matches_osqp_update_P_A(ctx, N, which):
     """impc_batch_update_matrices on a persistent structured workspace against the oracle's
     osqp_update_P / _A / _P_A (ora_update_P_A: unscale_data, new values, scale_data, refactor, the
     scaled iterates kept): setup + solve -> update q -> solve -> new P and / or A -> solve -> update
     bounds -> solve (the replayed scaling is the new one).  Identical statuses and iteration counts,
-    primal within 1e-5 relative at every step."""
-    cfg = scenarios.static_config(N=20, K=4, batch=12, identical=False, seed=518)
+    primal within 1e-5 relative at every step.  N = 20 runs the W = 19 instance, N = 30 / 40 the long
+    shape's chunked W = 29 / W = 39 instances (resume mode 2, the config-5 closed loop's path)."""
+    cfg = scenarios.static_config(N=N, K=4, batch=12, identical=False, seed=518 + N)
     pat, v = cfg["pattern"], cfg["values"]
     B = v["q"].shape[0]
     s = impc.default_settings(verbose=0, adaptive_rho_interval=25)
@@ -178,6 +180,121 @@ def test_matrix_update_matches_osqp_update_P_A(ctx, which):
         check(r3[0][i], r3[2][i], w.solve())
         w.update_bounds(l4[i], u4[i])
         check(r4[0][i], r4[2][i], w.solve())
+        w.close()
+
+
+def test_nonconvex_first_solve_then_convex_matrix_update(ctx):
+    """An indefinite P: a QP whose first setup fails to factorise (P + sigma I + A'RA not positive
+    definite: osqp_setup returns OSQP_NONCVX_ERROR, no workspace; here status NON_CVX with
+    setup_exitflag 5) leaves a defined workspace (the settings' rho, zero iterates), and a convex P
+    then given through impc_batch_update_matrices solves exactly as an oracle setup from scratch
+    with that P.  A QP that factorises but diverges (status NON_CVX from the residual test) keeps
+    its workspace with the iterates cold-started (store_solution), as the oracle's does through
+    osqp_update_P.  The other QPs of the batch follow the oracle's setup -> solve -> osqp_update_P
+    -> solve."""
+    cfg = scenarios.static_config(N=20, K=4, batch=8, identical=False, seed=520)
+    pat, v = cfg["pattern"], cfg["values"]
+    B = v["q"].shape[0]
+    s = impc.default_settings(verbose=0, adaptive_rho_interval=25)
+    bad = np.arange(B) % 2 == 0
+    Pbad = v["Px"].copy()
+    Pbad[bad] = -1e4
+    b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], B)
+    try:
+        b.set_kernel(impc.KERNEL_STRUCTURED)
+        b.set_settings(s)
+        b.set_values(Pbad, v["q"], v["Ax"], v["l"], v["u"])
+        b.set_persistent(True)
+        b.solve()
+        r1 = b.get()
+        rho, xs, zs, ys = b.get_persistent()
+        b.update_matrices(v["Px"], None)
+        b.solve()
+        r2 = b.get()
+    finally:
+        b.close()
+    os_ = ora.settings_from(s)
+    kinds = set()
+    for i in range(B):
+        try:
+            w = ora.Workspace(pat, Pbad[i], v["q"][i], v["Ax"][i], v["l"][i], v["u"][i], os_)
+        except RuntimeError:  # OSQP: osqp_setup fails, no workspace
+            kinds.add("setup")
+            assert r1[2][i]["status_val"] == -7 and r1[2][i]["setup_exitflag"] == 5, r1[2][i]
+            assert rho[i] == s.rho and not xs[i].any() and not zs[i].any() and not ys[i].any()
+            w = ora.Workspace(pat, v["Px"][i], v["q"][i], v["Ax"][i], v["l"][i], v["u"][i], os_)
+            check(r2[0][i], r2[2][i], w.solve())
+            w.close()
+            continue
+        x1 = w.solve()
+        check(r1[0][i], r1[2][i], x1)
+        if x1[2]["status_val"] == -7:
+            kinds.add("diverged")
+            assert not xs[i].any() and not zs[i].any() and not ys[i].any()  # store_solution's cold_start
+        w.update_matrices(v["Px"][i], None)
+        check(r2[0][i], r2[2][i], w.solve())
+        w.close()
+    assert kinds == {"setup", "diverged"}  # the scenario reaches both kinds
+
+
+@KERNELS
+def test_failed_rho_update_ends_the_solve_unsolved(ctx, kernel):
+    """osqp_solve with an adaptive-rho update whose refactorisation fails (P indefinite, but
+    P + sigma I + A'RA positive definite at the first rho) returns exitflag 1 with the status still
+    UNSOLVED at the iteration of that update (osqp.c, adapt_rho -> goto exit; oracle ora_solve_ws)."""
+    cfg = scenarios.static_config(N=20, K=4, batch=4, identical=False, seed=520)
+    pat, v = cfg["pattern"], cfg["values"]
+    B = v["q"].shape[0]
+    s = impc.default_settings(verbose=0, adaptive_rho_interval=25)
+    P = np.full_like(v["Px"], -1e3)
+    b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], B)
+    try:
+        b.set_kernel(kernel)
+        b.set_settings(s)
+        b.set_values(P, v["q"], v["Ax"], v["l"], v["u"])
+        b.solve()
+        _, _, info = b.get()
+    finally:
+        b.close()
+    _, _, io = ora.solve_batch(pat, P, v["q"], v["Ax"], v["l"], v["u"], ora.settings_from(s))
+    assert (io["status_val"] == -10).any()  # the scenario does reach a failed rho update
+    np.testing.assert_array_equal(info["status_val"], io["status_val"])
+    np.testing.assert_array_equal(info["iter"], io["iter"])
+    np.testing.assert_array_equal(info["rho_updates"], io["rho_updates"])
+
+
+def test_solve_without_solution_cold_starts_the_next(ctx):
+    """store_solution (auxil.c): a solve that ends without a solution (primal infeasible here)
+    cold-starts the workspace's iterates, so the next solve after osqp_update_bounds starts from
+    zero -- not from the divergent iterates -- as the oracle's persistent workspace does."""
+    cfg = scenarios.static_config(N=20, K=4, batch=4, identical=False, seed=606)
+    pat, v = cfg["pattern"], cfg["values"]
+    B = v["q"].shape[0]
+    s = impc.default_settings(verbose=0, adaptive_rho_interval=25)
+    l1 = v["l"].copy()
+    l1[0, 8 * 20 + 1] = 4.9  # box row contradicting the pinned x0 -> primal infeasible
+    b = impc.Batch(ctx, pat["n"], pat["m"], pat["Pp"], pat["Pi"], pat["Ap"], pat["Ai"], B)
+    try:
+        b.set_kernel(impc.KERNEL_STRUCTURED)
+        b.set_settings(s)
+        b.set_values(v["Px"], v["q"], v["Ax"], l1, v["u"])
+        b.set_persistent(True)
+        b.solve()
+        r1 = b.get()
+        _, xs, zs, ys = b.get_persistent()
+        b.update_bounds(v["l"], v["u"])
+        b.solve()
+        r2 = b.get()
+    finally:
+        b.close()
+    os_ = ora.settings_from(s)
+    assert r1[2][0]["status_val"] == -3
+    assert not xs[0].any() and not zs[0].any() and not ys[0].any()
+    for i in range(B):
+        w = ora.Workspace(pat, v["Px"][i], v["q"][i], v["Ax"][i], l1[i], v["u"][i], os_)
+        check(r1[0][i], r1[2][i], w.solve())
+        w.update_bounds(v["l"][i], v["u"][i])
+        check(r2[0][i], r2[2][i], w.solve())
         w.close()
 
 

@@ -61,10 +61,22 @@ def test_oracle_chain_first_plan_then_fanout():
     assert r2["branch"] == ref.FANOUT and r2["valid"] and 0 <= r2["best"] < 6
 
 
-def _check_replan(out, before, pos, vel, xref, dyn_cur, pred, pred_size, prob, has_pred, cur_size, cur_count, pd, s):
+def _row(out, k, r):
+    """x, y, info and assembled values of row r of shape k (k obstacle rows per stage)."""
+    sh = out["shapes"][k]
+    return sh["x"][r], sh["y"][r], sh["info"][r], [v[r] for v in sh["vals"]]
+
+
+def _check_replan(out, before, pos, vel, xref, dyn_cur, pred, pred_size, prob, has_pred, cur_size, cur_count, pd, s,
+                  num_pred=None):
+    """One replan against the restatement, instance by instance (num_pred [I]: each instance's
+    obstacle count K_i, its first K_i slots; None = every slot)."""
     plan_x, first, _, _ = before
-    for i in range(len(out["branch"])):
-        assert out["branch"][i] == ref.branch(first[i], has_pred[i], cur_count[i]), i
+    I = len(out["branch"])
+    Kall = pred.shape[1]
+    kp = np.full(I, Kall) if num_pred is None else np.asarray(num_pred)
+    for i in range(I):
+        assert out["branch"][i] == ref.branch(first[i], bool(has_pred[i]) and kp[i] > 0, cur_count[i]), i
     expect = plan_x.copy()
     expect_first = first.copy()
 
@@ -73,36 +85,42 @@ def _check_replan(out, before, pos, vel, xref, dyn_cur, pred, pred_size, prob, h
         for key, got in zip(("Px", "q", "Ax", "l", "u"), rows_vals):
             np.testing.assert_array_equal(got, vals[key], err_msg=f"{msg} {key}")
 
-    for j, i in enumerate(out["inst_fanout"]):
-        px = plan_x[i] if out["branch"][i] == FANOUT else None
-        fo, qps = ref.fanout_qps(pd, 0, px, pos[i], vel[i], xref[i], dyn_cur[i], pred[i], pred_size[i], prob[i])
+    for i in out["inst_fanout"]:
+        Ki = int(kp[i])
+        assert out["num_obs"][i] == Ki, i
+        px = plan_x[i]
+        fo, qps = ref.fanout_qps(pd, 0, px, pos[i], vel[i], xref[i], dyn_cur[i][:Ki], pred[i][:Ki],
+                                 pred_size[i][:Ki], prob[i][:Ki])
         assert out["ob_idx"][i] == fo["ob_idx"], i
         np.testing.assert_array_equal(out["cand_type"][i], fo["types"])
-        xs, stats = [], []
+        xs, oks = [], []
         for c in range(6):
-            slot = out["cand_slot"][i][c]
-            nm, row = ("single", 4 * j + slot) if slot < 4 else ("pair", 2 * j + slot - 4)
-            x, info = out["x_" + nm][row], out["info_" + nm][row]
-            check_qp(qps[c][:2], [v[row] for v in out["vals_" + nm]], f"instance {i} candidate {c}")
+            k, r = out["cand_rows"][i][c]
+            assert k == Ki + (1 if out["cand_slot"][i][c] >= 4 else 0)
+            x, y, info, vals = _row(out, k, r)
+            check_qp(qps[c][:2], vals, f"instance {i} candidate {c}")
             xo, yo, io = ref.solve(*qps[c], s)
-            compare((x[None], out["y_" + nm][row][None], info[None]), (xo[None], yo[None], io[None]))
+            compare((x[None], y[None], info[None]), (xo[None], yo[None], io[None]))
             xs.append(x)
-            stats.append(int(info["status_val"]))
-        best = ref.select(pd, pd, 0, px, xref[i], fo, xs, stats, prob[i][fo["ob_idx"]])
+            oks.append(ref.solve_traj_ok(info))
+        best = ref.select(pd, pd, 0, px, xref[i], fo, xs, oks, prob[i][fo["ob_idx"]])
         assert out["best_cand"][i] == best, (i, out["best_cand"][i], best)
         if best >= 0:
             expect[i] = xs[best]
             expect_first[i] = 0
-    for nm, idx, br in (("first", out["inst_first"], SINGLE_FIRST), ("current", out["inst_current"], SINGLE_CURRENT)):
-        for j, i in enumerate(idx):
+    for idx, br in ((out["inst_first"], SINGLE_FIRST), (out["inst_current"], SINGLE_CURRENT)):
+        for i in idx:
             cur = br == SINGLE_CURRENT
+            ci = int(cur_count[i]) if cur else 0
             pat, vals, ws = ref.single_qp(pd, first[i], plan_x[i], pos[i], vel[i], xref[i],
-                                          dyn_cur[i] if cur else None, cur_size[i] if cur else None)
-            check_qp((pat, vals), [v[j] for v in out["vals_" + nm]], f"instance {i} single ({nm})")
-            x, info = out["x_" + nm][j], out["info_" + nm][j]
+                                          dyn_cur[i][:ci] if cur else None, cur_size[i][:ci] if cur else None)
+            k, r = out["single_rows"][i]
+            assert k == ci, (i, k, ci)
+            x, y, info, got_vals = _row(out, k, r)
+            check_qp((pat, vals), got_vals, f"instance {i} single ({'current' if cur else 'first'})")
             xo, yo, io = ref.solve(pat, vals, ws, s)
-            compare((x[None], out["y_" + nm][j][None], info[None]), (xo[None], yo[None], io[None]))
-            if int(info["status_val"]) != ref.NON_CVX:
+            compare((x[None], y[None], info[None]), (xo[None], yo[None], io[None]))
+            if ref.solve_traj_ok(info):
                 expect[i] = x
                 expect_first[i] = 0
     return expect, expect_first
@@ -143,5 +161,50 @@ def test_mixed_branches_three_chained_replans(ctx):
         assert seen == {FANOUT, SINGLE_FIRST, SINGLE_CURRENT}
         # every first-plan instance with a plan fanned out on a later replan with predictions
         assert (rp.plans()[1] == 0).all()
+    finally:
+        rp.close()
+
+
+@pytest.mark.gpu
+def test_per_instance_obstacle_counts_three_chained_replans(ctx):
+    """Every instance with its own obstacle count per replan (K_i = predPos.size(), 0..K: the
+    detector keeps the obstacles in range and view, fakeDetector.cpp:493 -> updatePredObstacles
+    :343-373) and its own number of current obstacles without predictions (c_i, 0..K): the
+    candidates of an instance have K_i and K_i + 1 obstacle rows, all shapes of the replan in one
+    grouped launch.  Three chained replans against the restatement, instance by instance."""
+    Kmax = 5
+    buckets = scenarios.intent_config(N=N, K=Kmax, instances=I, hyps=6, seed=4343)
+    inst = next(iter(buckets.values()))["instances"]
+    p, pd = impc.mpc_params(horizon=N)
+    pred_size = np.broadcast_to(inst["size"], inst["pred"].shape).copy()
+    s = impc.default_settings(verbose=0)
+    L = inst["pred"].shape[3]
+    idx = np.arange(I)
+    rng = np.random.default_rng(43)
+    first = (idx % 6 == 0).astype(np.int8)
+    num_pred = [rng.integers(0, Kmax + 1, I) for _ in range(3)]          # K_i per replan, 0 = none
+    cur_count = rng.integers(0, Kmax + 1, I).astype(np.int32)
+    cur_size = np.broadcast_to(inst["size"], (I, Kmax, 3)).copy()
+    rp = DeviceReplan(ctx, p, pd, I, Kmax, L, s)
+    rp.set_state(inst["prev"], first)
+    pos, vel, pred = inst["pos"].copy(), inst["vel"].copy(), inst["pred"].copy()
+    shapes_seen = set()
+    try:
+        for step in range(3):
+            before = rp.plans()
+            dyn_cur = pred[:, :, 0, 0, :]
+            out = rp.run(pos, vel, inst["xref"], dyn_cur=dyn_cur, pred_pos=pred, pred_size=pred_size,
+                         prob=inst["prob_all"], num_pred=num_pred[step], cur_size=cur_size, cur_count=cur_count)
+            shapes_seen.update(out["shapes"])
+            expect, expect_first = _check_replan(out, before, pos, vel, inst["xref"], dyn_cur, pred, pred_size,
+                                                 inst["prob_all"], np.ones(I, bool), cur_size, cur_count, pd, s,
+                                                 num_pred=num_pred[step])
+            plan_x, ft, pc, valid = rp.plans()
+            np.testing.assert_array_equal(plan_x, expect)
+            np.testing.assert_array_equal(ft, expect_first)
+            pos = np.where(valid[:, None] == 1, plan_x[:, 8:11], pos)
+            vel = np.where(valid[:, None] == 1, plan_x[:, 11:14], vel)
+            pred = np.concatenate([pred[:, :, :, 1:], pred[:, :, :, -1:]], axis=3)
+        assert len(shapes_seen) >= Kmax  # most obstacle counts 0 .. K + 1 took part
     finally:
         rp.close()

@@ -1,8 +1,8 @@
 """The replan's wall-clock budget (makePlanWithPred, mpcPlanner.cpp:609-628): the 0.15 s candidate
 issue cut-off, timeLimit = max(solverTimeLimit_ - time, solverTimeLimit_) on every candidate of an
 instance that is not on its first plan (solveTraj sets it only when not firstTime_, :442-444), and
-the selection over the candidates whose solveTraj succeeded (every OSQP status but NON_CVX,
-:513-518).  The limit is measured on the device's constant-rate clock, whose rate is read from
+the selection over the candidates whose solveTraj succeeded (initSolver and solveProblem NoError,
+:475-478, :513-518).  The limit is measured on the device's constant-rate clock, whose rate is read from
 the device (hipDeviceAttributeWallClockRate) and checked against HIP events here."""
 import time
 
@@ -15,12 +15,17 @@ from impc.replan import ISSUE_CUTOFF_S, DeviceReplan, candidate_valid
 
 
 def test_candidate_valid_maps_slots_to_batch_rows():
-    # two instances; slot < 4 -> single-intent row 4i+slot, else two-intent row 2i+slot-4
+    # two instances; slot < 4 -> single-intent row 4i+slot, else two-intent row 2i+slot-4; a
+    # candidate is valid when solveTraj succeeded: setup ok and solveProblem NoError -- every final
+    # status (TIME_LIMIT_REACHED, a diverged NON_CVX) but a failed setup or a failed rho update
     slot = np.array([[0, 1, 2, 3, 4, 5], [4, 0, 5, 1, 2, 3]])
-    st_single = np.array([1, 1, 1, impc.NON_CVX, 1, impc.TIME_LIMIT_REACHED, 1, 1])
-    st_pair = np.array([1, impc.NON_CVX, impc.NON_CVX, 1])
-    got = candidate_valid(slot, st_single, st_pair)
-    np.testing.assert_array_equal(got, [[1, 1, 1, 0, 1, 0], [0, 1, 1, 1, 1, 1]])
+    info_s = np.zeros(8, impc.INFO_DTYPE)
+    info_s["status_val"] = [1, 1, 1, impc.NON_CVX, 1, impc.TIME_LIMIT_REACHED, 1, 1]
+    info_s["setup_exitflag"][3] = 5                       # initSolver failed (OSQP_NONCVX_ERROR)
+    info_p = np.zeros(4, impc.INFO_DTYPE)
+    info_p["status_val"] = [1, impc.NON_CVX, -10, 1]    # diverged (valid) / failed rho update (not)
+    got = candidate_valid(slot, info_s, info_p)
+    np.testing.assert_array_equal(got, [[1, 1, 1, 0, 1, 1], [0, 1, 1, 1, 1, 1]])
     assert got.dtype == np.int8
     assert ISSUE_CUTOFF_S == 0.15
 

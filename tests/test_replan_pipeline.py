@@ -80,7 +80,7 @@ def test_device_replan_matches_host_path(ctx):
                     ptrs[i, c] = xs["pair"] + 8 * n * (2 * i + sl - 4)
                     dyn_count[i, c] = K + 1
                     dyn_pos[i, c], dyn_size[i, c] = fo["pair_pos"][i, sl - 4], fo["pair_size"][i, sl - 4]
-        valid = candidate_valid(slot, batches["single"][1]["status_val"], batches["pair"][1]["status_val"])
+        valid = candidate_valid(slot, batches["single"][1], batches["pair"][1])
         params = dict(horizon=N, num_candidates=6, max_dynamic=K + 1, pred_len=L, num_static=0, prev_len=N,
                       dynamic_safety_dist=pd["dynamic_safety_dist"], static_safety_dist=pd["static_safety_dist"])
         ref = impc.select_best(ctx, params, ptrs.reshape(-1), valid, zeros, inst["prev"], np.full(I, N, np.int32),

@@ -1,0 +1,26 @@
+#!/bin/bash
+# Round 6 GPU runs, one phase per call: bash tools/gpu_r06.sh <phase> [args].  Every GPU step runs
+# under its own time limit; the script stops at the first failure.
+set -o pipefail
+R="$GRAFT_REPO_ROOT"; cd "$R" || exit 1
+mkdir -p gpurun_out/r06; export TMPDIR=/tmp
+O=gpurun_out/r06
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider"
+case "$1" in
+  tests)  # tests/<files...> given after the phase, then (after "--") an A/B of library variants
+    shift; T=(); while [ $# -gt 0 ] && [ "$1" != "--" ]; do T+=("$1"); shift; done; [ "${1:-}" = "--" ] && shift
+    timeout -k 10 1000 $PYT "${T[@]}" > $O/pytest_sel.log 2>&1 || { tail -80 $O/pytest_sel.log; exit 1; }
+    tail -3 $O/pytest_sel.log
+    [ $# -gt 0 ] && bash tools/exp.sh "$@"
+    ;;
+  gpu)  # the whole -m gpu suite
+    timeout -k 10 1000 $PYT -m gpu tests > $O/pytest_gpu.log 2>&1 || { tail -60 $O/pytest_gpu.log; exit 1; }
+    tail -3 $O/pytest_gpu.log
+    ;;
+  c5)  # config 5's closed loop with the step-by-step chain parity
+    timeout -k 10 900 python -u bench.py --workload config5 --steps 10 --warmup 10 > $O/bench_config5.json.log 2>&1 \
+      || { tail -30 $O/bench_config5.json.log; exit 1; }
+    tail -1 $O/bench_config5.json.log > $O/bench_config5.json
+    ;;
+  *) echo "unknown phase $1"; exit 2 ;;
+esac

@@ -5,7 +5,9 @@ commit), the config 3 workload (K = 8 dynamic obstacles, 6 candidates per instan
 Inputs are resident on the device before the timed region; every replan is timed from the call
 to the end of its commit on the device (impc_replan_run + a context synchronisation), i.e. the
 full call's wall clock, and the state each replan commits is the next one's (chained replans).
-Prints one JSON line."""
+call_return_s: the host time until impc_replan_run returns (the call queues the whole replan and
+does not wait for the device).  --instances 1 / 16 give the small-batch latency.  Prints one JSON
+line."""
 import argparse
 import json
 import os
@@ -41,7 +43,7 @@ def main():
            dict(pos=inst["pos"], vel=inst["vel"], xref=inst["xref"], dyn_cur=inst["obp"], pred_pos=inst["pred"],
                 pred_size=pred_size, prob=inst["prob_all"]).items()}
     ptr = {k: d.ptr for k, d in dev.items()}
-    walls, stage, iters, branches = [], [], [], []
+    walls, stage, iters, branches, ret = [], [], [], [], []
     for r in range(a.reps + 1):
         ctx.synchronize()
         t0 = time.perf_counter()
@@ -52,9 +54,10 @@ def main():
         if r:  # the first call also builds the kernel-class entry tables
             walls.append(wall)
             stage.append(st["stage_s"])
+            ret.append(st["total_s"])
         branches.append((st["fanout"], st["single_first"], st["single_current"]))
     # mean iterations of the last replan (inspection after the timed runs)
-    for k in (0, 1):
+    for k in (K, K + 1):  # the candidates' shapes (K and K + 1 obstacle rows)
         r = rp._shape_results(k, False)
         if r:
             iters.append(r["info"]["iter"])
@@ -64,7 +67,8 @@ def main():
                       "instances": I, "candidate_qps": 6 * I, "reps": a.reps,
                       "call_wall_s": w.tolist(), "call_wall_s_median": float(np.median(w)),
                       "replans_per_s": float(I / np.median(w)), "qp_solves_per_s": float(6 * I / np.median(w)),
-                      "stage_s_median": float(np.median(stage)), "branches_last": branches[-1],
+                      "stage_s_median": float(np.median(stage)), "call_return_s_median": float(np.median(ret)),
+                      "branches_last": branches[-1],
                       "mean_iter_last": float(it.mean()), "build_id": impc.lib.impc_build_id().decode()}))
     for d in dev.values():
         d.free()
