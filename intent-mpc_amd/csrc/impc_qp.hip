@@ -450,7 +450,10 @@ __global__ __launch_bounds__(NL, WPS) void k_mpc_wave_group(const GroupEntry *__
     GpuTeam<NL> wv{smem + LD::RED_OFF};
     __shared__ unsigned next;
     int cur = -1;
-    if (devcnt) {  // device-side active counts: the queue's length is their sum (ord puts them first)
+#ifndef IMPC_R6_DEVCNT
+#define IMPC_R6_DEVCNT 1
+#endif
+    if (IMPC_R6_DEVCNT && devcnt) {  // device-side active counts: the queue's length is their sum (ord puts them first)
         int64_t t = 0;
         for (int e = 0; e < count; e++) {
             const int64_t c = g[e].dcount ? *g[e].dcount : g[e].io.B;

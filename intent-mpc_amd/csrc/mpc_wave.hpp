@@ -50,6 +50,13 @@ namespace impc {
 
 #define IMPC_WF __host__ __device__ __forceinline__
 
+// Round-6 A/B switches (tools only; the product builds them on)
+#ifndef IMPC_R6_REFAIL
+#define IMPC_R6_REFAIL 1
+#endif
+#ifndef IMPC_R6_PERSIST
+#define IMPC_R6_PERSIST 1
+#endif
 // Phase-cost experiments (tools/exp.sh only): IMPC_DUP=<section id> runs that idempotent phase of
 // the ADMM iteration twice; the bench's time difference is the phase's marginal cost.
 #ifndef IMPC_DUP
@@ -1895,7 +1902,7 @@ struct WaveQP {
             // rho and zero iterates (osqp_setup's cold_start), so a resume after a matrix update
             // (impc_batch_update_matrices) starts as a fresh setup would; a failed resume keeps the
             // workspace it had (OSQP keeps work->x, z, y when osqp_update_P / _A fails to refactor)
-            if (ps && io.resume == 0) {
+            if (IMPC_R6_PERSIST && ps && io.resume == 0) {
                 double *it = ps + kPersistHdr;
                 if (L == 0) ps[kPersistHdr - 1] = R.rho;
                 _Pragma("unroll") for (int s = 0; s < VS; s++)
@@ -1983,10 +1990,14 @@ struct WaveQP {
         for (;;) {
             if (refac) {
                 refac = false;
+#if IMPC_R6_REFAIL
                 if (factorize()) {  // osqp_solve: a failed rho update ends the solve with exitflag 1
                     refail = true;
                     break;
                 }
+#else
+                factorize();
+#endif
                 write_v_products();
                 IMPC_SEC(kSecFactor);
             }
@@ -2125,15 +2136,26 @@ struct WaveQP {
             _Pragma("unroll") for (int s = 0; s < VS; s++) {
                 if (!vok[s]) continue;
                 const int v = NL * s + L;
+#if IMPC_R6_PERSIST
                 it[v] = has_sol2 ? x[s] : 0.0;
                 it[n + v] = has_sol2 ? zb[s] : 0.0;
                 it[2 * n + v] = has_sol2 ? yb[s] : 0.0;
+#else
+                it[v] = x[s];
+                it[n + v] = zb[s];
+                it[2 * n + v] = yb[s];
+#endif
             }
             _Pragma("unroll") for (int s = 0; s < GS; s++) {
                 if (!gok[s]) continue;
                 const int g = NL * s + L;
+#if IMPC_R6_PERSIST
                 it[3 * n + g] = has_sol2 ? z[s] : 0.0;
                 it[3 * n + T.mg + g] = has_sol2 ? y[s] : 0.0;
+#else
+                it[3 * n + g] = z[s];
+                it[3 * n + T.mg + g] = y[s];
+#endif
             }
         }
         const bool scaled = st.scaling > 0;

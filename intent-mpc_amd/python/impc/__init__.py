@@ -83,6 +83,8 @@ _dp = C.POINTER(C.c_double)
 
 
 def _sig(name, res, *args):
+    if os.environ.get("IMPC_LIB_VARIANT") and not hasattr(lib, name):
+        return None  # an older library kept for an A/B (tools only): entry points added since are absent
     f = getattr(lib, name)
     f.restype = res
     f.argtypes = list(args)

@@ -241,9 +241,14 @@ def test_nonconvex_first_solve_then_convex_matrix_update(ctx):
 def test_failed_rho_update_ends_the_solve_unsolved(ctx, kernel):
     """osqp_solve with an adaptive-rho update whose refactorisation fails (P indefinite, but
     P + sigma I + A'RA positive definite at the first rho) returns exitflag 1 with the status still
-    UNSOLVED at the iteration of that update (osqp.c, adapt_rho -> goto exit; oracle ora_solve_ws)."""
+    UNSOLVED at the iteration of that update (osqp.c, adapt_rho -> goto exit; oracle ora_solve_ws).
+    The seed's third QP is left out: with an indefinite P its iterates grow until the rho update,
+    and the iteration at which that happens differs between any two implementations (the oracle
+    1,025, the kernels' CPU builds 900 / 925, the generic kernel on MI355X 675; same status)."""
     cfg = scenarios.static_config(N=20, K=4, batch=4, identical=False, seed=520)
     pat, v = cfg["pattern"], cfg["values"]
+    keep = [0, 1, 3]
+    v = {k: a[keep] for k, a in v.items()}
     B = v["q"].shape[0]
     s = impc.default_settings(verbose=0, adaptive_rho_interval=25)
     P = np.full_like(v["Px"], -1e3)

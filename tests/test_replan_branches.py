@@ -67,6 +67,18 @@ def _row(out, k, r):
     return sh["x"][r], sh["y"][r], sh["info"][r], [v[r] for v in sh["vals"]]
 
 
+def _solution_check(x, y, info, xo, yo, io, degenerate):
+    """A QP's solution against the oracle's.  degenerate: the instance's state is an OSQP_NAN plan
+    (2143289344.0 in every entry) that an earlier replan committed -- the reference does commit one
+    when every candidate is infeasible or diverged, since solveProblem returns NoError for them
+    (mpcPlanner.cpp:513-518, 629-639) -- so the QP is linearised and warm-started at 2e9 and only its
+    status is compared (its iterates carry no precision)."""
+    if degenerate:
+        assert info["status_val"] == io["status_val"], (info, io)
+    else:
+        compare((x[None], y[None], info[None]), (xo[None], yo[None], io[None]))
+
+
 def _check_replan(out, before, pos, vel, xref, dyn_cur, pred, pred_size, prob, has_pred, cur_size, cur_count, pd, s,
                   num_pred=None):
     """One replan against the restatement, instance by instance (num_pred [I]: each instance's
@@ -100,7 +112,7 @@ def _check_replan(out, before, pos, vel, xref, dyn_cur, pred, pred_size, prob, h
             x, y, info, vals = _row(out, k, r)
             check_qp(qps[c][:2], vals, f"instance {i} candidate {c}")
             xo, yo, io = ref.solve(*qps[c], s)
-            compare((x[None], y[None], info[None]), (xo[None], yo[None], io[None]))
+            _solution_check(x, y, info, xo, yo, io, np.abs(px).max() >= 1e9)
             xs.append(x)
             oks.append(ref.solve_traj_ok(info))
         best = ref.select(pd, pd, 0, px, xref[i], fo, xs, oks, prob[i][fo["ob_idx"]])
@@ -119,7 +131,7 @@ def _check_replan(out, before, pos, vel, xref, dyn_cur, pred, pred_size, prob, h
             x, y, info, got_vals = _row(out, k, r)
             check_qp((pat, vals), got_vals, f"instance {i} single ({'current' if cur else 'first'})")
             xo, yo, io = ref.solve(pat, vals, ws, s)
-            compare((x[None], y[None], info[None]), (xo[None], yo[None], io[None]))
+            _solution_check(x, y, info, xo, yo, io, not first[i] and np.abs(plan_x[i]).max() >= 1e9)
             if ref.solve_traj_ok(info):
                 expect[i] = x
                 expect_first[i] = 0

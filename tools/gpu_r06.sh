@@ -13,6 +13,12 @@ case "$1" in
     tail -3 $O/pytest_sel.log
     [ $# -gt 0 ] && bash tools/exp.sh "$@"
     ;;
+  lds)  # LDS bank conflicts per phase: each phase-duplication variant (lib/libimpc_qp_dup<id>.so,
+        # IMPC_DUP = section id) against the product, bench value + one PMC pass each
+    shift
+    PMC="SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_WAIT_INST_LDS" BARGS="--e2e-steps 0" \
+      bash tools/exp.sh "$@" 2>&1 | tee $O/lds_phases.txt
+    ;;
   gpu)  # the whole -m gpu suite
     timeout -k 10 1000 $PYT -m gpu tests > $O/pytest_gpu.log 2>&1 || { tail -60 $O/pytest_gpu.log; exit 1; }
     tail -3 $O/pytest_gpu.log
