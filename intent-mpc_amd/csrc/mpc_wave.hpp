@@ -134,7 +134,10 @@ namespace impc {
 struct WaveTables {
     int32_t n, m, mg, N, W, CG, nnzP, nnzA;
     const int32_t *var_orig, *var_pdiag, *var_boxrow, *var_boxpos;
-    const int32_t *gen_row, *gen_col, *gen_pos, *colg, *term_ptr, *term;
+    // general rows: table slot g is the kernel's row slot g / NL of lane g mod NL (gen_row -1: an
+    // empty slot), the rows spread over the lanes by MpcStructure::place; gen_dst [4 mg]: each
+    // entry's products slot (-1 absent); the factorisation program indexes the table slots
+    const int32_t *gen_row, *gen_col, *gen_pos, *gen_dst, *term_ptr, *term;
     int32_t HS;               // heavy columns (second products tier), MpcStructure::HS; 0: one tier
     const int32_t *col_hid;   // [n] heavy-column index or -1 (stage order)
     int32_t T1r;              // first-tier rows: cg4(CG) (one tier) or kProdTier1 (two tiers)
@@ -225,12 +228,12 @@ struct WaveLds {
     static constexpr int X_OFF = E_OFF + NP;                // xbuf
     static constexpr int RED_OFF = X_OFF + NP;              // team reduction scratch [kRedLen]
     static constexpr int JUNK_OFF = RED_OFF + kRedLen;      // per-lane discard slots [NL]
-    static constexpr int GSLOT_OFF = JUNK_OFF + NL;         // int16 [4 NL GS]: general entry -> product slot
     // One-variable-per-lane shape: the Ruiz scaling vectors D, E and the ADMM deltas of the
     // termination checks live here (the long-horizon shape keeps them in HBM / registers: its LDS
     // is full).  Layout of each: [var slots NMAX][box rows NMAX][general slots NL GS].
     static constexpr bool ONCHIP = VS == 1;
     static constexpr int VEC_N = 2 * NMAX + NL * GS;
+    static constexpr int GSLOT_OFF = JUNK_OFF + NL;         // int16 [4 NL GS]: general entry -> product slot
     static constexpr int SCL_OFF = GSLOT_OFF + NL * GS;           // D, E (scaling)
     static constexpr int DLT_OFF = SCL_OFF + (ONCHIP ? VEC_N : 0);  // dx, dy (check iterations)
     static constexpr int P_OFF = DLT_OFF + (ONCHIP ? VEC_N : 0);  // products, column-slot layout (size below)
@@ -243,7 +246,7 @@ struct WaveLds {
     // product per obstacle row, so the second tier is (CG4 - 4) rows of the HS heavy columns
     // instead of CG4 rows of all n (K = 21: 21 KB instead of 49 KB).  It doubles as the
     // factorisation's (4g + e) scratch and general-row rho.  Sized from the pattern at run time,
-    // followed by 8 discard slots (index p_size).
+    // followed by kDiscard discard slots (index p_size).
     static constexpr int T1 = kProdTier1;
     static IMPC_WF int cg4(int CG) { return (CG + 3) & ~3; }
     // +PAD: the obstacle rows of one stage write their products to the same column in different
@@ -257,10 +260,16 @@ struct WaveLds {
         return c > f ? c : f;
     }
     static IMPC_WF int p_size(const WaveTables &T) { return p_size(T.CG, T.n, T.HS, T.mg, T.T1r); }
+    // discard slots after the products region: an absent entry's zero product lands on one whose
+    // bank no present entry of its 16-lane write group uses (MpcStructure::place)
+    static constexpr int kDiscard = 16;
+    // the entry addresses of a lane L past the tables (a dense-order batch's row slots >= mg):
+    // products discard slot p_size + (L mod 16), x exchange zero NMAX + (L mod 32)
+    static IMPC_WF int pad_lds(int pz, int L) { return ((pz + (L & 15)) << 16) | (NMAX + (L & 31)); }
     // the chunk operators' region of the one-slot shape (IMPC_CHUNK19), after the products
     static constexpr int CHX = (VS == 1 && IMPC_CHUNK19) ? 448 : 0;
-    static IMPC_WF int ch_off(const WaveTables &T) { return P_OFF + p_size(T) + 8; }
-    static IMPC_WF int size(const WaveTables &T) { return P_OFF + p_size(T) + 8 + CHX; }
+    static IMPC_WF int ch_off(const WaveTables &T) { return P_OFF + p_size(T) + kDiscard; }
+    static IMPC_WF int size(const WaveTables &T) { return P_OFF + p_size(T) + kDiscard + CHX; }
     // factorisation aliases (inside R..X region and the products buffer)
     static constexpr int FA = R_OFF, FL = FA + 169, FI = FL + 169, FB = FI + 169, FG = FB + 104, FE = FG + 104,
                          DIAGX = FE + 64;
@@ -469,23 +478,24 @@ struct WaveQP {
         }
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
             int g = NL * s + L;
-            gok[s] = g < T.mg;
+            const bool tab = g < T.mg;
+            gok[s] = tab && T.gen_row[g] >= 0;
             z[s] = y[s] = lg[s] = ug[s] = dyg_[s] = 0.0;
             gt[s] = 0;
             const int16_t *gs = (const int16_t *)(lds + LD::GSLOT_OFF);
             const int pz = LD::p_size(T);
             _Pragma("unroll") for (int e = 0; e < 4; e++) {
                 a[s][e] = 0.0;
-                gc[s][e] = (pz << 16) | LD::NMAX;  // discard slot / zero tail of the x exchange
+                gc[s][e] = LD::pad_lds(pz, L);  // past the tables: discard slot / zero tail
             }
-            if (gok[s]) {
+            if (tab) {  // an absent entry (gen_col = -1 - k): its discard slot, the zero at NMAX + k
                 _Pragma("unroll") for (int e = 0; e < 4; e++) {
                     int col = T.gen_col[4 * g + e], pos = T.gen_pos[4 * g + e];
-                    if (col >= 0) {
-                        gc[s][e] = ((int)gs[4 * g + e] << 16) | col;
-                        a[s][e] = Aval(pos);
-                    }
+                    gc[s][e] = ((int)gs[4 * g + e] << 16) | (col >= 0 ? col : LD::NMAX - 1 - col);
+                    if (col >= 0) a[s][e] = Aval(pos);
                 }
+            }
+            if (gok[s]) {
                 int row = T.gen_row[g];
                 lg[s] = dmin(dmax(io.l[bm + row], -kInf), kInf);
                 ug[s] = dmin(dmax(io.u[bm + row], -kInf), kInf);
@@ -497,28 +507,19 @@ struct WaveQP {
         }
     }
 
-    // Per-workgroup tables (once per launch): the product slot of every general-row entry
-    // (mpc_structure colg inverted into the column-slot layout, int16 in LDS; padded entries get
-    // the discard slot), and a zeroed products region (slots no entry maps to must read 0).
+    // Per-workgroup tables (once per launch and batch): the product slot of every general-row
+    // entry (gen_dst, int16 in LDS) and a zeroed products region (slots no entry maps to must read 0).
     static IMPC_WF void load_tables(WV &w, const WaveTables &T, double *lds) {
         int16_t *gs = (int16_t *)(lds + LD::GSLOT_OFF);
-        const int pz = LD::p_size(T);
-        for (int e = w.lane(); e < 4 * NL * GS; e += NL) gs[e] = (int16_t)pz;
         double *pb = lds + LD::P_OFF;
-        for (int e = w.lane(); e < pz + 8; e += NL) pb[e] = 0.0;
-        w.sync();
-        for (int e = w.lane(); e < T.n * T.CG; e += NL) {
-            const int v = e / T.CG, t = e % T.CG, id = T.colg[e];
-            if (id >= 0)
-                gs[id] = (int16_t)(t < T.T1r ? t * LD::stride(T.n) + v
-                                             : T.T1r * LD::stride(T.n) + (t - T.T1r) * LD::hsp(T.HS) + T.col_hid[v]);
-        }
+        for (int e = w.lane(); e < LD::p_size(T) + LD::kDiscard; e += NL) pb[e] = 0.0;
+        for (int e = w.lane(); e < 4 * T.mg; e += NL) gs[e] = (int16_t)T.gen_dst[e];
         w.sync();
     }
 
     IMPC_WF void zero_products() {
         double *pb = pbuf();
-        const int cnt = LD::p_size(T) + 8;
+        const int cnt = LD::p_size(T) + LD::kDiscard;
         for (int i = L; i < cnt; i += NL) pb[i] = 0.0;
         wv.sync();
     }

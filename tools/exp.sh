@@ -4,8 +4,16 @@
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; cd "$R" || exit 1
 mkdir -p gpurun_out/exp; export TMPDIR=/tmp
+# a variant "env:NAME=VALUE" runs the product library with that environment variable set
+prev=
 for v in "$@"; do
-  if [ "$v" = base ]; then unset IMPC_LIB_VARIANT; else export IMPC_LIB_VARIANT=$v; fi
+  unset IMPC_LIB_VARIANT
+  [ -n "$prev" ] && unset "$prev"; prev=
+  case "$v" in
+    base) ;;
+    env:*) kv=${v#env:}; export "$kv"; prev=${kv%%=*}; v=${kv//=/_} ;;
+    *) export IMPC_LIB_VARIANT=$v ;;
+  esac
   timeout -k 10 300 python bench.py --steps ${STEPS:-2} --warmup 1 --cpu-sample 0 ${BARGS:-} > gpurun_out/exp/$v.log 2>&1 || { tail -20 gpurun_out/exp/$v.log; exit 1; }
   python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], round(d['value']), d['kernel_ms'], d['iters']['mean'])" gpurun_out/exp/$v.log $v
   if [ -n "${PMC:-}" ]; then
