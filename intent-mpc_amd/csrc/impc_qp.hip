@@ -450,10 +450,7 @@ __global__ __launch_bounds__(NL, WPS) void k_mpc_wave_group(const GroupEntry *__
     GpuTeam<NL> wv{smem + LD::RED_OFF};
     __shared__ unsigned next;
     int cur = -1;
-#ifndef IMPC_R6_DEVCNT
-#define IMPC_R6_DEVCNT 1
-#endif
-    if (IMPC_R6_DEVCNT && devcnt) {  // device-side active counts: the queue's length is their sum (ord puts them first)
+    if (devcnt) {  // device-side active counts: the queue's length is their sum (ord puts them first)
         int64_t t = 0;
         for (int e = 0; e < count; e++) {
             const int64_t c = g[e].dcount ? *g[e].dcount : g[e].io.B;
@@ -622,7 +619,6 @@ struct impc_batch_s {
     bool tier = false;  // two-tier products layout (grouped-kernel instances only)
     int gs = 0;  // general-row slots per lane of the structured kernel
     int vs = 1;  // variable slots per lane (kWaveVS, or kWaveVSLong for long horizons)
-    int per_cu = 1;  // resident teams per CU the shape is sized for (Shape<vs>::PER_CU)
     void *d_tables = nullptr;
     double *d_scal = nullptr;
     unsigned *d_counter = nullptr;
@@ -1108,13 +1104,6 @@ bool wavefront_shape_on() {
     return IMPC_WAVEFRONT != 0 && !(e && e[0] == '0');
 }
 
-// The general rows spread over the lanes for conflict-free LDS banks (MpcStructure::place) unless
-// IMPC_ROW_PLACE=0 is in the environment when the batch is created (A/B: the dense row order).
-bool row_place_on() {
-    const char *e = std::getenv("IMPC_ROW_PLACE");
-    return !(e && e[0] == '0');
-}
-
 // Shape selection: (when built) the wavefront shape if the pattern fits it with four QPs per CU,
 // else the team shape (n <= 256), else the long shape.  Sets b->vs, b->gs, b->tier and the tables' layout
 // fields; false if no structured shape takes the pattern.
@@ -1146,7 +1135,6 @@ bool choose_shape(impc_batch b) {
         if (!lds || lds > (need_full ? budget : (size_t)(160 * 1024 - 1024))) return false;
         b->vs = vs;
         b->gs = g;
-        b->per_cu = per_cu;
         b->tier = t.T1r < impc::WaveLds<256, kWaveVS, 2>::cg4(s.CG);
         return true;
     };
@@ -1165,26 +1153,10 @@ int prepare_structured(impc_batch b) {
         b->structured_ok = false;  // the generic kernel takes it
         return IMPC_OK;
     }
-    impc::MpcStructure &s = *b->ms;
+    const impc::MpcStructure &s = *b->ms;
     impc::WaveTables &t = b->wt;
-    // the general rows' lane placement for the chosen shape (conflict-free LDS banks): spread over
-    // all NL GS row slots unless that would cost the shape a resident team per CU (the factorisation
-    // scratch grows with the slot count), else the dense order
-    {
-        const int nl = b->vs == kWaveVSFront ? Shape<kWaveVSFront>::NL : Shape<kWaveVS>::NL;
-        int slots = s.mg;
-        if (row_place_on()) {
-            impc::WaveTables tp = t;
-            tp.mg = nl * b->gs;
-            const size_t cap = 160 * 1024 - 1024, l0 = wave_lds_bytes(b->vs, b->gs, t), l1 = wave_lds_bytes(b->vs, b->gs, tp);
-            if (l1 && cap / l1 >= std::min<size_t>(cap / l0, (size_t)b->per_cu)) slots = tp.mg;
-        }
-        using LD0 = impc::WaveLds<256, kWaveVS, 2>;
-        s.place(slots, t.T1r, LD0::stride(s.n), LD0::hsp(s.HS), LD0::p_size(s.CG, s.n, t.HS, slots, t.T1r), nl * b->vs);
-        t.mg = s.mg;
-    }
     std::vector<const std::vector<int32_t> *> arrs = {&s.var_orig, &s.var_pdiag, &s.var_boxrow, &s.var_boxpos,
-                                                      &s.gen_row,  &s.gen_col,   &s.gen_pos,    &s.gen_dst,
+                                                      &s.gen_row,  &s.gen_col,   &s.gen_pos,    &s.colg,
                                                       &s.term_ptr, &s.term,      &s.col_hid};
     std::vector<size_t> offs;
     size_t tot = 0;
@@ -1199,7 +1171,7 @@ int prepare_structured(impc_batch b) {
     IMPC_TRY(h2d_sync(b->ctx->stream, b->d_tables, h.data(), h.size() * 4));
     const int32_t *base = (const int32_t *)b->d_tables;
     const int32_t **dst_ptrs[] = {&t.var_orig, &t.var_pdiag, &t.var_boxrow, &t.var_boxpos, &t.gen_row,
-                                  &t.gen_col,  &t.gen_pos,   &t.gen_dst,    &t.term_ptr,   &t.term,
+                                  &t.gen_col,  &t.gen_pos,   &t.colg,       &t.term_ptr,   &t.term,
                                   &t.col_hid};
     for (size_t k = 0; k < arrs.size(); k++) *dst_ptrs[k] = base + offs[k];
     // per-QP HBM scratch for the scaling vectors: the wavefront and long shapes (the team shape keeps
@@ -2257,7 +2229,6 @@ int impc_batch_get_persistent(impc_batch b, double *rho, double *x, double *z, d
             if (y) y[k * m + ms.var_boxrow[v]] = it[2 * n + v];
         }
         for (int64_t g = 0; g < mg; g++) {
-            if (ms.gen_row[g] < 0) continue;  // an empty row slot
             if (z) z[k * m + ms.gen_row[g]] = it[3 * n + g];
             if (y) y[k * m + ms.gen_row[g]] = it[3 * n + mg + g];
         }

@@ -2,7 +2,6 @@
 #include "mpc_structure.hpp"
 
 #include <algorithm>
-#include <cmath>
 
 namespace impc {
 
@@ -113,193 +112,7 @@ std::string MpcStructure::analyse(int64_t n64, int64_t m64, const int64_t *Pp, c
         term_ptr[d + 1] = (int32_t)term.size();
     }
     if (term.empty()) term.push_back(0);
-    mgd = mg;
-    gen_dst.clear();
     return "";
-}
-
-namespace {
-
-// fixed-seed generator: the placement is a function of the pattern and the shape alone
-struct Lcg {
-    uint64_t s = 0x9E3779B97F4A7C15ull;
-    uint32_t next() {
-        s = s * 6364136223846793005ull + 1442695040888963407ull;
-        return (uint32_t)(s >> 32);
-    }
-    int below(int n) { return (int)(((uint64_t)next() * (uint64_t)n) >> 32); }
-    double unit() { return (next() >> 8) * (1.0 / 16777216.0); }
-};
-
-}  // namespace
-
-void MpcStructure::place(int slots, int T1r, int stride, int hsp, int pz, int nmax) {
-    const bool spread = slots > mgd;
-    // per dense row and entry: products slot (slot t of column v, colg order) and x index
-    std::vector<int32_t> wa((size_t)4 * mgd, -1), ra((size_t)4 * mgd, -1);
-    for (int32_t v = 0; v < n; v++)
-        for (int32_t t = 0; t < CG; t++) {
-            const int32_t id = colg[(size_t)v * CG + t];
-            if (id < 0) continue;
-            wa[id] = t < T1r ? t * stride + v : T1r * stride + (t - T1r) * hsp + col_hid[v];
-            ra[id] = v;
-        }
-    const int L = std::max<int>(slots, mgd);
-    std::vector<int32_t> lane(L, -1);  // table slot -> dense row
-    for (int32_t g = 0; g < mgd; g++) lane[g] = g;
-    // bank occupancy, kept incrementally: per (16-lane group, entry) the write addresses per bank
-    // (distinct within a group), per (32-lane pair, entry) the rows reading each column and the
-    // distinct columns per bank
-    const int G = (L + 15) / 16, H = (L + 31) / 32;
-    std::vector<int16_t> cw((size_t)G * 4 * 16, 0), dr((size_t)H * 4 * 32, 0), cr((size_t)H * 4 * n, 0);
-    auto upd = [&](int p, int g, int s) {  // row g enters (s = 1) or leaves (s = -1) slot p
-        if (g < 0) return;
-        const size_t j = (size_t)p / 16, h = (size_t)p / 32;
-        for (int e = 0; e < 4; e++) {
-            const int32_t w = wa[4 * g + e], r = ra[4 * g + e];
-            if (w >= 0) cw[(j * 4 + e) * 16 + (w & 15)] += s;
-            if (r >= 0) {
-                int16_t &c = cr[(h * 4 + e) * n + r];
-                c += s;
-                if ((s > 0 && c == 1) || (s < 0 && c == 0)) dr[(h * 4 + e) * 32 + (r & 31)] += s;
-            }
-        }
-    };
-    // extra LDS cycles of the write group j / the read pair h, all four entries
-    auto wcost = [&](int j) {
-        int c = 0;
-        for (int e = 0; e < 4; e++) {
-            int mx = 0;
-            for (int b = 0; b < 16; b++) mx = std::max<int>(mx, cw[((size_t)j * 4 + e) * 16 + b]);
-            c += mx > 1 ? mx - 1 : 0;
-        }
-        return c;
-    };
-    auto rcost = [&](int h) {
-        int c = 0;
-        for (int e = 0; e < 4; e++) {
-            int mx = 0;
-            for (int b = 0; b < 32; b++) mx = std::max<int>(mx, dr[((size_t)h * 4 + e) * 32 + b]);
-            c += mx > 1 ? mx - 1 : 0;
-        }
-        return c;
-    };
-    place_conflicts[0] = place_conflicts[1] = 0;
-    place_iters = 0;
-    if (spread && L > mgd) {
-        // first fit: each row into the least-filled 16-lane group where none of its entries meets
-        // a write bank the group holds or a read bank its 32-lane pair holds with another column
-        std::vector<int> fill(G, 0);
-        std::fill(lane.begin(), lane.end(), -1);
-        for (int32_t g = 0; g < mgd; g++) {
-            int best = 0, bk = 1 << 30;
-            for (int j = 0; j < G; j++) {
-                if (fill[j] >= 16 || 16 * j + fill[j] >= L) continue;
-                const size_t h = (size_t)j / 2;
-                int c = 0;
-                for (int e = 0; e < 4; e++) {
-                    const int32_t w = wa[4 * g + e], r = ra[4 * g + e];
-                    if (w >= 0 && cw[((size_t)j * 4 + e) * 16 + (w & 15)] > 0) c++;
-                    if (r >= 0 && cr[(h * 4 + e) * n + r] == 0 && dr[(h * 4 + e) * 32 + (r & 31)] > 0) c++;
-                }
-                const int key = c * 64 + fill[j];
-                if (key < bk) bk = key, best = j;
-            }
-            const int p = 16 * best + fill[best]++;
-            lane[p] = g;
-            upd(p, g, 1);
-        }
-    } else {
-        for (int p = 0; p < L; p++) upd(p, lane[p], 1);
-    }
-    std::vector<int> Wc(G), Rc(H);
-    int tot = 0;
-    for (int j = 0; j < G; j++) tot += Wc[j] = wcost(j);
-    for (int h = 0; h < H; h++) tot += Rc[h] = rcost(h);
-    if (spread && tot > 0 && L > mgd) {
-        // annealing over slot swaps from there (a fixed seed and schedule: deterministic); a move
-        // takes a slot of a conflicting group and any slot of another group, a row or empty
-        Lcg rng;
-        const int iters = 200000;
-        const double T0 = 0.3, T1 = 0.03, decay = std::pow(T1 / T0, 1.0 / iters);
-        double T = T0;
-        std::vector<int32_t> best = lane;
-        int best_tot = tot;
-        auto swp = [&](int a, int b) {
-            upd(a, lane[a], -1);
-            upd(b, lane[b], -1);
-            std::swap(lane[a], lane[b]);
-            upd(a, lane[a], 1);
-            upd(b, lane[b], 1);
-        };
-        for (int it = 0; it < iters && tot > 0; it++, T *= decay) {
-            int a = rng.below(L);
-            for (int k = 0; k < 16 && Wc[a / 16] == 0 && Rc[a / 32] == 0; k++) a = rng.below(L);
-            const int b = rng.below(L);
-            if (a / 16 == b / 16 || lane[a] == lane[b]) continue;
-            const int ja = a / 16, jb = b / 16, ha = a / 32, hb = b / 32;
-            const int before = Wc[ja] + Wc[jb] + Rc[ha] + (hb != ha ? Rc[hb] : 0);
-            swp(a, b);
-            const int wa2 = wcost(ja), wb2 = wcost(jb), ra2 = rcost(ha), rb2 = hb != ha ? rcost(hb) : 0;
-            const int d = wa2 + wb2 + ra2 + rb2 - before;
-            if (d <= 0 || rng.unit() < std::exp(-d / T)) {
-                Wc[ja] = wa2;
-                Wc[jb] = wb2;
-                Rc[ha] = ra2;
-                if (hb != ha) Rc[hb] = rb2;
-                tot += d;
-                if (tot < best_tot) best_tot = tot, best = lane, place_iters = it;
-            } else {
-                swp(a, b);
-            }
-        }
-        if (best != lane) {
-            for (int p = 0; p < L; p++) upd(p, lane[p], -1);
-            lane = best;
-            for (int p = 0; p < L; p++) upd(p, lane[p], 1);
-        }
-    }
-    for (int j = 0; j < G; j++) place_conflicts[0] += wcost(j);
-    for (int h = 0; h < H; h++) place_conflicts[1] += rcost(h);
-    // renumber the tables to the slots; an absent entry (padded, or any entry of an empty slot)
-    // writes its zero product to a discard slot pz + k and reads a zero of the x exchange's tail,
-    // nmax + k' (gen_col = -1 - k'), each on a bank no present entry of its group uses
-    std::vector<int32_t> row2(L, -1), col2((size_t)4 * L, -1), pos2((size_t)4 * L, -1), slot_of(mgd, -1);
-    gen_dst.assign((size_t)4 * L, -1);
-    for (int p = 0; p < L; p++) {
-        const int g = lane[p];
-        if (g < 0) continue;
-        slot_of[g] = p;
-        row2[p] = gen_row[g];
-        for (int e = 0; e < 4; e++) pos2[4 * p + e] = gen_pos[4 * g + e];
-    }
-    for (int p = 0; p < L; p++)
-        for (int e = 0; e < 4; e++) {
-            const int g = lane[p];
-            if (g >= 0 && wa[4 * g + e] >= 0) {
-                gen_dst[4 * p + e] = wa[4 * g + e];
-                col2[4 * p + e] = ra[4 * g + e];
-                continue;
-            }
-            uint32_t wu = 0, ru = 0;
-            for (int i = 16 * (p / 16); i < std::min(L, 16 * (p / 16) + 16); i++)
-                if (lane[i] >= 0 && wa[4 * lane[i] + e] >= 0) wu |= 1u << (wa[4 * lane[i] + e] & 15);
-            for (int i = 32 * (p / 32); i < std::min(L, 32 * (p / 32) + 32); i++)
-                if (lane[i] >= 0 && ra[4 * lane[i] + e] >= 0) ru |= 1u << (ra[4 * lane[i] + e] & 31);
-            int bw = 0, br = 0;
-            while (bw < 15 && (wu >> bw & 1)) bw++;
-            while (br < 31 && (ru >> br & 1)) br++;
-            gen_dst[4 * p + e] = pz + ((bw - pz) & 15);
-            col2[4 * p + e] = -1 - ((br - nmax) & 31);
-        }
-    for (auto &id : colg)
-        if (id >= 0) id = 4 * slot_of[id >> 2] + (id & 3);
-    if (mgd > 0)  // the program on the slots (same term order)
-        for (auto &c : term) c = (slot_of[c >> 4] << 4) | (c & 15);
-    gen_row.swap(row2);
-    gen_col.swap(col2);
-    gen_pos.swap(pos2);
-    mg = L;
 }
 
 }  // namespace impc

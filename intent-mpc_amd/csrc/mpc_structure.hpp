@@ -35,22 +35,6 @@ struct MpcStructure {
     // Returns "" when the pattern is stage-structured, else the reason it is not.
     std::string analyse(int64_t n, int64_t m, const int64_t *Pp, const int64_t *Pi, const int64_t *Ap,
                         const int64_t *Ai);
-
-    // ---- lane placement of the general rows (place(), once, after the kernel shape is chosen)
-    // Table slot g of gen_row / gen_col / gen_pos is the kernel's row slot g / NL of lane g mod NL.
-    // place() spreads the mgd rows over `slots` table slots (gen_row -1: an empty slot) so that
-    // the products writes (ds_write_b64: 16-lane groups, bank = address mod 16 in doubles) and the
-    // x-exchange reads (32-lane groups, address mod 32) of every entry column e hit distinct banks.
-    // Each column keeps its entries' products slots in row order (the gather sums) and the
-    // factorisation program its term order (renumbered to the slots), so the arithmetic is unchanged.
-    int32_t mgd = 0;                  // general rows
-    std::vector<int32_t> gen_dst;     // [4 mg] products slot per entry (absent: a discard slot)
-    int32_t place_conflicts[2] = {0, 0}, place_iters = 0;  // modelled extra LDS cycles per pass: writes, reads
-    // slots: NL GS of the shape to spread over, or mgd (the dense order); stride / hsp / T1r: its
-    // products layout (mpc_wave.hpp WaveLds); pz: the products region's size for mg = slots (16
-    // discard slots follow it); nmax: the x exchange's length (32 zero slots follow it).  An absent
-    // entry's gen_col is -1 - k: it reads the zero at nmax + k.
-    void place(int slots, int T1r, int stride, int hsp, int pz, int nmax);
 };
 
 constexpr int kStageDests = 13 * 13 + 8 * 13;  // M_kk (13x13) + coupling B_k (8x13)

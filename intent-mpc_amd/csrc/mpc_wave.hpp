@@ -50,13 +50,6 @@ namespace impc {
 
 #define IMPC_WF __host__ __device__ __forceinline__
 
-// Round-6 A/B switches (tools only; the product builds them on)
-#ifndef IMPC_R6_REFAIL
-#define IMPC_R6_REFAIL 1
-#endif
-#ifndef IMPC_R6_PERSIST
-#define IMPC_R6_PERSIST 1
-#endif
 // Phase-cost experiments (tools/exp.sh only): IMPC_DUP=<section id> runs that idempotent phase of
 // the ADMM iteration twice; the bench's time difference is the phase's marginal cost.
 #ifndef IMPC_DUP
@@ -134,10 +127,7 @@ namespace impc {
 struct WaveTables {
     int32_t n, m, mg, N, W, CG, nnzP, nnzA;
     const int32_t *var_orig, *var_pdiag, *var_boxrow, *var_boxpos;
-    // general rows: table slot g is the kernel's row slot g / NL of lane g mod NL (gen_row -1: an
-    // empty slot), the rows spread over the lanes by MpcStructure::place; gen_dst [4 mg]: each
-    // entry's products slot (-1 absent); the factorisation program indexes the table slots
-    const int32_t *gen_row, *gen_col, *gen_pos, *gen_dst, *term_ptr, *term;
+    const int32_t *gen_row, *gen_col, *gen_pos, *colg, *term_ptr, *term;
     int32_t HS;               // heavy columns (second products tier), MpcStructure::HS; 0: one tier
     const int32_t *col_hid;   // [n] heavy-column index or -1 (stage order)
     int32_t T1r;              // first-tier rows: cg4(CG) (one tier) or kProdTier1 (two tiers)
@@ -228,12 +218,12 @@ struct WaveLds {
     static constexpr int X_OFF = E_OFF + NP;                // xbuf
     static constexpr int RED_OFF = X_OFF + NP;              // team reduction scratch [kRedLen]
     static constexpr int JUNK_OFF = RED_OFF + kRedLen;      // per-lane discard slots [NL]
+    static constexpr int GSLOT_OFF = JUNK_OFF + NL;         // int16 [4 NL GS]: general entry -> product slot
     // One-variable-per-lane shape: the Ruiz scaling vectors D, E and the ADMM deltas of the
     // termination checks live here (the long-horizon shape keeps them in HBM / registers: its LDS
     // is full).  Layout of each: [var slots NMAX][box rows NMAX][general slots NL GS].
     static constexpr bool ONCHIP = VS == 1;
     static constexpr int VEC_N = 2 * NMAX + NL * GS;
-    static constexpr int GSLOT_OFF = JUNK_OFF + NL;         // int16 [4 NL GS]: general entry -> product slot
     static constexpr int SCL_OFF = GSLOT_OFF + NL * GS;           // D, E (scaling)
     static constexpr int DLT_OFF = SCL_OFF + (ONCHIP ? VEC_N : 0);  // dx, dy (check iterations)
     static constexpr int P_OFF = DLT_OFF + (ONCHIP ? VEC_N : 0);  // products, column-slot layout (size below)
@@ -246,7 +236,7 @@ struct WaveLds {
     // product per obstacle row, so the second tier is (CG4 - 4) rows of the HS heavy columns
     // instead of CG4 rows of all n (K = 21: 21 KB instead of 49 KB).  It doubles as the
     // factorisation's (4g + e) scratch and general-row rho.  Sized from the pattern at run time,
-    // followed by kDiscard discard slots (index p_size).
+    // followed by 8 discard slots (index p_size).
     static constexpr int T1 = kProdTier1;
     static IMPC_WF int cg4(int CG) { return (CG + 3) & ~3; }
     // +PAD: the obstacle rows of one stage write their products to the same column in different
@@ -260,16 +250,10 @@ struct WaveLds {
         return c > f ? c : f;
     }
     static IMPC_WF int p_size(const WaveTables &T) { return p_size(T.CG, T.n, T.HS, T.mg, T.T1r); }
-    // discard slots after the products region: an absent entry's zero product lands on one whose
-    // bank no present entry of its 16-lane write group uses (MpcStructure::place)
-    static constexpr int kDiscard = 16;
-    // the entry addresses of a lane L past the tables (a dense-order batch's row slots >= mg):
-    // products discard slot p_size + (L mod 16), x exchange zero NMAX + (L mod 32)
-    static IMPC_WF int pad_lds(int pz, int L) { return ((pz + (L & 15)) << 16) | (NMAX + (L & 31)); }
     // the chunk operators' region of the one-slot shape (IMPC_CHUNK19), after the products
     static constexpr int CHX = (VS == 1 && IMPC_CHUNK19) ? 448 : 0;
-    static IMPC_WF int ch_off(const WaveTables &T) { return P_OFF + p_size(T) + kDiscard; }
-    static IMPC_WF int size(const WaveTables &T) { return P_OFF + p_size(T) + kDiscard + CHX; }
+    static IMPC_WF int ch_off(const WaveTables &T) { return P_OFF + p_size(T) + 8; }
+    static IMPC_WF int size(const WaveTables &T) { return P_OFF + p_size(T) + 8 + CHX; }
     // factorisation aliases (inside R..X region and the products buffer)
     static constexpr int FA = R_OFF, FL = FA + 169, FI = FL + 169, FB = FI + 169, FG = FB + 104, FE = FG + 104,
                          DIAGX = FE + 64;
@@ -478,24 +462,23 @@ struct WaveQP {
         }
         _Pragma("unroll") for (int s = 0; s < GS; s++) {
             int g = NL * s + L;
-            const bool tab = g < T.mg;
-            gok[s] = tab && T.gen_row[g] >= 0;
+            gok[s] = g < T.mg;
             z[s] = y[s] = lg[s] = ug[s] = dyg_[s] = 0.0;
             gt[s] = 0;
             const int16_t *gs = (const int16_t *)(lds + LD::GSLOT_OFF);
             const int pz = LD::p_size(T);
             _Pragma("unroll") for (int e = 0; e < 4; e++) {
                 a[s][e] = 0.0;
-                gc[s][e] = LD::pad_lds(pz, L);  // past the tables: discard slot / zero tail
-            }
-            if (tab) {  // an absent entry (gen_col = -1 - k): its discard slot, the zero at NMAX + k
-                _Pragma("unroll") for (int e = 0; e < 4; e++) {
-                    int col = T.gen_col[4 * g + e], pos = T.gen_pos[4 * g + e];
-                    gc[s][e] = ((int)gs[4 * g + e] << 16) | (col >= 0 ? col : LD::NMAX - 1 - col);
-                    if (col >= 0) a[s][e] = Aval(pos);
-                }
+                gc[s][e] = (pz << 16) | LD::NMAX;  // discard slot / zero tail of the x exchange
             }
             if (gok[s]) {
+                _Pragma("unroll") for (int e = 0; e < 4; e++) {
+                    int col = T.gen_col[4 * g + e], pos = T.gen_pos[4 * g + e];
+                    if (col >= 0) {
+                        gc[s][e] = ((int)gs[4 * g + e] << 16) | col;
+                        a[s][e] = Aval(pos);
+                    }
+                }
                 int row = T.gen_row[g];
                 lg[s] = dmin(dmax(io.l[bm + row], -kInf), kInf);
                 ug[s] = dmin(dmax(io.u[bm + row], -kInf), kInf);
@@ -507,19 +490,28 @@ struct WaveQP {
         }
     }
 
-    // Per-workgroup tables (once per launch and batch): the product slot of every general-row
-    // entry (gen_dst, int16 in LDS) and a zeroed products region (slots no entry maps to must read 0).
+    // Per-workgroup tables (once per launch): the product slot of every general-row entry
+    // (mpc_structure colg inverted into the column-slot layout, int16 in LDS; padded entries get
+    // the discard slot), and a zeroed products region (slots no entry maps to must read 0).
     static IMPC_WF void load_tables(WV &w, const WaveTables &T, double *lds) {
         int16_t *gs = (int16_t *)(lds + LD::GSLOT_OFF);
+        const int pz = LD::p_size(T);
+        for (int e = w.lane(); e < 4 * NL * GS; e += NL) gs[e] = (int16_t)pz;
         double *pb = lds + LD::P_OFF;
-        for (int e = w.lane(); e < LD::p_size(T) + LD::kDiscard; e += NL) pb[e] = 0.0;
-        for (int e = w.lane(); e < 4 * T.mg; e += NL) gs[e] = (int16_t)T.gen_dst[e];
+        for (int e = w.lane(); e < pz + 8; e += NL) pb[e] = 0.0;
+        w.sync();
+        for (int e = w.lane(); e < T.n * T.CG; e += NL) {
+            const int v = e / T.CG, t = e % T.CG, id = T.colg[e];
+            if (id >= 0)
+                gs[id] = (int16_t)(t < T.T1r ? t * LD::stride(T.n) + v
+                                             : T.T1r * LD::stride(T.n) + (t - T.T1r) * LD::hsp(T.HS) + T.col_hid[v]);
+        }
         w.sync();
     }
 
     IMPC_WF void zero_products() {
         double *pb = pbuf();
-        const int cnt = LD::p_size(T) + LD::kDiscard;
+        const int cnt = LD::p_size(T) + 8;
         for (int i = L; i < cnt; i += NL) pb[i] = 0.0;
         wv.sync();
     }
@@ -1840,6 +1832,26 @@ struct WaveQP {
     // The scaling vectors D, E live in the per-QP global scratch (written by scale()) and are
     // reloaded only where OSQP needs them (warm start, termination checks, unscaling), so they do
     // not occupy registers across the ADMM loop.
+    // the persistent workspace (WaveIO::persist) from the registers: rho and the scaled iterates
+    IMPC_WF void write_persist(double *ps) {
+        const int n = T.n;
+        double *it = ps + kPersistHdr;
+        if (L == 0) ps[kPersistHdr - 1] = R.rho;
+        _Pragma("unroll") for (int s = 0; s < VS; s++)
+            if (vok[s]) {
+                const int v = NL * s + L;
+                it[v] = x[s];
+                it[n + v] = zb[s];
+                it[2 * n + v] = yb[s];
+            }
+        _Pragma("unroll") for (int s = 0; s < GS; s++)
+            if (gok[s]) {
+                const int g = NL * s + L;
+                it[3 * n + g] = z[s];
+                it[3 * n + T.mg + g] = y[s];
+            }
+    }
+
     IMPC_WF void solve(int64_t b) {
         const int n = T.n, m = T.m;
         // time_limit clock: from the start of the QP's setup (load, scaling, factorisation), as
@@ -1900,17 +1912,11 @@ struct WaveQP {
                 out->rho_estimate = R.rho;
             }
             // a first setup that fails its factorisation leaves a defined workspace: the settings'
-            // rho and zero iterates (osqp_setup's cold_start), so a resume after a matrix update
-            // (impc_batch_update_matrices) starts as a fresh setup would; a failed resume keeps the
-            // workspace it had (OSQP keeps work->x, z, y when osqp_update_P / _A fails to refactor)
-            if (IMPC_R6_PERSIST && ps && io.resume == 0) {
-                double *it = ps + kPersistHdr;
-                if (L == 0) ps[kPersistHdr - 1] = R.rho;
-                _Pragma("unroll") for (int s = 0; s < VS; s++)
-                    if (vok[s]) it[NL * s + L] = it[n + NL * s + L] = it[2 * n + NL * s + L] = 0.0;
-                _Pragma("unroll") for (int s = 0; s < GS; s++)
-                    if (gok[s]) it[3 * n + NL * s + L] = it[3 * n + T.mg + NL * s + L] = 0.0;
-            }
+            // rho and zero iterates (osqp_setup's cold_start; load() zeroed them), so a resume after a
+            // matrix update (impc_batch_update_matrices) starts as a fresh setup would; a failed
+            // resume keeps the workspace it had (OSQP keeps work->x, z, y when osqp_update_P / _A
+            // fails to refactor)
+            if (ps && io.resume == 0) write_persist(ps);
             wv.sync();
             return;
         }
@@ -1991,14 +1997,10 @@ struct WaveQP {
         for (;;) {
             if (refac) {
                 refac = false;
-#if IMPC_R6_REFAIL
                 if (factorize()) {  // osqp_solve: a failed rho update ends the solve with exitflag 1
                     refail = true;
                     break;
                 }
-#else
-                factorize();
-#endif
                 write_v_products();
                 IMPC_SEC(kSecFactor);
             }
@@ -2078,21 +2080,7 @@ struct WaveQP {
             // OSQP 0.6.2 jumps to exit: no termination check, no stored solution (the outputs keep
             // the previous solve's), status stays UNSOLVED, info.iter is the last update_info's;
             // the workspace keeps the new rho and its iterates as they are
-            if (ps) {
-                double *it = ps + kPersistHdr;
-                if (L == 0) ps[kPersistHdr - 1] = R.rho;
-                _Pragma("unroll") for (int s = 0; s < VS; s++)
-                    if (vok[s]) {
-                        it[NL * s + L] = x[s];
-                        it[n + NL * s + L] = zb[s];
-                        it[2 * n + NL * s + L] = yb[s];
-                    }
-                _Pragma("unroll") for (int s = 0; s < GS; s++)
-                    if (gok[s]) {
-                        it[3 * n + NL * s + L] = z[s];
-                        it[3 * n + T.mg + NL * s + L] = y[s];
-                    }
-            }
+            if (ps) write_persist(ps);
             if (L == 0) {
                 out->iter = info_iter;
                 out->status_val = IMPC_UNSOLVED;
@@ -2130,35 +2118,6 @@ struct WaveQP {
         const bool has_sol2 = status != IMPC_PRIMAL_INFEASIBLE && status != IMPC_PRIMAL_INFEASIBLE_INACCURATE &&
                               status != IMPC_DUAL_INFEASIBLE && status != IMPC_DUAL_INFEASIBLE_INACCURATE &&
                               status != IMPC_NON_CVX;
-        if (ps) {  // the workspace after osqp_solve: rho and the scaled iterates -- zero when the
-                   // solve ended without a solution (store_solution's cold_start, auxil.c)
-            double *it = ps + kPersistHdr;
-            if (L == 0) ps[kPersistHdr - 1] = R.rho;
-            _Pragma("unroll") for (int s = 0; s < VS; s++) {
-                if (!vok[s]) continue;
-                const int v = NL * s + L;
-#if IMPC_R6_PERSIST
-                it[v] = has_sol2 ? x[s] : 0.0;
-                it[n + v] = has_sol2 ? zb[s] : 0.0;
-                it[2 * n + v] = has_sol2 ? yb[s] : 0.0;
-#else
-                it[v] = x[s];
-                it[n + v] = zb[s];
-                it[2 * n + v] = yb[s];
-#endif
-            }
-            _Pragma("unroll") for (int s = 0; s < GS; s++) {
-                if (!gok[s]) continue;
-                const int g = NL * s + L;
-#if IMPC_R6_PERSIST
-                it[3 * n + g] = has_sol2 ? z[s] : 0.0;
-                it[3 * n + T.mg + g] = has_sol2 ? y[s] : 0.0;
-#else
-                it[3 * n + g] = z[s];
-                it[3 * n + T.mg + g] = y[s];
-#endif
-            }
-        }
         const bool scaled = st.scaling > 0;
         _Pragma("unroll") for (int s = 0; s < VS; s++) {
             if (!vok[s]) continue;
@@ -2171,6 +2130,14 @@ struct WaveQP {
             if (!gok[s]) continue;
             double yv = has_sol2 ? (scaled ? (Eg[s] * y[s]) * cinv : y[s]) : kNan;
             io.yo[b * m + T.gen_row[NL * s + L]] = yv;
+        }
+        if (ps) {  // the workspace after osqp_solve: rho and the scaled iterates -- zero when the
+                   // solve ended without a solution (store_solution's cold_start, auxil.c)
+            if (!has_sol2) {
+                _Pragma("unroll") for (int s = 0; s < VS; s++) x[s] = zb[s] = yb[s] = 0.0;
+                _Pragma("unroll") for (int s = 0; s < GS; s++) z[s] = y[s] = 0.0;
+            }
+            write_persist(ps);
         }
         if (L == 0 && io.qpt) {
             io.qpt[2 * b] = t0;

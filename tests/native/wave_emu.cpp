@@ -7,7 +7,6 @@
 #include <algorithm>
 #include <barrier>
 #include <utility>
-#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <limits>
@@ -147,37 +146,32 @@ void run(const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSetti
         tier ? run_w<VS, GS, 0, true>(T, io, st) : run_w<VS, GS, 0, false>(T, io, st);
 }
 
-// the product's shapes for the team size (impc_qp.hip kWaveVS / kWaveVSLong / kGsMax): variable
-// and general-row slots per lane, or false
-bool shape_of(const impc::MpcStructure &ms, int &vs, int &gs) {
-    if (NL == 64) {  // one QP per wavefront: four variable slots, up to six general-row slots
-        if (ms.n > 4 * NL || ms.mg > 6 * NL) return false;
-        vs = 4;
-        gs = std::max(2, (ms.mg + NL - 1) / NL);
-    } else {
-        if (ms.n > 3 * NL || ms.mg > 4 * NL) return false;
-        gs = ms.mg <= 2 * NL ? 2 : ms.mg <= 3 * NL ? 3 : 4;
-        vs = ms.n <= NL ? 1 : 3;
-    }
-    return true;
-}
-
-void dispatch(int vs, int gs, const impc::WaveTables &T, const impc::WaveIO &io, const impc::DevSettings &st) {
-    if constexpr (NL == 64) {
+// the product's shapes for the team size (impc_qp.hip kWaveVS / kWaveVSLong / kGsMax)
+template <int N>
+int dispatch(const impc::MpcStructure &ms, const impc::WaveTables &T, const impc::WaveIO &io,
+             const impc::DevSettings &st) {
+    if constexpr (N == 64) {  // one QP per wavefront: four variable slots, up to six general-row slots
+        if (ms.n > 4 * N || ms.mg > 6 * N) return 2;
+        const int gs = std::max(2, (ms.mg + N - 1) / N);
         if (gs == 2) run<4, 2>(T, io, st);
         else if (gs == 3) run<4, 3>(T, io, st);
         else if (gs == 4) run<4, 4>(T, io, st);
         else if (gs == 5) run<4, 5>(T, io, st);
         else run<4, 6>(T, io, st);
-    } else if (vs == 1) {
-        if (gs == 2) run<1, 2>(T, io, st);
-        else if (gs == 3) run<1, 3>(T, io, st);
-        else run<1, 4>(T, io, st);
     } else {
-        if (gs == 2) run<3, 2>(T, io, st);
-        else if (gs == 3) run<3, 3>(T, io, st);
-        else run<3, 4>(T, io, st);
+        if (ms.n > 3 * N || ms.mg > 4 * N) return 2;
+        const int gs = ms.mg <= 2 * N ? 2 : ms.mg <= 3 * N ? 3 : 4;
+        if (ms.n <= N) {
+            if (gs == 2) run<1, 2>(T, io, st);
+            else if (gs == 3) run<1, 3>(T, io, st);
+            else run<1, 4>(T, io, st);
+        } else {
+            if (gs == 2) run<3, 2>(T, io, st);
+            else if (gs == 3) run<3, 3>(T, io, st);
+            else run<3, 4>(T, io, st);
+        }
     }
+    return 0;
 }
 
 }  // namespace
@@ -188,21 +182,13 @@ extern "C" int emu_wave_solve_batch(int64_t n, int64_t m, const int64_t *Pp, con
                                     const double *yws, double *xo, double *yo, impc_info *info) {
     impc::MpcStructure ms;
     if (!ms.analyse(n, m, Pp, Pi, Ap, Ai).empty()) return 1;
-    if (ms.CG > impc::WaveLds<NL, 1, 2>::CGM) return 2;
-    int vs = 0, gs = 0;
-    if (!shape_of(ms, vs, gs)) return 2;
-    // the emulation takes the two-tier products layout whenever the pattern has heavy columns (the
-    // product uses it where one tier would cost occupancy), so both gathers are covered on the CPU
-    using LD0 = impc::WaveLds<NL, 1, 2>;
-    const int T1r = ms.HS == 0 ? LD0::cg4(ms.CG) : impc::kProdTier1;
-    // the product's lane placement of the general rows (EMU_ROW_PLACE=0: the dense order)
-    const char *pe = std::getenv("EMU_ROW_PLACE");
-    const int slots = (pe && pe[0] == '0') ? ms.mg : NL * gs;
-    ms.place(slots, T1r, LD0::stride(ms.n), LD0::hsp(ms.HS), LD0::p_size(ms.CG, ms.n, ms.HS, slots, T1r), NL * vs);
     impc::WaveTables T{ms.n, ms.m, ms.mg, ms.N, ms.W, ms.CG, ms.nnzP, ms.nnzA,
                        ms.var_orig.data(), ms.var_pdiag.data(), ms.var_boxrow.data(), ms.var_boxpos.data(),
-                       ms.gen_row.data(), ms.gen_col.data(), ms.gen_pos.data(), ms.gen_dst.data(),
-                       ms.term_ptr.data(), ms.term.data(), ms.HS, ms.col_hid.data(), T1r};
+                       ms.gen_row.data(), ms.gen_col.data(), ms.gen_pos.data(), ms.colg.data(),
+                       ms.term_ptr.data(), ms.term.data(), ms.HS, ms.col_hid.data(), impc::kProdTier1};
+    // the emulation takes the two-tier products layout whenever the pattern has heavy columns (the
+    // product uses it where one tier would cost occupancy), so both gathers are covered on the CPU
+    if (ms.HS == 0) T.T1r = impc::WaveLds<NL, 1, 2>::cg4(ms.CG);
     // per-QP scratch of the scaling vectors (shapes without them in LDS)
     std::vector<double> zx((size_t)B * n, 0.0), zy((size_t)B * m, 0.0), scal((size_t)B * (2 * n + ms.mg), 0.0);
     impc::WaveIO io{B, Px, q, Ax, l, u, xws ? xws : zx.data(), yws ? yws : zy.data(), xws ? 1 : 0,
@@ -225,6 +211,6 @@ extern "C" int emu_wave_solve_batch(int64_t n, int64_t m, const int64_t *Pp, con
     st.scaled_termination = (int32_t)s->scaled_termination;
     st.check_termination = (int32_t)s->check_termination;
     st.warm_start = (int32_t)s->warm_start;
-    dispatch(vs, gs, T, io, st);
-    return 0;
+    if (ms.CG > impc::WaveLds<NL, 1, 2>::CGM) return 2;
+    return dispatch<NL>(ms, T, io, st);
 }

@@ -28,5 +28,16 @@ case "$1" in
       || { tail -30 $O/bench_config5.json.log; exit 1; }
     tail -1 $O/bench_config5.json.log > $O/bench_config5.json
     ;;
+  meas)  # replan / live-loop measurements of the final build and the NON_CVX trace
+    timeout -k 10 600 python -u tools/trace_noncvx.py > $O/noncvx_trace.json 2> $O/noncvx_trace.err || { tail -30 $O/noncvx_trace.err; exit 1; }
+    for I in 8192 16 1; do
+      R=5; [ $I -lt 100 ] && R=30
+      timeout -k 10 300 python -u tools/replan_bench.py --instances $I --reps $R > $O/replan_full_call_I$I.json 2> $O/replan_I$I.err || { tail -30 $O/replan_I$I.err; exit 1; }
+      ( cd ab_r05 && timeout -k 10 300 python -u tools/replan_bench.py --instances $I --reps $R ) > $O/replan_full_call_I${I}_r05.json 2> $O/replan_I${I}_r05.err || { tail -30 $O/replan_I${I}_r05.err; exit 1; }
+    done
+    timeout -k 10 600 python -u tools/live_loop.py > $O/live_loop.json 2> $O/live_loop.err || { tail -30 $O/live_loop.err; exit 1; }
+    timeout -k 10 600 python -u tools/live_loop.py --mixed-k --obstacles 8 > $O/live_loop_mixed_k.json 2> $O/live_loop_mixed.err || { tail -30 $O/live_loop_mixed.err; exit 1; }
+    tail -n 1 $O/*.json
+    ;;
   *) echo "unknown phase $1"; exit 2 ;;
 esac
