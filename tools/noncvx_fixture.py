@@ -20,6 +20,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dump", nargs="?", default=os.path.join(ROOT, "gpurun_out", "r06", "noncvx.npz"))
     ap.add_argument("--keep", type=int, default=8)
+    ap.add_argument("--codes", default="0,4", help="candidate slots kept in the fixture (0-3 one intent, 4-5 two)")
+    ap.add_argument("--groups", type=int, default=3, help="distinct (replan, instance) groups kept")
     ap.add_argument("--out", default=os.path.join(ROOT, "tests", "golden", "noncvx_live.npz"))
     a = ap.parse_args()
     d = np.load(a.dump)
@@ -28,6 +30,8 @@ def main():
     s = impc.default_settings(verbose=0)
     so = ora.settings_from(s)
     rows, keep = [], {}
+    codes = {int(c) for c in a.codes.split(",")}
+    groups = []
     seen = {}
     for j in range(d["inst"].shape[0]):
         K = int(d["K"][j])
@@ -44,7 +48,10 @@ def main():
                              pri_res=float(io["pri_res"][0]), dua_res=float(io["dua_res"][0]),
                              rho_updates=int(io["rho_updates"][0])))
         rows.append(r)
-        if len(keep.get("inst", [])) < a.keep:
+        grp = (r["replan"], r["inst"])
+        if grp not in groups and len(groups) < a.groups:
+            groups.append(grp)
+        if len(keep.get("inst", [])) < a.keep and grp in groups and r["code"] in codes:
             for key, val in (("K", K), ("replan", r["replan"]), ("inst", r["inst"]), ("code", r["code"]),
                              ("status", r["device"]["status"]), ("iter", r["device"]["iter"]),
                              ("oracle_status", r["oracle"]["status"]), ("oracle_iter", r["oracle"]["iter"])):

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--horizon", type=int, default=30)
     ap.add_argument("--max-dump", type=int, default=64)
     ap.add_argument("--out", default=os.path.join("gpurun_out", "r06", "noncvx.npz"))
+    ap.add_argument("--watch", default="", help="instances (comma-separated) whose every replan is logged: "
+                    "branch, chosen candidate, each candidate's status / iterations / max |x|, max |plan| after")
     a = ap.parse_args()
     I, K, R, N = a.instances, a.obstacles, a.replans, a.horizon
     sc = scenarios.live_loop(I, K, R, N=N, seed=4100)
@@ -42,6 +44,8 @@ def main():
     dump = {k: [] for k in ("replan", "inst", "code", "K", "Px", "q", "Ax", "l", "u", "x_ws", "status", "iter",
                             "setup_exitflag", "pri_res", "dua_res", "rho_updates")}
     per_replan = []
+    watch = [int(v) for v in a.watch.split(",") if v]
+    log = []
     for r in range(R):
         plan_x, first, _, _ = rp.plans()  # the warm starts of this replan
         paths.xref_device(pos_d.ptr, xref_d.ptr)
@@ -70,6 +74,18 @@ def main():
                                ("pri_res", "pri_res"), ("dua_res", "dua_res"), ("rho_updates", "rho_updates")):
                     dump[key].append(inf[f])
         per_replan.append(int(n_bad))
+        if watch:
+            plan_after, _, _, valid = rp.plans()
+            for i in watch:
+                cands = []
+                for k, sh in out["shapes"].items():
+                    for row in np.flatnonzero(sh["row_inst"] == i):
+                        inf = sh["info"][row]
+                        cands.append(dict(k=int(k), code=int(sh["row_code"][row]), status=int(inf["status_val"]),
+                                          iter=int(inf["iter"]), max_abs_x=float(np.abs(sh["x"][row]).max())))
+                log.append(dict(replan=r, inst=i, branch=int(out["branch"][i]), best=int(out["best_cand"][i]),
+                                valid=int(valid[i]), max_abs_plan=float(np.abs(plan_after[i]).max()),
+                                cands=sorted(cands, key=lambda c: c["code"])))
         rp.advance_device(pd["ts"], pos_d.ptr, vel_d.ptr)
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     arrays = {}
@@ -82,6 +98,9 @@ def main():
         else:
             arrays[k] = np.array(v)
     np.savez(a.out, N=N, **arrays)
+    if watch:
+        with open(os.path.splitext(a.out)[0] + "_watch.json", "w") as f:
+            json.dump(log, f, indent=0)
     print(json.dumps({"instances": I, "replans": R, "noncvx_per_replan": per_replan, "dumped": len(dump["inst"]),
                       "out": a.out, "build_id": impc.lib.impc_build_id().decode()}), flush=True)
     for d in (pos_d, vel_d, xref_d, psize_d, prob_d, pred_d, cur_d):
