@@ -10,7 +10,8 @@
  *                                               impc_settings (OSQPSettings mirror)
  *   OsqpEigen::Data      (Data.hpp:44-151)      setNumberOf*, setHessianMatrix (upper triangle,
  *                                               Data.tpp:38), setGradient, setLinearConstraints-
- *                                               Matrix, setLower/UpperBound
+ *                                               Matrix, setLower/UpperBound, getGradient,
+ *                                               getData (OSQP's OSQPData view)
  *   OsqpEigen::Solver    (Solver.hpp:87-249)    initSolver, setWarmStart, solveProblem, getStatus,
  *                                               getSolution, getDualSolution, clearSolver,
  *                                               clearSolverVariables, updateGradient /
@@ -57,6 +58,32 @@
 #include <vector>
 
 #include "../impc_qp.h"
+
+/* OSQP 0.6.2's public data types (osqp/include/types.h, glob_opts.h with DLONG / no DFLOAT), the
+ * return type of Data::getData(); skipped when the real osqp.h came first. */
+#ifndef OSQP_TYPES_H
+typedef long long c_int;
+typedef double c_float;
+typedef struct {
+    c_int nzmax;
+    c_int m;
+    c_int n;
+    c_int *p;
+    c_int *i;
+    c_float *x;
+    c_int nz;
+} csc;
+typedef struct {
+    c_int n;
+    c_int m;
+    csc *P;
+    csc *A;
+    c_float *q;
+    c_float *l;
+    c_float *u;
+} OSQPData;
+#endif
+static_assert(sizeof(c_int) == sizeof(int64_t), "OSQPData views the shim's int64 index arrays");
 
 namespace OsqpEigen {
 
@@ -188,10 +215,15 @@ public:
 };
 
 /* Data.hpp:44-151: same member names and argument types (setGradient / set*Bound take
- * Eigen::Ref<VectorXd> by value, the matrices an Eigen::SparseCompressedBase). */
+ * Eigen::Ref<VectorXd> by value, the matrices an Eigen::SparseCompressedBase).  getData() returns
+ * OSQP 0.6.2's public OSQPData (the types below, osqp/include/types.h with DLONG: c_int = long
+ * long) viewing this object's arrays: P upper triangular CSC, A CSC, q, l, u. */
 class Data {
     int64_t m_n = 0, m_m = 0;
     bool m_hasP = false, m_hasA = false, m_hasq = false, m_hasl = false, m_hasu = false;
+    ::csc m_P{}, m_A{};
+    ::OSQPData m_view{};
+    ::OSQPData *m_viewp = &m_view;
 
 public:
     std::vector<int64_t> Pp, Pi, Ap, Ai;
@@ -243,6 +275,38 @@ public:
         return setLowerBound(lowerBound) && setUpperBound(upperBound);
     }
     bool isSet() const { return m_n > 0 && m_hasP && m_hasA && m_hasq && m_hasl && m_hasu; }
+    // Data.hpp:99 -- the gradient as a vector (a copy)
+    Eigen::Matrix<double, Eigen::Dynamic, 1> getGradient() {
+        Eigen::Matrix<double, Eigen::Dynamic, 1> g;
+        g.setZero(m_n);
+        for (int64_t i = 0; i < (int64_t)q.size() && i < m_n; i++) g(i) = q[i];
+        return g;
+    }
+    // Data.hpp:145 -- the problem data in OSQP's struct, pointing into this object (valid until the
+    // next set* / clear* call); a matrix not set yet has nullptr arrays
+    ::OSQPData *const &getData() const {
+        auto *self = const_cast<Data *>(this);
+        auto fill = [](::csc &c, int64_t rows, int64_t cols, std::vector<int64_t> &p, std::vector<int64_t> &i,
+                       std::vector<double> &x) {
+            c.m = (c_int)rows;
+            c.n = (c_int)cols;
+            c.nzmax = (c_int)x.size();
+            c.p = p.empty() ? nullptr : (c_int *)p.data();
+            c.i = i.empty() ? nullptr : (c_int *)i.data();
+            c.x = x.empty() ? nullptr : x.data();
+            c.nz = -1;  // compressed column form
+        };
+        fill(self->m_P, m_n, m_n, self->Pp, self->Pi, self->Px);
+        fill(self->m_A, m_m, m_n, self->Ap, self->Ai, self->Ax);
+        self->m_view.n = (c_int)m_n;
+        self->m_view.m = (c_int)m_m;
+        self->m_view.P = m_hasP ? &self->m_P : nullptr;
+        self->m_view.A = m_hasA ? &self->m_A : nullptr;
+        self->m_view.q = m_hasq ? self->q.data() : nullptr;
+        self->m_view.l = m_hasl ? self->l.data() : nullptr;
+        self->m_view.u = m_hasu ? self->u.data() : nullptr;
+        return m_viewp;
+    }
 };
 
 /* Solver.hpp:87-249: same member names and signatures (Solver.hpp:196-231 templates included). */

@@ -366,6 +366,15 @@ int main(int argc, char **argv) {
     CHECK(d.Pi.size() == 3 && d.Pi[0] == 0 && d.Pi[1] == 0 && d.Pi[2] == 1);
     CHECK(d.Px.size() == 3 && d.Px[0] == 4.0 && d.Px[1] == 1.0 && d.Px[2] == 2.0);
     CHECK(d.Ap.size() == 3 && d.Ap[2] == 4 && d.Ai[0] == 0 && d.Ai[1] == 1 && d.Ai[2] == 0 && d.Ai[3] == 2);
+    // Data.hpp:99 / :145 accessors: the gradient, and OSQP's OSQPData view of the stored problem
+    CHECK(solver.data()->getGradient().size() == 2 && solver.data()->getGradient()(1) == 1.0);
+    {
+        OSQPData *const &od = solver.data()->getData();
+        CHECK(od && od->n == 2 && od->m == 3 && od->P && od->A && od->q && od->l && od->u);
+        CHECK(od->P->n == 2 && od->P->nzmax == 3 && od->P->p[2] == 3 && od->P->i[2] == 1 && od->P->x[2] == 2.0);
+        CHECK(od->A->m == 3 && od->A->p[2] == 4 && od->A->i[3] == 2 && od->A->nz == -1);
+        CHECK(od->q[0] == 1.0 && od->l[0] == 1.0 && od->u[1] == 0.7);
+    }
     // size errors are reported, not accepted
     Eigen::VectorXd bad(5);
     CHECK(!solver.data()->setGradient(bad));
