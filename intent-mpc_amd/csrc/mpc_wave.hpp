@@ -264,6 +264,10 @@ struct WaveLds {
     static_assert(VS != 3 || FB2 + 104 <= RED_OFF, "factorisation scratch does not fit");
 };
 
+// the status register's mark of a failed refactorisation inside the iteration loop (never a
+// reported status: the exit path writes UNSOLVED)
+constexpr int64_t kRefailMark = -1000;
+
 struct WaveRho {
     double rho, r_eq, r_ineq, r_loose, i_eq, i_ineq, i_loose;
     IMPC_WF void set(double r) {
@@ -1984,7 +1988,8 @@ struct WaveQP {
         // the loop's settings read once into registers (the batch's settings live in global memory
         // for a grouped launch: read in the loop they cost a scalar-memory round trip each
         // iteration, after every barrier)
-        const int32_t max_iter = st.max_iter, rho_int = st.adaptive_rho ? st.rho_interval : 0;
+        int32_t max_iter = st.max_iter;  // (dropped to 0 by a failed refactorisation, below)
+        const int32_t rho_int = st.adaptive_rho ? st.rho_interval : 0;
         // team-uniform, in scalar registers (io.tlim: the QP's own limit)
         const double tl = wv.uniform(io.tlim ? io.tlim[b] : st.time_limit), tick = st.tick_s;
         const bool tlim = tl > 0;
@@ -1992,14 +1997,18 @@ struct WaveQP {
         // The refactorisation after an adaptive-rho update runs between two passes of the inner
         // iteration loop rather than inside it: the register allocator then places the spills the
         // factorisation's temporaries force around that (rare) call, outside the hot loop.
-        bool refac = false, refail = false;
+        bool refac = false;
         iter = 1;
         for (;;) {
             if (refac) {
                 refac = false;
-                if (factorize()) {  // osqp_solve: a failed rho update ends the solve with exitflag 1
-                    refail = true;
-                    break;
+                // osqp_solve: a failed rho update ends the solve with exitflag 1.  It leaves the loop
+                // through the loop's one exit -- the pass bound drops to 0, the status register
+                // carries the mark -- so no second exit edge (and its live values) burdens the
+                // register allocation of the passes (round 6: 217.5 -> 213.9 ms per config-3 launch)
+                if (factorize()) {
+                    max_iter = 0;
+                    status = kRefailMark;
                 }
                 write_v_products();
                 IMPC_SEC(kSecFactor);
@@ -2076,7 +2085,7 @@ struct WaveQP {
             }
             iter++;  // this iteration is complete; the next pass starts at the next one
         }
-        if (refail) {
+        if (status == kRefailMark) {
             // OSQP 0.6.2 jumps to exit: no termination check, no stored solution (the outputs keep
             // the previous solve's), status stays UNSOLVED, info.iter is the last update_info's;
             // the workspace keeps the new rho and its iterates as they are
