@@ -44,7 +44,7 @@ case "$1" in
     cd /tmp || exit 1
     A3="--steps 1 --warmup 0 --cpu-sample 0 --e2e-steps 0"
     A5="--workload config5 --steps 1 --warmup 10 --receding-replay 0 --cpu-sample 0 --e2e-steps 0"
-    AL="--workload live --steps 1 --warmup 0 --cpu-sample 0 --e2e-steps 0"
+    Al="--workload live --steps 1 --warmup 0 --cpu-sample 0 --e2e-steps 0"
     P="$R/$O/prof"; mkdir -p "$P"
     pmc() {  # name counters args...
       local n=$1 c=$2; shift 2
@@ -52,11 +52,27 @@ case "$1" in
     }
     SQ1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"
     SQ2="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"
+    if [ "${2:-}" = sqlive ]; then  # only the live workload's SQ passes
+      pmc sql_1 "$SQ1" $Al && pmc sql_2 "$SQ2" $Al || exit 1
+      python3 - "$P" <<'PY'
+import csv, glob, sys
+o = sys.argv[1]
+tot = {}
+for p in ("1", "2"):
+    for f in glob.glob(f"{o}/sql_{p}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "k_mpc_wave_group" in r["Kernel_Name"]:
+                tot[r["Counter_Name"]] = tot.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+for k in sorted(tot): print(f"{k:24s} {tot[k]:.6g}")
+print(f"WAIT_ANY/WAVE_CYCLES {tot['SQ_WAIT_ANY']/tot['SQ_WAVE_CYCLES']:.3f}  ACTIVE_INST_VALU/WAVE_CYCLES {tot['SQ_ACTIVE_INST_VALU']/tot['SQ_WAVE_CYCLES']:.3f}  LDS_BANK_CONFLICT/ACTIVE_INST_LDS {tot['SQ_LDS_BANK_CONFLICT']/tot['SQ_ACTIVE_INST_LDS']:.3f}")
+PY
+      exit 0
+    fi
     pmc pmc3_fetch FETCH_SIZE $A3 && pmc pmc3_write WRITE_SIZE $A3 || exit 1
     python3 "$R/tools/pmc_summary.py" "$P/pmc3_fetch" "$P/pmc3_write" k_mpc_wave_group 65536 shared config3 > "$P/pmc_k_solve.json" || exit 1
     pmc pmc5_fetch FETCH_SIZE $A5 && pmc pmc5_write WRITE_SIZE $A5 || exit 1
     python3 "$R/tools/pmc_summary.py" "$P/pmc5_fetch" "$P/pmc5_write" k_mpc_wave_group 65536 shared config5 last > "$P/pmc_config5.json" || exit 1
-    pmc pmcl_fetch FETCH_SIZE $AL && pmc pmcl_write WRITE_SIZE $AL || exit 1
+    pmc pmcl_fetch FETCH_SIZE $Al && pmc pmcl_write WRITE_SIZE $Al || exit 1
     python3 "$R/tools/pmc_summary.py" "$P/pmcl_fetch" "$P/pmcl_write" k_mpc_wave_group 65536 shared live > "$P/pmc_live.json" || exit 1
     for w in 3 5 l; do
       eval A=\$A$w
