@@ -52,9 +52,6 @@ namespace impc {
 
 // Phase-cost experiments (tools/exp.sh only): IMPC_DUP=<section id> runs that idempotent phase of
 // the ADMM iteration twice; the bench's time difference is the phase's marginal cost.
-#ifndef IMPC_FPIPE
-#define IMPC_FPIPE 1
-#endif
 #ifndef IMPC_DUP
 #define IMPC_DUP -1
 #endif
@@ -265,9 +262,6 @@ struct WaveLds {
     // the coupling block of odd stages (IMPC_FACT3: B_k double-buffered by stage parity)
     static constexpr int FB2 = DIAGX + NMAX;
     static_assert(VS != 3 || FB2 + 104 <= RED_OFF, "factorisation scratch does not fit");
-    // the next stage's M_kk, assembled during this stage's elimination (IMPC_FPIPE, long shape)
-    static constexpr int FA2 = FB2 + 104;
-    static_assert(VS != 3 || FA2 + 169 <= RED_OFF, "factorisation scratch does not fit");
 };
 
 // the status register's mark of a failed refactorisation inside the iteration loop (never a
@@ -414,11 +408,6 @@ struct WaveQP {
     // P3P2P1 a_CL is still one 8-lane reduction.  Chain per sweep: 2 CL steps and one reduction
     // (W = 39: 16 instead of 20).
     static constexpr bool F3 = IMPC_FACT2 && IMPC_FACT3 && VS == 3;
-    // IMPC_FPIPE (long shape): stage k+1's assembly (everything but the Schur term E_k) runs on the
-    // fourth wavefront during stage k's Gauss-Jordan steps, which use lanes < 169 only; stage
-    // k+1 then starts with the 64 lanes of E_k subtracting it in place -- the same operations in
-    // the same order (terms, + diagonal, - E), off the stage chain
-    static constexpr bool PIPE = F3 && IMPC_FPIPE && NL == 256;
     static constexpr int NCH = (WF > 0 && VS == 3 && IMPC_CHUNK5) ? 5 : 4;
     static constexpr bool CHUNK = WF > 0 && NL == 256 && (VS == 3 || (VS == 1 && IMPC_CHUNK19 != 0));
     static constexpr int CL = WF > 0 ? (NCH == 5 ? 2 * ((WF + 9) / 10) : 2 * ((WF + 7) / 8)) : 2;
@@ -779,51 +768,11 @@ struct WaveQP {
                 tp[u][1] = ok ? T.term_ptr[(int64_t)k * kStageDests + d + 1] : 0;
             }
         };
-        if constexpr (!PIPE) load_tp(0);
+        load_tp(0);
 #endif
-        // stage ks's destination d (M_kk[r][c] at 13 r + c, B_k at 169 + ...): the program's terms in
-        // order, plus the diagonal; the Schur term is the caller's (IMPC_FPIPE)
-        auto asm_dest = [&](int ks, int d, double *Ad, double *Bd) {
-            const int szs = ks < W ? 13 : 8;
-            const bool isB = d >= 169;
-            if (isB && ks == W) return;
-            const int dd = isB ? d - 169 : d;
-            const int r = dd / 13, cc = dd % 13;
-            double val = 0.0;
-            if (isB || (r < szs && cc < szs)) {
-                const int32_t t0 = T.term_ptr[(int64_t)ks * kStageDests + d];
-                const int32_t t1 = T.term_ptr[(int64_t)ks * kStageDests + d + 1];
-                for (int32_t t = t0; t < t1; t += IMPC_F2B) {
-                    int32_t cd[IMPC_F2B];
-                    _Pragma("unroll") for (int v = 0; v < IMPC_F2B; v++) cd[v] = t + v < t1 ? T.term[t + v] : 0;
-                    double rg[IMPC_F2B], we[IMPC_F2B], wf[IMPC_F2B];
-                    _Pragma("unroll") for (int v = 0; v < IMPC_F2B; v++) {
-                        const int32_t g = cd[v] >> 4, e = (cd[v] >> 2) & 3, f = cd[v] & 3;
-                        rg[v] = rhog[g];
-                        we[v] = w[4 * g + e];
-                        wf[v] = w[4 * g + f];
-                    }
-                    _Pragma("unroll") for (int v = 0; v < IMPC_F2B; v++)
-                        if (t + v < t1) val += rg[v] * we[v] * wf[v];
-                }
-                if (!isB && r == cc) val += diagx[13 * ks + r];
-            }
-            (isB ? Bd : Ad)[dd] = val;
-        };
-        (void)asm_dest;
         for (int k = 0; k < N; k++) {
             const int sz = k < W ? 13 : 8;
             if constexpr (F3) Bb = lds + ((k & 1) ? LD::FB2 : LD::FB);
-            if constexpr (PIPE) {
-                A = lds + ((k & 1) ? LD::FA2 : LD::FA);
-                if (k == 0) {
-                    for (int d = L; d < kStageDests; d += NL) asm_dest(0, d, A, Bb);
-                } else if (L < 64) {  // M_kk was assembled during stage k-1: its Schur term
-                    A[13 * (L >> 3) + (L & 7)] -= e_reg;
-                }
-                wv.sync();
-                IMPC_SEC(kSecFAsm);
-            } else {
             // assemble M_kk and Bbar_k
 #if IMPC_FACT2
             int32_t tc[ND][2];
@@ -878,7 +827,6 @@ struct WaveQP {
             }
             wv.sync();
             IMPC_SEC(kSecFAsm);
-            }
             // Ahat_k^{-1} by Gauss-Jordan elimination: one element per lane, the pivots in order
             // (SPD, no pivoting needed; a non-positive-definite pivot flags the factorisation as
             // failed, as a failed Cholesky did), ping-pong between two LDS buffers so every step
@@ -891,12 +839,6 @@ struct WaveQP {
                 //   D[i][c] = S[i][c] - (S[i][J] Q) S[J][c]; a non-PD pivot block flags failure
                 for (int j = 0; j < sz; j += 2) {
                     const bool two = j + 1 < sz, last = j + (two ? 2 : 1) >= sz;
-                    if constexpr (PIPE) {  // the fourth wavefront: one slice of stage k+1's assembly per step
-                        const int d = (L - 192) + 64 * (j >> 1);
-                        if (L >= 192 && k + 1 < N && d < kStageDests)
-                            asm_dest(k + 1, d, lds + (((k + 1) & 1) ? LD::FA2 : LD::FA),
-                                     lds + (((k + 1) & 1) ? LD::FB2 : LD::FB));
-                    }
                     // element (gi, gc) of the 13 x 13 block per lane (a team of fewer than 169 lanes
                     // takes several)
                     for (int el = L; el < 169; el += NL) {
