@@ -52,6 +52,20 @@ namespace impc {
 
 // Phase-cost experiments (tools/exp.sh only): IMPC_DUP=<section id> runs that idempotent phase of
 // the ADMM iteration twice; the bench's time difference is the phase's marginal cost.
+// The serial recursions' wavefront at a raised issue priority (s_setprio) while it runs them: the
+// co-resident team's waves share its SIMD, and the recursion is the team's critical path (round 6:
+// config 3 213.9 / 214.1 -> 210.8 / 210.5 ms per launch at priority 2, 211.1 / 211.2 at 3; identical
+// iterations; 0 = off)
+#ifndef IMPC_PRIO
+#define IMPC_PRIO 2
+#endif
+#if IMPC_PRIO && defined(__HIP_DEVICE_COMPILE__)
+#define IMPC_PRIO_UP() __builtin_amdgcn_s_setprio(IMPC_PRIO)
+#define IMPC_PRIO_DOWN() __builtin_amdgcn_s_setprio(0)
+#else
+#define IMPC_PRIO_UP() ((void)0)
+#define IMPC_PRIO_DOWN() ((void)0)
+#endif
 #ifndef IMPC_DUP
 #define IMPC_DUP -1
 #endif
@@ -1467,10 +1481,12 @@ struct WaveQP {
             } else if constexpr (CHUNK) {
                 fwd_chunked(tb, rb);
             } else if ((L >> 6) == rw) {
+                IMPC_PRIO_UP();
                 if (W == LD::WSPEC)
                     fwd_sweep<LD::WSPEC>(tb, rb, W);
                 else
                     fwd_sweep<0>(tb, rb, W);
+                IMPC_PRIO_DOWN();
             }
             wv.lsync();
         }
@@ -1499,12 +1515,14 @@ struct WaveQP {
             } else if constexpr (CHUNK) {
                 bwd_chunked(eb, xb);
             } else if ((L >> 6) == rw) {
+                IMPC_PRIO_UP();
                 if (W == LD::WSPEC)
                     bwd_sweep<((LD::WSPEC - 1) & 1) != 0, LD::WSPEC>(eb, xb, W);
                 else if ((W - 1) & 1)
                     bwd_sweep<true, 0>(eb, xb, W);
                 else
                     bwd_sweep<false, 0>(eb, xb, W);
+                IMPC_PRIO_DOWN();
             }
             wv.lsync();
         }
