@@ -136,3 +136,22 @@ def test_structured_emulation_wavefront_team_horizons(N):
     cfg = scenarios.static_config(N=N, K=4, batch=1, identical=False, seed=1900 + N)
     s = impc.default_settings(**S25)
     compare(emulate(cfg, s, EMU64_PATH), oracle(cfg, s))
+
+
+def test_structured_emulation_failed_rho_update_ends_unsolved():
+    """The structured kernel body's osqp_solve exit on a failed adaptive-rho refactorisation (P
+    indefinite; P + sigma I + A'RA positive definite at the first rho only): status UNSOLVED at the
+    iteration of the update, as the oracle (the GPU twin: tests/test_persistent.py::
+    test_failed_rho_update_ends_the_solve_unsolved, same QPs)."""
+    cfg = scenarios.static_config(N=20, K=4, batch=4, identical=False, seed=520)
+    keep = [0, 1, 3]
+    v = {k: a[keep] for k, a in cfg["values"].items()}
+    v["Px"] = np.full_like(v["Px"], -1e3)
+    c = dict(cfg, values=v)
+    s = impc.default_settings(**S25)
+    _, _, info = emulate(c, s)
+    _, _, io = oracle(c, s)
+    assert (io["status_val"] == impc.UNSOLVED).any()
+    np.testing.assert_array_equal(info["status_val"], io["status_val"])
+    np.testing.assert_array_equal(info["iter"], io["iter"])
+    np.testing.assert_array_equal(info["rho_updates"], io["rho_updates"])
