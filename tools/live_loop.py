@@ -72,7 +72,8 @@ def main():
         num_pred = np.random.default_rng(4101).integers(0, K + 1, (R, Iall)).astype(np.int32)[:, lo:hi]
     gen_s = time.time() - t0
     p, pd, L = sc["params"], sc["pd"], sc["L"]
-    ctx = impc.Context(local_rank)
+    # IMPC_RANK_DEVICE: every rank on that device (a rehearsal of the rank path on a one-GPU box)
+    ctx = impc.Context(int(os.environ.get("IMPC_RANK_DEVICE", local_rank)))
     rp = DeviceReplan(ctx, p, pd, I, K, L, impc.default_settings(verbose=0))
     paths = impc.ReferencePaths(ctx, list(sc["paths"][lo:hi]), pd["ts"], N)
     Dv = impc.DeviceArray
