@@ -322,7 +322,9 @@ def main():
         share = [float(w[bounds[r]:bounds[r + 1]].sum()) for r in range(args.shard_of or world)]
     t_gen = time.time() - t_gen
 
-    ctx = impc.Context(local_rank)
+    # IMPC_RANK_DEVICE: every rank on that device (a rehearsal of the rank path on a one-GPU box;
+    # never set by the driver)
+    ctx = impc.Context(int(os.environ.get("IMPC_RANK_DEVICE", local_rank)))
     batches, nvar = [], []
     qw = scenarios.queue_weight(bks[0]["params"], bks[0]["N"]) if args.queue == "longest" else None
     for bk in bks:
@@ -341,7 +343,10 @@ def main():
         t[rank] = total_qps
         dist.all_reduce(t)
         counts = [int(c) for c in t]
-    comm = D.make_comm(dist, ctx) if (world > 1 or args.workload == "config4") else None
+    # (a rehearsal with every rank on one device, IMPC_RANK_DEVICE, has no RCCL communicator: RCCL
+    # refuses two ranks on one GPU, "invalid usage"; the step then skips the cost all-gather)
+    rehearsal = "IMPC_RANK_DEVICE" in os.environ and world > 1
+    comm = D.make_comm(dist, ctx) if ((world > 1 or args.workload == "config4") and not rehearsal) else None
     receding = None
     if args.workload == "config5" and args.receding:  # persistent workspaces: setup + first solve, untimed
         receding = RecedingLoop(impc, ctx, batches, args.warmup + args.steps)
@@ -349,7 +354,7 @@ def main():
     max_qps = max(counts)
     recv = impc.DeviceArray(ctx, (world * max_qps,), impc.INFO_DTYPE) if comm is not None else None
     # strong scaling: the cost records of the step's QPs reach every rank inside the step
-    gather_in_step = (args.workload == "config4" or (strong and world > 1)) and not args.no_allgather
+    gather_in_step = (args.workload == "config4" or (strong and world > 1)) and not args.no_allgather and comm is not None
 
     def launch():
         if receding is not None:  # the closed loop's next step, built on the device
