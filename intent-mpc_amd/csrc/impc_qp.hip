@@ -1099,6 +1099,13 @@ size_t wave_lds_bytes(int vs, int gs, const impc::WaveTables &T) {
 
 // A library built with the wavefront shape uses it unless IMPC_WAVEFRONT_SHAPE=0 is in the
 // environment when the batch is created (A/B in one process).
+// The scaling vectors of the wavefront / long shapes in LDS where it has the room (WaveTables::
+// scal_lds) unless IMPC_SCAL_LDS=0 is in the environment when the batch is created (A/B).
+bool scal_lds_on() {
+    const char *e = std::getenv("IMPC_SCAL_LDS");
+    return !(e && e[0] == '0');
+}
+
 bool wavefront_shape_on() {
     const char *e = std::getenv("IMPC_WAVEFRONT_SHAPE");
     return IMPC_WAVEFRONT != 0 && !(e && e[0] == '0');
@@ -1135,6 +1142,14 @@ bool choose_shape(impc_batch b) {
         if (!lds || lds > (need_full ? budget : (size_t)(160 * 1024 - 1024))) return false;
         b->vs = vs;
         b->gs = g;
+        // D, E in LDS when the shape keeps them in HBM and the room costs no resident team
+        t.scal_lds = 0;
+        if (!(vs == kWaveVS && impc::WaveLds<256, kWaveVS, 2>::ONCHIP) && scal_lds_on()) {
+            impc::WaveTables t2 = t;
+            t2.scal_lds = 1;
+            const size_t cap = 160 * 1024 - 1024, l2 = wave_lds_bytes(vs, g, t2);
+            if (l2 && l2 <= cap && cap / l2 >= std::min<size_t>(cap / lds, (size_t)per_cu)) t.scal_lds = 1;
+        }
         b->tier = t.T1r < impc::WaveLds<256, kWaveVS, 2>::cg4(s.CG);
         return true;
     };
@@ -1176,7 +1191,7 @@ int prepare_structured(impc_batch b) {
     for (size_t k = 0; k < arrs.size(); k++) *dst_ptrs[k] = base + offs[k];
     // per-QP HBM scratch for the scaling vectors: the wavefront and long shapes (the team shape keeps
     // them in LDS, mpc_wave.hpp WaveLds::ONCHIP)
-    const bool onchip = b->vs == kWaveVS && impc::WaveLds<256, kWaveVS, 2>::ONCHIP;
+    const bool onchip = (b->vs == kWaveVS && impc::WaveLds<256, kWaveVS, 2>::ONCHIP) || t.scal_lds;
     const size_t scal_bytes = onchip ? 0 : sizeof(double) * (size_t)b->B * (size_t)(2 * s.n + s.mg);
     if (scal_bytes) HIP_OK(hipMalloc((void **)&b->d_scal, scal_bytes));
     HIP_OK(hipMalloc((void **)&b->d_counter, 256));

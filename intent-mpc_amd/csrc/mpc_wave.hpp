@@ -145,6 +145,10 @@ struct WaveTables {
     int32_t HS;               // heavy columns (second products tier), MpcStructure::HS; 0: one tier
     const int32_t *col_hid;   // [n] heavy-column index or -1 (stage order)
     int32_t T1r;              // first-tier rows: cg4(CG) (one tier) or kProdTier1 (two tiers)
+    // the scaling vectors D, E of a shape without them in its fixed LDS layout (WaveLds::ONCHIP
+    // false): 1 = in LDS after the products region when the CU's LDS has the room (the batch
+    // setup decides), 0 = in the per-QP HBM scratch (WaveIO::scal).  (In the struct's padding.)
+    int32_t scal_lds;
 };
 
 struct WaveIO {
@@ -267,7 +271,11 @@ struct WaveLds {
     // the chunk operators' region of the one-slot shape (IMPC_CHUNK19), after the products
     static constexpr int CHX = (VS == 1 && IMPC_CHUNK19) ? 448 : 0;
     static IMPC_WF int ch_off(const WaveTables &T) { return P_OFF + p_size(T) + 8; }
-    static IMPC_WF int size(const WaveTables &T) { return P_OFF + p_size(T) + 8 + CHX; }
+    // D, E in LDS for a shape without them in the fixed layout (WaveTables::scal_lds)
+    static IMPC_WF int scl2_off(const WaveTables &T) { return P_OFF + p_size(T) + 8 + CHX; }
+    static IMPC_WF int size(const WaveTables &T) {
+        return scl2_off(T) + (!ONCHIP && T.scal_lds ? 2 * T.n + T.mg : 0);
+    }
     // factorisation aliases (inside R..X region and the products buffer)
     static constexpr int FA = R_OFF, FL = FA + 169, FI = FL + 169, FB = FI + 169, FG = FB + 104, FE = FG + 104,
                          DIAGX = FE + 64;
@@ -392,7 +400,7 @@ struct WaveQP {
     // [D n][E box n][E general mg], in LDS or in the per-QP HBM scratch
     IMPC_WF double *scal(int64_t b) {
         if constexpr (LD::ONCHIP) return lds + LD::SCL_OFF;
-        else return io.scal + b * (int64_t)(2 * T.n + T.mg);
+        else return T.scal_lds ? lds + LD::scl2_off(T) : io.scal + b * (int64_t)(2 * T.n + T.mg);
     }
 
     IMPC_WF double *F() { return lds + LD::F_OFF; }

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <barrier>
 #include <utility>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <limits>
@@ -189,6 +190,10 @@ extern "C" int emu_wave_solve_batch(int64_t n, int64_t m, const int64_t *Pp, con
     // the emulation takes the two-tier products layout whenever the pattern has heavy columns (the
     // product uses it where one tier would cost occupancy), so both gathers are covered on the CPU
     if (ms.HS == 0) T.T1r = impc::WaveLds<NL, 1, 2>::cg4(ms.CG);
+    // EMU_SCAL_LDS=1: the scaling vectors of a shape without them in its fixed layout in LDS
+    // (WaveTables::scal_lds, what the product picks where the CU has the room)
+    const char *sl = std::getenv("EMU_SCAL_LDS");
+    T.scal_lds = sl && sl[0] == '1' ? 1 : 0;
     // per-QP scratch of the scaling vectors (shapes without them in LDS)
     std::vector<double> zx((size_t)B * n, 0.0), zy((size_t)B * m, 0.0), scal((size_t)B * (2 * n + ms.mg), 0.0);
     impc::WaveIO io{B, Px, q, Ax, l, u, xws ? xws : zx.data(), yws ? yws : zy.data(), xws ? 1 : 0,

@@ -155,3 +155,18 @@ def test_structured_emulation_failed_rho_update_ends_unsolved():
     np.testing.assert_array_equal(info["status_val"], io["status_val"])
     np.testing.assert_array_equal(info["iter"], io["iter"])
     np.testing.assert_array_equal(info["rho_updates"], io["rho_updates"])
+
+
+@pytest.mark.parametrize("which", ["long", "wave64"])
+def test_structured_emulation_scaling_vectors_in_lds(which, monkeypatch):
+    """The wavefront and long shapes keep D, E in LDS after the products region when the CU has
+    the room (WaveTables::scal_lds, decided at batch setup): the same results as the oracle (and,
+    checked when built, bitwise the same as with them in the HBM scratch)."""
+    monkeypatch.setenv("EMU_SCAL_LDS", "1")
+    s = impc.default_settings(**S25)
+    if which == "long":
+        cfg = CFG["config5_N40"]
+        compare(emulate(take(cfg, 1), s), oracle(take(cfg, 1), s))
+    else:
+        cfg = take(CFG["config3_K8"], 1)
+        compare(emulate(cfg, s, EMU64_PATH), oracle(cfg, s))
