@@ -33,7 +33,9 @@ case "$1" in
     for I in 8192 16 1; do
       R=5; [ $I -lt 100 ] && R=30
       timeout -k 10 300 python -u tools/replan_bench.py --instances $I --reps $R > $O/replan_full_call_I$I.json 2> $O/replan_I$I.err || { tail -30 $O/replan_I$I.err; exit 1; }
-      ( cd ab_r05 && timeout -k 10 300 python -u tools/replan_bench.py --instances $I --reps $R ) > $O/replan_full_call_I${I}_r05.json 2> $O/replan_I${I}_r05.err || { tail -30 $O/replan_I${I}_r05.err; exit 1; }
+      if [ -d ab_r05 ]; then  # the round-5 build beside, when staged (before / after of the host syncs)
+        ( cd ab_r05 && timeout -k 10 300 python -u tools/replan_bench.py --instances $I --reps $R ) > $O/replan_full_call_I${I}_r05.json 2> $O/replan_I${I}_r05.err || { tail -30 $O/replan_I${I}_r05.err; exit 1; }
+      fi
     done
     timeout -k 10 600 python -u tools/live_loop.py > $O/live_loop.json 2> $O/live_loop.err || { tail -30 $O/live_loop.err; exit 1; }
     timeout -k 10 600 python -u tools/live_loop.py --mixed-k --obstacles 8 > $O/live_loop_mixed_k.json 2> $O/live_loop_mixed.err || { tail -30 $O/live_loop_mixed.err; exit 1; }
