@@ -63,9 +63,12 @@ int impc_replan_commit_device(impc_ctx ctx, int32_t horizon, int64_t n, int64_t 
  *                   (updateDynamicObstacles :316-341);
  * all of it in ONE grouped solve, then every plan committed into the state (:636-639 / :653-657).
  * The QPs are grouped by obstacle count: shape k (0 .. K + 1) is one solver batch holding every
- * QP of the replan with k obstacle rows per stage -- first plans (k = 0), current-obstacle solves
- * (k = c_i), single-intent candidates (k = K_i) and two-intent candidates (k = K_i + 1) -- and the
- * grouped launch spans all of them.  Which rows exist is decided on the device (a scan over the
+ * QP of the replan with k dynamic-obstacle rows per stage -- first plans (k = 0), current-obstacle
+ * solves (k = c_i), single-intent candidates (k = K_i) and two-intent candidates (k = K_i + 1) -- and
+ * the grouped launch spans all of them.  With num_static = S_st > 0 every QP not on a first plan
+ * also has S_st static-obstacle rows per stage (after the dynamic ones, with the reference's
+ * isDyamic index quirk, :1194), shape 0 holds the not-first plans without dynamic obstacles, and
+ * one more shape, K + 2, holds the first plans (no obstacle rows at all).  Which rows exist is decided on the device (a scan over the
  * instances), and the solver reads each shape's QP count from device memory: the call never
  * synchronises with the device and nothing returns to the host -- it queues the whole replan and
  * returns.  Device memory: shape k's batch is sized for its worst case (I rows for k = 0, 4 I for
@@ -96,7 +99,10 @@ typedef struct {
                                   verbose off, warm start on) */
     double issue_cutoff_s;     /* makePlanWithPred's 0.15 s; <= 0: no cut-off */
     int32_t queue_order;       /* IMPC_QUEUE_* of the grouped solve (results are identical) */
-    int32_t reserved;
+    int32_t num_static;        /* S_st, 0 <= S_st <= 30: the static obstacles every instance carries
+                                  (obclustering_->getStaticObstacles(), :594) into each solveTraj
+                                  and getTrajectoryScore not on a first plan (:593-602, :615-620,
+                                  :652); 0 = none (the live planner: clustering disabled, :191-193) */
 } impc_replan_config;
 
 /* Per-replan inputs, all DEVICE pointers (K = num_obstacles, L = pred_len, N = horizon).  An
@@ -117,6 +123,9 @@ typedef struct {
                                       (counted against the issue cut-off) */
     const int32_t *num_pred;       /* [I] K_i = predPos.size() (0 .. K; 0 = no predictions, as
                                       has_pred = 0); NULL = K for every instance */
+    const double *st_centroid;     /* [I][S_st][3] staticObstacle::centroid; with num_static > 0 */
+    const double *st_size;         /* [I][S_st][3] staticObstacle::size */
+    const double *st_yaw;          /* [I][S_st]    staticObstacle::yaw */
 } impc_replan_inputs;
 
 /* What the last impc_replan_run did (host values; reading them synchronises the context). */
@@ -148,20 +157,23 @@ int impc_replan_get_stats(impc_replan rp, impc_replan_stats *out);
  * Per instance of the last run: branch [I] (IMPC_REPLAN_*), best_cand [I] (fan-out instances:
  * the selected candidate or -1; -1 otherwise), ob_idx [I] (closest obstacle; -1 for single-solve
  * instances), cand_type / cand_slot [I][6] (getIntentComb order; -1 for single-solve instances),
- * num_obs [I] (fan-out: K_i; single solve: the obstacle count of its QP = its shape), slot_row
- * [I][6] (fan-out: the row of slot s in shape K_i (s < 4) or K_i + 1 (s >= 4); single solve: its
- * row in shape num_obs at [0]; -1 elsewhere). */
+ * num_obs [I] (fan-out: K_i; single solve: the dynamic-obstacle count of its QP = its shape, except
+ * a first plan with num_static > 0: shape K + 2), slot_row [I][6] (fan-out: the row of slot s in
+ * shape K_i (s < 4) or K_i + 1 (s >= 4); single solve: its row in its shape at [0]; -1
+ * elsewhere), shape [I] (the shape of the instance's single solve; fan-out: K_i). */
 typedef struct {
     double *plan_x, *plan_states;
     int32_t *prev_count;
     int8_t *first_time, *valid, *branch;
     int32_t *best_cand, *ob_idx, *cand_type, *cand_slot;
     int32_t *num_obs, *slot_row;
+    int32_t *shape;
 } impc_replan_view;
 int impc_replan_view_device(impc_replan rp, impc_replan_view *out);
 
 /* Inspection of the last run (tests, tools; synchronises the context): shape k = the QPs with k
- * obstacle rows per stage (0 <= k <= K + 1) -- its solver batch, the number of its rows solved in
+ * dynamic-obstacle rows per stage (0 <= k <= K + 1; k = K + 2: the first plans of a replan object
+ * with num_static > 0) -- its solver batch, the number of its rows solved in
  * the last replan, each row's instance and kind (DEVICE int32 row_inst / int8 row_code [count]:
  * 0..3 single-intent slot, 4..5 two-intent slot, 6 first plan / no obstacles, 7 current obstacles;
  * single solves first, then the candidates, each in ascending instance order) and the assembled

@@ -2531,13 +2531,15 @@ int batch_tlim_device(impc_batch b, double **out) {
 double tick_s(impc_ctx ctx) { return ctx->tick_s; }
 int build_rows(impc_mpc_builder bd, int64_t cap, const int64_t *dcount, const int32_t *row_inst, const int64_t *osrc,
                const double *pos, const double *vel, const double *xref, const double *lin, const double *pred_pos,
-               const double *pred_size, const double *held_pos, const double *held_size, const BatchInputs &out,
-               hipStream_t st) {
+               const double *pred_size, const double *held_pos, const double *held_size, const double *st_centroid,
+               const double *st_size, const double *st_yaw, const BatchInputs &out, hipStream_t st) {
     if (!bd || cap < 1) return fail(IMPC_INVALID_ARGUMENT, "build_rows: null builder or empty capacity");
+    if (bd->S > 0 && (!st_centroid || !st_size || !st_yaw))
+        return fail(IMPC_INVALID_ARGUMENT, "build_rows: static obstacles required by the builder");
     impc_build::Args a{cap, bd->n, bd->m, bd->nnzP, bd->nnzA, bd->obs_off, bd->N, bd->W, bd->S, bd->Kd, bd->K, bd->L,
                        bd->p.dynamic_safety_dist, bd->p.static_safety_dist, bd->p.position_weight,
                        bd->p.velocity_weight, bd->d_tPx, bd->d_tAx, bd->d_tl, bd->d_tu, bd->d_slot, pos, vel, xref,
-                       lin, nullptr, nullptr, nullptr, pred_pos, pred_size, out.Px, out.q, out.Ax, out.l, out.u};
+                       lin, st_centroid, st_size, st_yaw, pred_pos, pred_size, out.Px, out.q, out.Ax, out.l, out.u};
     a.dcount = dcount, a.row_inst = row_inst, a.osrc = osrc, a.hp = held_pos, a.hs = held_size;
     const int64_t groups = std::min<int64_t>(cap, (int64_t)bd->ctx->num_cu * 8);
     hipLaunchKernelGGL(impc_build::k_build, dim3((unsigned)groups), dim3(256), 0, st, a);

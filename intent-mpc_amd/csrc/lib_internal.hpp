@@ -46,10 +46,11 @@ int batch_set_active_device(impc_batch b, const int64_t *d_count);
 int batch_tlim_device(impc_batch b, double **out);
 // seconds per tick of the device clock the time limits run on (hipDeviceAttributeWallClockRate)
 double tick_s(impc_ctx ctx);
-// The device builder over replan rows (mpc_build.hpp Args: dcount / row_inst / osrc / held arrays),
+// The device builder over replan rows (mpc_build.hpp Args: dcount / row_inst / osrc / held arrays;
+// static obstacles per instance, [*][builder's S][3] / [*][S], unread when the builder has none),
 // writing the QP values into a batch's input arrays; asynchronous on `st`.
 int build_rows(impc_mpc_builder bd, int64_t cap, const int64_t *dcount, const int32_t *row_inst, const int64_t *osrc,
                const double *pos, const double *vel, const double *xref, const double *lin, const double *pred_pos,
-               const double *pred_size, const double *held_pos, const double *held_size, const BatchInputs &out,
-               hipStream_t st);
+               const double *pred_size, const double *held_pos, const double *held_size, const double *st_centroid,
+               const double *st_size, const double *st_yaw, const BatchInputs &out, hipStream_t st);
 }  // namespace impc_lib

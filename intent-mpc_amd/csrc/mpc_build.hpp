@@ -25,8 +25,8 @@ struct Args {
     const double *cp, *cv, *xref, *ls, *stc, *sts, *sty, *dp, *ds;
     double *Px, *q, *Ax, *l, *u;
     // replan rows (impc_lib::build_rows, replan_run.hip): the row count in device memory (rows >=
-    // *dcount are not built), each row's planning instance (x0, reference and linearisation
-    // point are per-instance arrays, indexed by row_inst[b]) and each dynamic obstacle's source:
+    // *dcount are not built), each row's planning instance (x0, reference, linearisation point
+    // and static obstacles are per-instance arrays, indexed by row_inst[b]) and each dynamic obstacle's source:
     // osrc[b][j] = (offset << 1) | held -- held = 0: the trajectory at dp / ds + offset, step
     // stride 3 (a prediction); held = 1: the position at hp / hs + offset for every stage (a
     // current obstacle, updateDynamicObstacles :316-341).  All null: the plain layouts above.
@@ -91,10 +91,10 @@ __global__ __launch_bounds__(256) void k_build(Args a) {
                 yaw = 0.0;
             } else {
                 const int js = j - a.Kd;
-                const double *c = a.stc + ((int64_t)b * a.S + js) * 3, *z = a.sts + ((int64_t)b * a.S + js) * 3;
+                const double *c = a.stc + (ib * a.S + js) * 3, *z = a.sts + (ib * a.S + js) * 3;
                 ox = c[0], oy = c[1], oz = c[2];
                 sx = z[0] / 2 + a.ssafe, sy = z[1] / 2 + a.ssafe, sz = z[2] / 2 + a.ssafe;
-                yaw = a.sty[(int64_t)b * a.S + js];
+                yaw = a.sty[ib * a.S + js];
             }
             double cx, cy, cz;  // linearisation point (:1042-1051)
             if (a.ls) {

@@ -58,18 +58,26 @@ constexpr int kPlanLanes = 512;
 constexpr int kMaxObstacles = 30;
 constexpr int FORWARD = 0, LEFT = 1, RIGHT = 2, STOP = 3;  // dynamicPredictor's intent enum
 
-// Shape k's rows in the flat row arrays: shape 0 holds the first-plan / obstacle-free single
-// solves (<= I rows); shapes 1..K at most four rows per instance (the four single-intent
+// Shape k's rows in the flat row arrays: shape 0 holds the single solves without dynamic
+// obstacles (<= I rows); shapes 1..K at most four rows per instance (the four single-intent
 // candidates of an instance with K_i = k, or the two two-intent candidates of one with K_i + 1 =
 // k, or one current-obstacle single solve with c_i = k); shape K + 1 the two-intent candidates of
-// the instances with K_i = K (<= 2 I rows).
-__host__ __device__ inline int64_t shape_base(int64_t I, int k) { return k == 0 ? 0 : I + 4 * I * (int64_t)(k - 1); }
-__host__ __device__ inline int64_t shape_cap(int64_t I, int K, int k) { return k == 0 ? I : k <= K ? 4 * I : 2 * I; }
+// the instances with K_i = K (<= 2 I rows); shape K + 2, present with static obstacles only, the
+// first plans (<= I rows; without static obstacles they are shape 0's).
+__host__ __device__ inline int64_t shape_base(int64_t I, int K, int k) {
+    return k == 0 ? 0 : k <= K + 1 ? I + 4 * I * (int64_t)(k - 1) : I * (4 * (int64_t)K + 3);
+}
+__host__ __device__ inline int64_t shape_cap(int64_t I, int K, int k) {
+    return k == 0 ? I : k <= K ? 4 * I : k == K + 1 ? 2 * I : I;
+}
 __host__ __device__ inline int shape_of(int64_t I, int K, int64_t f) {
     if (f < I) return 0;
+    if (f >= I * (4 * (int64_t)K + 3)) return K + 2;
     const int64_t k = 1 + (f - I) / (4 * I);
     return (int)(k < K + 1 ? k : K + 1);
 }
+// the dynamic-obstacle rows per stage of shape k's QPs
+__host__ __device__ inline int shape_dyn(int K, int k) { return k <= K + 1 ? k : 0; }
 
 // per-shape device pointers, fixed when the replan object is created
 struct ShapeDev {
@@ -95,15 +103,21 @@ struct Decide {
 
 struct PlanArgs {
     int64_t I;
-    int32_t K, S;
+    int32_t K, S, first_shape;  // first_shape: the first plans' shape (K + 2 with static obstacles, else 0)
     Decide decide;
     int8_t *branch;
-    int32_t *num_obs, *slot_row, *best;
+    int32_t *num_obs, *shp, *slot_row, *best;
     int32_t *row_inst;
     int8_t *row_code;
     int64_t *cnt;               // [S] single solves per shape, [S .. 2S) rows per shape, [2S .. 2S+3) branches
     unsigned long long *clk;    // [0] the device clock at the start of the replan
 };
+
+// The shape of a single solve: a first plan's QP has no obstacle rows (static and dynamic obstacles
+// cleared, :593-602), any other has the current obstacles' c_i (0 with SINGLE_FIRST) and the statics.
+__device__ inline int single_shape(const PlanArgs &a, int64_t i, int br, int ci) {
+    return br == IMPC_REPLAN_SINGLE_CURRENT ? ci : a.decide.first_time[i] != 0 ? a.first_shape : 0;
+}
 
 // One workgroup of kPlanLanes lanes, lane t owning a contiguous range of instances.  Counters
 // [R = 2S + 3][kPlanLanes] in LDS (rows 0..S-1: single solves of shape k, S..2S-1: candidate rows
@@ -127,7 +141,7 @@ __global__ __launch_bounds__(kPlanLanes) void k_plan_rows(PlanArgs a) {
             cl[(S + ki) * kPlanLanes + t] += 4;
             cl[(S + ki + 1) * kPlanLanes + t] += 2;
         } else {
-            cl[(br == IMPC_REPLAN_SINGLE_FIRST ? 0 : ci) * kPlanLanes + t]++;
+            cl[single_shape(a, i, br, ci) * kPlanLanes + t]++;
         }
     }
     for (int r = 0; r < R; r++) {  // exclusive scan inside each wavefront
@@ -160,21 +174,23 @@ __global__ __launch_bounds__(kPlanLanes) void k_plan_rows(PlanArgs a) {
         for (int s = 0; s < 6; s++) sr[s] = -1;
         if (br == IMPC_REPLAN_FANOUT) {
             a.num_obs[i] = ki;
+            a.shp[i] = ki;
             for (int s = 0; s < 6; s++) {
                 const int k = s < 4 ? ki : ki + 1;
                 const int64_t r = total(k) + cl[(S + k) * kPlanLanes + t]++;
-                const int64_t f = shape_base(a.I, k) + r;
+                const int64_t f = shape_base(a.I, a.K, k) + r;
                 a.row_inst[f] = (int32_t)i;
                 a.row_code[f] = (int8_t)s;
                 sr[s] = (int32_t)r;
             }
         } else {
-            const int k = br == IMPC_REPLAN_SINGLE_FIRST ? 0 : ci;
+            const int k = single_shape(a, i, br, ci);
             const int64_t r = cl[k * kPlanLanes + t]++;
-            const int64_t f = shape_base(a.I, k) + r;
+            const int64_t f = shape_base(a.I, a.K, k) + r;
             a.row_inst[f] = (int32_t)i;
-            a.row_code[f] = (int8_t)(k == 0 ? IMPC_REPLAN_ROW_FIRST : IMPC_REPLAN_ROW_CURRENT);
-            a.num_obs[i] = k;
+            a.row_code[f] = (int8_t)(br == IMPC_REPLAN_SINGLE_FIRST ? IMPC_REPLAN_ROW_FIRST : IMPC_REPLAN_ROW_CURRENT);
+            a.num_obs[i] = br == IMPC_REPLAN_SINGLE_FIRST ? 0 : ci;
+            a.shp[i] = k;
             sr[0] = (int32_t)r;
         }
     }
@@ -312,7 +328,7 @@ struct PrepArgs {
 __global__ __launch_bounds__(64) void k_prep(PrepArgs a) {
     for (int64_t f = blockIdx.x; f < a.total; f += gridDim.x) {
         const int k = shape_of(a.I, a.K, f);
-        const int64_t r = f - shape_base(a.I, k);
+        const int64_t r = f - shape_base(a.I, a.K, k);
         if (r >= a.cnt[a.S + k]) continue;
         const ShapeDev sd = a.sh[k];
         const int64_t i = a.row_inst[f];
@@ -321,7 +337,8 @@ __global__ __launch_bounds__(64) void k_prep(PrepArgs a) {
         double *dst = sd.xws + r * a.n;
         for (int64_t e = threadIdx.x; e < a.n; e += blockDim.x) dst[e] = src[e];
         if (threadIdx.x == 0) sd.tlim[r] = code < 6 ? a.cand_limit : 0.0;
-        for (int o = threadIdx.x; o < k; o += blockDim.x) {
+        const int kd = shape_dyn(a.K, k);
+        for (int o = threadIdx.x; o < kd; o += blockDim.x) {
             int64_t off;
             if (code == IMPC_REPLAN_ROW_CURRENT) {  // held over the horizon
                 off = ((i * a.K + o) * 3) << 1 | 1;
@@ -330,7 +347,7 @@ __global__ __launch_bounds__(64) void k_prep(PrepArgs a) {
                 cand_obstacle(a.ob[i], a.slot_type[6 * i + code], code >= 4, o, a.prob + i * a.K * 4, kk, intent);
                 off = ((((i * a.K + kk) * 4 + intent) * (int64_t)a.L) * 3) << 1;
             }
-            sd.osrc[r * k + o] = off;
+            sd.osrc[r * kd + o] = off;
         }
     }
 }
@@ -407,7 +424,7 @@ struct CommitArgs {
     int32_t N;
     const ShapeDev *sh;
     const int8_t *branch;
-    const int32_t *num_obs, *slot_row, *best;
+    const int32_t *shp, *slot_row, *best;
     const double *const *x_cand;
     double *plan_x, *plan_states;
     int32_t *prev_count;
@@ -423,7 +440,7 @@ __global__ __launch_bounds__(64) void k_commit(CommitArgs a) {
             const int b = a.best[i];
             if (b >= 0) src = a.x_cand[6 * i + b];
         } else {
-            const int k = a.num_obs[i];
+            const int k = a.shp[i];
             const int64_t r = a.slot_row[6 * i];
             if (impc_lib::solve_traj_ok(a.sh[k].info[r])) src = a.sh[k].x + r * a.n;
         }
@@ -479,9 +496,10 @@ struct Arena {
     }
 };
 
-// one QP shape of the replan (k obstacle rows per stage): its solver batch and on-device builder
+// one QP shape of the replan (k dynamic- and nst static-obstacle rows per stage): its solver batch
+// and on-device builder
 struct Shape {
-    int32_t k = 0;
+    int32_t k = 0, nst = 0;
     int64_t cap = 0;
     impc_qp_dims dm{};
     impc_batch batch = nullptr;
@@ -505,7 +523,7 @@ struct impc_replan_s {
     int8_t *first_time = nullptr, *valid = nullptr, *zeros8 = nullptr;
     // rows of the shapes and per-instance outputs
     int8_t *branch = nullptr, *row_code = nullptr;
-    int32_t *row_inst = nullptr, *num_obs = nullptr, *slot_row = nullptr, *slot_type = nullptr;
+    int32_t *row_inst = nullptr, *num_obs = nullptr, *shp = nullptr, *slot_row = nullptr, *slot_type = nullptr;
     int32_t *best = nullptr, *ob = nullptr, *ctype = nullptr, *cslot = nullptr, *issued = nullptr;
     int64_t *cnt = nullptr, *solve = nullptr;
     unsigned long long *clk = nullptr;
@@ -516,7 +534,8 @@ struct impc_replan_s {
     int32_t *dyn_count = nullptr, *best_pos = nullptr;
     double *dyn_pos = nullptr, *dyn_size = nullptr, *scores = nullptr, *weighted = nullptr;
     int8_t *cvalid = nullptr;
-    std::vector<Shape> sh;  // S = K + 2 shapes, by obstacle count
+    int32_t nst = 0;        // static obstacles per instance (cfg.num_static)
+    std::vector<Shape> sh;  // S = K + 2 shapes by dynamic-obstacle count, + the first plans' with statics
     std::vector<impc_batch> group;
     impc_replan_stats stats{};
     bool ran = false;
@@ -528,11 +547,11 @@ namespace {
 
 int fail(int code, const char *msg) { return impc_lib::set_error(code, msg); }
 
-int make_shape(impc_replan rp, Shape &s, int32_t k, int64_t cap) {
-    s.k = k, s.cap = cap;
-    RP_TRY(impc_mpc_dims(&rp->cfg.mpc, 0, k, &s.dm));
+int make_shape(impc_replan rp, Shape &s, int32_t k, int32_t nst, int64_t cap) {
+    s.k = k, s.nst = nst, s.cap = cap;
+    RP_TRY(impc_mpc_dims(&rp->cfg.mpc, nst, k, &s.dm));
     std::vector<int64_t> Pp(s.dm.n + 1), Pi(std::max<int64_t>(s.dm.nnzP, 1)), Ap(s.dm.n + 1), Ai(s.dm.nnzA);
-    RP_TRY(impc_mpc_build_pattern(&rp->cfg.mpc, 0, k, Pp.data(), Pi.data(), Ap.data(), Ai.data()));
+    RP_TRY(impc_mpc_build_pattern(&rp->cfg.mpc, nst, k, Pp.data(), Pi.data(), Ap.data(), Ai.data()));
     RP_TRY(impc_batch_create(rp->ctx, s.dm.n, s.dm.m, Pp.data(), Pi.data(), Ap.data(), Ai.data(), cap, &s.batch));
     RP_TRY(impc_batch_set_settings(s.batch, &rp->cfg.settings));
     if (rp->cfg.queue_order == IMPC_QUEUE_LONGEST_FIRST) {
@@ -541,7 +560,7 @@ int make_shape(impc_replan rp, Shape &s, int32_t k, int64_t cap) {
         RP_TRY(impc_batch_set_queue_order(s.batch, IMPC_QUEUE_LONGEST_FIRST, qw));
     }
     RP_TRY(impc_batch_set_kernel(s.batch, IMPC_KERNEL_STRUCTURED));
-    RP_TRY(impc_mpc_builder_create(rp->ctx, &rp->cfg.mpc, 0, k, rp->L, &s.bld));
+    RP_TRY(impc_mpc_builder_create(rp->ctx, &rp->cfg.mpc, nst, k, rp->L, &s.bld));
     impc_lib::BatchInputs bi{};
     RP_TRY(impc_lib::batch_inputs_view(s.batch, &bi));
     double *x = nullptr;
@@ -575,9 +594,10 @@ int impc_replan_create(impc_ctx ctx, const impc_replan_config *cfg, impc_replan 
     *out = nullptr;
     const int64_t I = cfg->instances;
     const int32_t N = cfg->mpc.horizon, K = cfg->num_obstacles, L = cfg->pred_len;
-    if (I < 1 || I > ((int64_t)1 << 24) || N < 2 || K < 1 || K > kMaxObstacles || L < 1)
-        return fail(IMPC_INVALID_ARGUMENT,
-                    "replan: 1 <= instances <= 2^24, horizon >= 2, 1 <= num_obstacles <= 30, pred_len >= 1");
+    if (I < 1 || I > ((int64_t)1 << 24) || N < 2 || K < 1 || K > kMaxObstacles || L < 1 || cfg->num_static < 0 ||
+        cfg->num_static > kMaxObstacles)
+        return fail(IMPC_INVALID_ARGUMENT, "replan: 1 <= instances <= 2^24, horizon >= 2, 1 <= num_obstacles <= 30, "
+                                           "pred_len >= 1, 0 <= num_static <= 30");
     if (cfg->mpc.num_half_space != 0)
         return fail(IMPC_UNSUPPORTED, "replan: the live planner path has no FOV half-spaces (num_half_space = 0)");
     if (cfg->queue_order != IMPC_QUEUE_FIFO && cfg->queue_order != IMPC_QUEUE_LONGEST_FIRST)
@@ -586,9 +606,10 @@ int impc_replan_create(impc_ctx ctx, const impc_replan_config *cfg, impc_replan 
     std::unique_ptr<impc_replan_s> rp(new impc_replan_s());
     rp->ctx = ctx;
     rp->cfg = *cfg;
-    rp->I = I, rp->N = N, rp->K = K, rp->L = L, rp->S = K + 2;
+    rp->I = I, rp->N = N, rp->K = K, rp->L = L, rp->nst = cfg->num_static;
+    rp->S = K + 2 + (rp->nst > 0 ? 1 : 0);
     rp->n = 13 * (int64_t)N - 5;
-    rp->rows = shape_base(I, K + 1) + shape_cap(I, K, K + 1);
+    rp->rows = shape_base(I, K, rp->S - 1) + shape_cap(I, K, rp->S - 1);
     const int64_t n = rp->n, S = rp->S;
     Arena &a = rp->mem;
     int rc = IMPC_OK;
@@ -611,6 +632,7 @@ int impc_replan_create(impc_ctx ctx, const impc_replan_config *cfg, impc_replan 
     RP_CK(a.get((size_t)rp->rows, &rp->row_inst));
     RP_CK(a.get((size_t)rp->rows, &rp->row_code));
     RP_CK(a.get((size_t)I, &rp->num_obs));
+    RP_CK(a.get((size_t)I, &rp->shp));
     RP_CK(a.get((size_t)(6 * I), &rp->slot_row));
     RP_CK(a.get((size_t)(6 * I), &rp->slot_type));
     RP_CK(a.get((size_t)I, &rp->best));
@@ -639,12 +661,12 @@ int impc_replan_create(impc_ctx ctx, const impc_replan_config *cfg, impc_replan 
         cleanup();
         return fail(IMPC_DEVICE_ERROR, "replan: memset");
     }
-    // one solver batch per obstacle count, each reading its QP count from device memory
+    // one solver batch per shape, each reading its QP count from device memory
     rp->sh.resize((size_t)S);
     std::vector<ShapeDev> hdev((size_t)S);
     for (int32_t k = 0; k < S; k++) {
         Shape &s = rp->sh[(size_t)k];
-        RP_CK(make_shape(rp.get(), s, k, shape_cap(I, K, k)));
+        RP_CK(make_shape(rp.get(), s, shape_dyn(K, k), k <= K + 1 ? rp->nst : 0, shape_cap(I, K, k)));
         RP_CK(impc_lib::batch_set_active_device(s.batch, rp->solve + k));
         hdev[(size_t)k] = s.dev;
         rp->group.push_back(s.batch);
@@ -706,6 +728,8 @@ int impc_replan_run(impc_replan rp, const impc_replan_inputs *in) {
     if (!in->pos || !in->vel || !in->xref || !in->dyn_cur || !in->pred_pos || !in->pred_size || !in->prob)
         return fail(IMPC_INVALID_ARGUMENT, "replan: pos, vel, xref, dyn_cur, pred_pos, pred_size, prob are required");
     if (in->cur_count && !in->cur_size) return fail(IMPC_INVALID_ARGUMENT, "replan: cur_count needs cur_size");
+    if (rp->nst > 0 && (!in->st_centroid || !in->st_size || !in->st_yaw))
+        return fail(IMPC_INVALID_ARGUMENT, "replan: num_static > 0 needs st_centroid, st_size, st_yaw");
     impc_ctx ctx = rp->ctx;
     RP_HIP(hipSetDevice(impc_lib::device(ctx)));
     hipStream_t st = impc_lib::stream(ctx);
@@ -714,8 +738,20 @@ int impc_replan_run(impc_replan rp, const impc_replan_inputs *in) {
     const int32_t N = rp->N, K = rp->K, L = rp->L, S = rp->S;
 
     // ---- the branch and the rows of every instance (:593-606)
-    PlanArgs pa{I, K, S, Decide{rp->first_time, in->has_pred, in->num_pred, in->cur_count, K, in->cur_size ? 1 : 0},
-                rp->branch, rp->num_obs, rp->slot_row, rp->best, rp->row_inst, rp->row_code, rp->cnt, rp->clk};
+    PlanArgs pa{I,
+                K,
+                S,
+                rp->nst > 0 ? K + 2 : 0,
+                Decide{rp->first_time, in->has_pred, in->num_pred, in->cur_count, K, in->cur_size ? 1 : 0},
+                rp->branch,
+                rp->num_obs,
+                rp->shp,
+                rp->slot_row,
+                rp->best,
+                rp->row_inst,
+                rp->row_code,
+                rp->cnt,
+                rp->clk};
     const size_t lds = sizeof(int32_t) * (size_t)(2 * S + 3) * (kPlanLanes + kPlanLanes / 64);
     hipLaunchKernelGGL(k_plan_rows, dim3(1), dim3(kPlanLanes), lds, st, pa);
     RP_HIP(hipGetLastError());
@@ -735,9 +771,11 @@ int impc_replan_run(impc_replan rp, const impc_replan_inputs *in) {
         Shape &s = rp->sh[(size_t)k];
         impc_lib::BatchInputs bi{};
         RP_TRY(impc_lib::batch_inputs_begin(s.batch, &bi));
-        RP_TRY(impc_lib::build_rows(s.bld, s.cap, rp->cnt + S + k, rp->row_inst + shape_base(I, k), s.dev.osrc,
+        const bool stat = s.nst > 0;
+        RP_TRY(impc_lib::build_rows(s.bld, s.cap, rp->cnt + S + k, rp->row_inst + shape_base(I, K, k), s.dev.osrc,
                                     in->pos, in->vel, in->xref, rp->plan_states, in->pred_pos, in->pred_size,
-                                    in->dyn_cur, in->cur_size, bi, st));
+                                    in->dyn_cur, in->cur_size, stat ? in->st_centroid : nullptr,
+                                    stat ? in->st_size : nullptr, stat ? in->st_yaw : nullptr, bi, st));
         RP_TRY(impc_lib::batch_inputs_end(s.batch, true));
     }
     // ---- the issue cut-off on the device clock; ONE grouped solve over every shape
@@ -754,13 +792,14 @@ int impc_replan_run(impc_replan rp, const impc_replan_inputs *in) {
     RP_HIP(hipGetLastError());
     impc_select_params sp{};
     sp.horizon = N, sp.num_candidates = 6, sp.max_dynamic = K + 1, sp.pred_len = L;
-    sp.num_static = 0, sp.prev_len = N;
+    sp.num_static = rp->nst, sp.prev_len = N;  // getTrajectoryScore's staticObstacles (:620)
     sp.dynamic_safety_dist = rp->cfg.mpc.dynamic_safety_dist;
     sp.static_safety_dist = rp->cfg.mpc.static_safety_dist;
     RP_TRY(impc_select_best_device(ctx, &sp, I, rp->x_cand, rp->cvalid, rp->zeros8, rp->plan_states, rp->prev_count,
-                                   in->xref, nullptr, nullptr, rp->dyn_count, rp->dyn_pos, rp->dyn_size, rp->cprob,
+                                   in->xref, rp->nst ? in->st_centroid : nullptr, rp->nst ? in->st_size : nullptr,
+                                   rp->dyn_count, rp->dyn_pos, rp->dyn_size, rp->cprob,
                                    rp->best, rp->best_pos, rp->scores, rp->weighted, nullptr));
-    CommitArgs cm{I, n, N, rp->d_sh, rp->branch, rp->num_obs, rp->slot_row, rp->best, rp->x_cand, rp->plan_x,
+    CommitArgs cm{I, n, N, rp->d_sh, rp->branch, rp->shp, rp->slot_row, rp->best, rp->x_cand, rp->plan_x,
                   rp->plan_states, rp->prev_count, rp->first_time, rp->valid};
     hipLaunchKernelGGL(k_commit, dim3(grid_for(rp, I, 1)), dim3(64), 0, st, cm);
     RP_HIP(hipGetLastError());
@@ -797,7 +836,7 @@ int impc_replan_view_device(impc_replan rp, impc_replan_view *out) {
     out->plan_x = rp->plan_x, out->plan_states = rp->plan_states, out->prev_count = rp->prev_count;
     out->first_time = rp->first_time, out->valid = rp->valid, out->branch = rp->branch;
     out->best_cand = rp->best, out->ob_idx = rp->ob, out->cand_type = rp->ctype, out->cand_slot = rp->cslot;
-    out->num_obs = rp->num_obs, out->slot_row = rp->slot_row;
+    out->num_obs = rp->num_obs, out->slot_row = rp->slot_row, out->shape = rp->shp;
     return IMPC_OK;
 }
 
@@ -805,7 +844,7 @@ int impc_replan_shape(impc_replan rp, int32_t obstacles, impc_batch *batch, int6
                       const int8_t **row_code, const double **Px, const double **q, const double **Ax,
                       const double **l, const double **u) {
     if (!rp || obstacles < 0 || obstacles >= rp->S)
-        return fail(IMPC_INVALID_ARGUMENT, "replan: shape (obstacle count) must be in 0 .. num_obstacles + 1");
+        return fail(IMPC_INVALID_ARGUMENT, "replan: shape must be in 0 .. num_obstacles + 1 (+ 2 with num_static)");
     const Shape &s = rp->sh[(size_t)obstacles];
     int64_t c = 0;
     if (rp->ran) {
@@ -814,7 +853,7 @@ int impc_replan_shape(impc_replan rp, int32_t obstacles, impc_batch *batch, int6
     }
     if (batch) *batch = s.batch;
     if (count) *count = c;
-    const int64_t base = shape_base(rp->I, obstacles);
+    const int64_t base = shape_base(rp->I, rp->K, obstacles);
     if (row_inst) *row_inst = rp->row_inst + base;
     if (row_code) *row_code = rp->row_code + base;
     impc_lib::BatchInputs bi{};

@@ -29,7 +29,10 @@ updatePredObstacles :343-373).  The QPs of a replan are grouped by obstacle coun
 every QP with k obstacle rows per stage (first plans k = 0, current-obstacle solves k = c_i,
 single-intent candidates K_i, two-intent candidates K_i + 1), one solver batch per shape, all in
 one grouped launch whose per-shape QP counts the device decides and the solver reads from device
-memory -- the library call never waits for the device and reads nothing back.
+memory -- the library call never waits for the device and reads nothing back.  With num_static
+S_st > 0 every QP not on a first plan also carries the instance's S_st static obstacles
+(obclustering_->getStaticObstacles(), :594; scored by getTrajectoryScore too) and the first plans
+move to shape K + 2.
 
 Everything here beyond impc_replan_run / impc_replan_set_state (input uploads, the per-shape
 results and assembled values of run()'s return dict) is test plumbing.
@@ -53,14 +56,15 @@ class ReplanConfig(C.Structure):
     """impc_replan_config (include/impc_replan.h)."""
     _fields_ = [("instances", C.c_int64), ("num_obstacles", C.c_int32), ("pred_len", C.c_int32),
                 ("mpc", MpcParams), ("settings", Settings), ("issue_cutoff_s", C.c_double),
-                ("queue_order", C.c_int32), ("reserved", C.c_int32)]
+                ("queue_order", C.c_int32), ("num_static", C.c_int32)]
 
 
 class ReplanInputs(C.Structure):
     """impc_replan_inputs: device pointers + the budget."""
     _fields_ = [(k, C.c_void_p) for k in ("pos", "vel", "xref", "dyn_cur", "pred_pos", "pred_size", "prob", "has_pred",
                                           "cur_size", "cur_count")] + \
-               [("solver_time_limit", C.c_double), ("elapsed_s", C.c_double), ("num_pred", C.c_void_p)]
+               [("solver_time_limit", C.c_double), ("elapsed_s", C.c_double), ("num_pred", C.c_void_p),
+                ("st_centroid", C.c_void_p), ("st_size", C.c_void_p), ("st_yaw", C.c_void_p)]
 
 
 class ReplanStats(C.Structure):
@@ -71,7 +75,8 @@ class ReplanStats(C.Structure):
 
 class ReplanView(C.Structure):
     _fields_ = [(k, C.c_void_p) for k in ("plan_x", "plan_states", "prev_count", "first_time", "valid", "branch",
-                                          "best_cand", "ob_idx", "cand_type", "cand_slot", "num_obs", "slot_row")]
+                                          "best_cand", "ob_idx", "cand_type", "cand_slot", "num_obs", "slot_row",
+                                          "shape")]
 
 
 def _sig(name, *args):
@@ -113,7 +118,8 @@ def candidate_valid(cand_slot, info_single, info_pair):
 
 def assemble(per_inst, shapes):
     """The per-kind views of one replan from its per-shape rows (shapes[k] = dict(x, y, info[, vals,
-    lat]) of the rows shape k solved) and the per-instance outputs (branch, num_obs, slot_row):
+    lat]) of the rows shape k solved) and the per-instance outputs (branch, num_obs, slot_row, shape
+    -- the single solve's shape, = num_obs without static obstacles):
     x_<kind>, y_<kind>, info_<kind>, vals_<kind>, lat_<kind> for the kinds single (the single-intent
     candidates, row 4 j + slot of the j-th fan-out instance), pair (two-intent, 2 j + slot - 4),
     first and current (row j of the j-th instance on that branch).  x and info are arrays; y and
@@ -121,13 +127,14 @@ def assemble(per_inst, shapes):
     with no solved row is None.  Also cand_rows [I][6] = (shape, row) of candidate c (getIntentComb
     order) and single_rows [I] = (shape, row)."""
     br, K, R = per_inst["branch"], per_inst["num_obs"], per_inst["slot_row"]
+    SH = per_inst.get("shape", K)
     I = br.shape[0]
     out = {"inst_fanout": np.flatnonzero(br == FANOUT), "inst_first": np.flatnonzero(br == SINGLE_FIRST),
            "inst_current": np.flatnonzero(br == SINGLE_CURRENT)}
     rows = {"single": [(int(K[i]), int(R[i, s])) for i in out["inst_fanout"] for s in range(4)],
             "pair": [(int(K[i]) + 1, int(R[i, s])) for i in out["inst_fanout"] for s in (4, 5)],
-            "first": [(int(K[i]), int(R[i, 0])) for i in out["inst_first"]],
-            "current": [(int(K[i]), int(R[i, 0])) for i in out["inst_current"]]}
+            "first": [(int(SH[i]), int(R[i, 0])) for i in out["inst_first"]],
+            "current": [(int(SH[i]), int(R[i, 0])) for i in out["inst_current"]]}
     for nm in CATEGORIES:
         rr = rows[nm]
         ok = bool(rr) and all(k in shapes and r < shapes[k]["x"].shape[0] for k, r in rr)
@@ -146,7 +153,7 @@ def assemble(per_inst, shapes):
     slot = per_inst.get("cand_slot")
     out["cand_rows"] = [[((int(K[i]) + (1 if slot[i, c] >= 4 else 0)), int(R[i, slot[i, c]])) for c in range(6)]
                         if br[i] == FANOUT else None for i in range(I)] if slot is not None else None
-    out["single_rows"] = [(int(K[i]), int(R[i, 0])) if br[i] != FANOUT else None for i in range(I)]
+    out["single_rows"] = [(int(SH[i]), int(R[i, 0])) if br[i] != FANOUT else None for i in range(I)]
     return out
 
 
@@ -169,15 +176,19 @@ def _get(ctx, ptr, shape, dtype):
 
 class DeviceReplan:
     """impc_replan: I planning instances with K dynamic obstacles each (L prediction steps, horizon
-    N = params.horizon); the planner state lives in the object on the device."""
+    N = params.horizon) and num_static static obstacles each; the planner state lives in the object
+    on the device."""
 
-    def __init__(self, ctx, params, pd, I, K, L, settings, issue_cutoff_s=ISSUE_CUTOFF_S, queue_order=QUEUE_FIFO):
+    def __init__(self, ctx, params, pd, I, K, L, settings, issue_cutoff_s=ISSUE_CUTOFF_S, queue_order=QUEUE_FIFO,
+                 num_static=0):
         self.ctx, self.params, self.pd, self.I, self.K, self.L = ctx, params, pd, int(I), int(K), int(L)
+        self.S_st = int(num_static)
+        self.num_shapes = self.K + 2 + (1 if self.S_st else 0)
         self.N = params.horizon
         self.n = 13 * self.N - 5
         self.settings = settings
         cfg = ReplanConfig(instances=self.I, num_obstacles=self.K, pred_len=self.L, mpc=params, settings=settings,
-                           issue_cutoff_s=issue_cutoff_s, queue_order=queue_order)
+                           issue_cutoff_s=issue_cutoff_s, queue_order=queue_order, num_static=self.S_st)
         h = _P()
         _check(lib.impc_replan_create(ctx.h, C.byref(cfg), C.byref(h)), "impc_replan_create")
         self.h = h
@@ -212,12 +223,13 @@ class DeviceReplan:
 
     # ---- one replan
     def run_device(self, pos, vel, xref, dyn_cur, pred_pos, pred_size, prob, has_pred=None, cur_size=None,
-                   cur_count=None, solver_time_limit=0.0, elapsed_s=0.0, num_pred=None):
+                   cur_count=None, solver_time_limit=0.0, elapsed_s=0.0, num_pred=None, st_centroid=None,
+                   st_size=None, st_yaw=None):
         """impc_replan_run on device addresses (ints); the product call."""
         inp = ReplanInputs(pos=pos, vel=vel, xref=xref, dyn_cur=dyn_cur, pred_pos=pred_pos, pred_size=pred_size,
                            prob=prob, has_pred=has_pred, cur_size=cur_size, cur_count=cur_count,
                            solver_time_limit=float(solver_time_limit or 0.0), elapsed_s=float(elapsed_s),
-                           num_pred=num_pred)
+                           num_pred=num_pred, st_centroid=st_centroid, st_size=st_size, st_yaw=st_yaw)
         _check(lib.impc_replan_run(self.h, C.byref(inp)), "impc_replan_run")
 
     def advance_device(self, t, pos_ptr, vel_ptr):
@@ -231,7 +243,8 @@ class DeviceReplan:
         return {f: getattr(s, f) for f, _ in ReplanStats._fields_}
 
     def shape(self, k):
-        """impc_replan_shape k (obstacle count 0 .. K + 1): (batch handle, QP count solved, row_inst
+        """impc_replan_shape k (dynamic-obstacle count 0 .. K + 1; K + 2: the first plans with static
+        obstacles): (batch handle, QP count solved, row_inst
         and row_code device pointers, device value pointers)."""
         b, cnt, ri, rc = _P(), C.c_int64(), _P(), _P()
         ptrs = [_P() for _ in range(5)]
@@ -272,13 +285,14 @@ class DeviceReplan:
 
     def run(self, pos, vel, xref, prev=None, first_time=None, prev_count=None, dyn_cur=None, pred_pos=None,
             pred_size=None, prob=None, timings=None, solver_time_limit=None, t_start=None, profile=False,
-            has_pred=None, cur_size=None, cur_count=None, values=True, num_pred=None):
+            has_pred=None, cur_size=None, cur_count=None, values=True, num_pred=None, static=None):
         """One makePlanWithPred over all instances from host arrays (uploaded here; test plumbing
         around impc_replan_run).  Inputs: pos, vel [I][3]; xref [I][N][8] or an
         impc.ReferencePaths (getXRef on the device, from `pos`); dyn_cur [I][K][3]; pred_pos /
         pred_size [I][K][4][L][3], prob [I][K][4]; has_pred [I] (default all); num_pred [I] (K_i,
         0..K: each instance's first K_i obstacle slots; default K); cur_size [I][K][3] + cur_count [I]
-        (0..K): the current dynamic obstacles a no-prediction instance keeps (default none).  prev [I][N][8] / first_time [I]: when given, the planner state is set
+        (0..K): the current dynamic obstacles a no-prediction instance keeps (default none).  static =
+        (centroid [I][S_st][3], size [I][S_st][3], yaw [I][S_st]) with num_static > 0.  prev [I][N][8] / first_time [I]: when given, the planner state is set
         from them first (impc_replan_set_state; prev_count is implied -- 0 on a first plan, N
         otherwise -- and checked when passed); else the replan continues from the committed state.
 
@@ -323,9 +337,15 @@ class DeviceReplan:
                     cur_count=None if (cur_size is None or cur_count is None) else dev(np.asarray(cur_count).reshape(I),
                                                                                       np.int32),
                     num_pred=None if num_pred is None else dev(np.asarray(num_pred).reshape(I), np.int32))
+        if self.S_st:
+            assert static is not None, "num_static > 0: static = (centroid, size, yaw) per instance"
+            S = self.S_st
+            args.update(st_centroid=dev(np.asarray(static[0]).reshape(I, S, 3)),
+                        st_size=dev(np.asarray(static[1]).reshape(I, S, 3)),
+                        st_yaw=dev(np.asarray(static[2]).reshape(I, S)))
         self.ctx.synchronize()
         t_up = time.perf_counter() - t0
-        batches = [self.shape(k)[0] for k in range(self.K + 2)]
+        batches = [self.shape(k)[0] for k in range(self.num_shapes)]
         if profile:
             for b in batches:
                 if b:
@@ -357,9 +377,10 @@ class DeviceReplan:
                    ob_idx=_get(self.ctx, v.ob_idx, I, np.int32), cand_type=_get(self.ctx, v.cand_type, (I, 6), np.int32),
                    cand_slot=_get(self.ctx, v.cand_slot, (I, 6), np.int32), valid=_get(self.ctx, v.valid, I, np.int8),
                    num_obs=_get(self.ctx, v.num_obs, I, np.int32), slot_row=_get(self.ctx, v.slot_row, (I, 6), np.int32),
+                   shape=_get(self.ctx, v.shape, I, np.int32),
                    issued=bool(st["issued"]), time_limit=st["time_limit"])
         shapes = {}
-        for k in range(self.K + 2):
+        for k in range(self.num_shapes):
             r = self._shape_results(k, values, profile)
             if r:
                 shapes[k] = r

@@ -67,3 +67,30 @@ def test_no_device_fails_loudly():
     with pytest.raises(impc.ImpcError) as e:
         impc.Context(0)
     assert "impc_ctx_create" in str(e.value)
+
+
+def test_replan_struct_layouts_match_the_header(tmp_path):
+    """impc_replan_config / _inputs / _view: the ctypes mirror's size and field offsets equal the
+    C compiler's for include/impc_replan.h (gcc on the header itself)."""
+    import shutil
+    import subprocess
+    from impc.replan import ReplanConfig, ReplanInputs, ReplanView
+    if not shutil.which("gcc"):
+        pytest.skip("no C compiler")
+    structs = (("impc_replan_config", ReplanConfig), ("impc_replan_inputs", ReplanInputs),
+               ("impc_replan_view", ReplanView))
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "impc_replan.h"', "int main(void) {"]
+    for cname, py in structs:
+        lines.append(f'printf("%zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("%zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0; }")
+    src, exe = tmp_path / "layout.c", tmp_path / "layout"
+    src.write_text("\n".join(lines))
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    want = []
+    for _, py in structs:
+        want.append(C.sizeof(py))
+        want += [getattr(py, f).offset for f, _ in py._fields_]
+    assert got == want
