@@ -15,10 +15,12 @@
 // program dumps (outside the timed call) the branch table, the selection, the committed state and
 // each shape's QPs and solutions.
 //   replan_example <inputs.bin> <outputs.bin>
-// inputs.bin: int32 I, K, L, N, R, P; impc_mpc_params; impc_settings; pos [I][3], vel [I][3],
+// inputs.bin: int32 I, K, L, N, R, P, S; impc_mpc_params; impc_settings; pos [I][3], vel [I][3],
 // xref [I][N][8], prev [I][N][8], first_time int8 [I], dyn/pred_pos [I][K][4][L][3], pred_size
 // [I][K][4][L][3], prob [I][K][4], cur_size [I][K][3], cur_count int32 [I], has_pred int8 [R][I],
-// and when P = 1 num_pred int32 [R][I] (each instance's obstacle count per replan).
+// when P = 1 num_pred int32 [R][I] (each instance's obstacle count per replan), and when S > 0
+// each instance's S static obstacles (getStaticObstacles): centroid [I][S][3], size [I][S][3],
+// yaw [I][S].
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -82,18 +84,19 @@ int main(int argc, char **argv) {
     }
     FILE *f = std::fopen(argv[1], "rb");
     if (!f) return 2;
-    int32_t hdr[6];
+    int32_t hdr[7];
     impc_mpc_params mp{};
     impc_settings st{};
     bool ok = std::fread(hdr, sizeof hdr, 1, f) == 1 && std::fread(&mp, sizeof mp, 1, f) == 1 &&
               std::fread(&st, sizeof st, 1, f) == 1;
-    const int64_t I = hdr[0], K = hdr[1], L = hdr[2], N = hdr[3], R = hdr[4], P = hdr[5];
-    std::vector<double> pos, vel, xref, prev, pred, psize, prob, csize;
+    const int64_t I = hdr[0], K = hdr[1], L = hdr[2], N = hdr[3], R = hdr[4], P = hdr[5], S = hdr[6];
+    std::vector<double> pos, vel, xref, prev, pred, psize, prob, csize, scen, ssize, syaw;
     std::vector<int8_t> first, has_pred;
     std::vector<int32_t> ccount, npred;
     ok = ok && rd(f, pos, I * 3) && rd(f, vel, I * 3) && rd(f, xref, I * N * 8) && rd(f, prev, I * N * 8) &&
          rd(f, first, I) && rd(f, pred, I * K * 4 * L * 3) && rd(f, psize, I * K * 4 * L * 3) && rd(f, prob, I * K * 4) &&
-         rd(f, csize, I * K * 3) && rd(f, ccount, I) && rd(f, has_pred, R * I) && (!P || rd(f, npred, R * I));
+         rd(f, csize, I * K * 3) && rd(f, ccount, I) && rd(f, has_pred, R * I) && (!P || rd(f, npred, R * I)) &&
+         (!S || (rd(f, scen, I * S * 3) && rd(f, ssize, I * S * 3) && rd(f, syaw, I * S)));
     std::fclose(f);
     if (!ok || mp.horizon != N) {
         std::fprintf(stderr, "short or inconsistent input file\n");
@@ -109,6 +112,7 @@ int main(int argc, char **argv) {
     cfg.settings = st;
     cfg.issue_cutoff_s = 0.15;  // makePlanWithPred (:613)
     cfg.queue_order = IMPC_QUEUE_FIFO;
+    cfg.num_static = (int32_t)S;  // obclustering_->getStaticObstacles() per instance (:594)
     impc_replan rp = nullptr;
     CK(impc_replan_create(ctx, &cfg, &rp));
     // the planner state the scenario starts from: plan_x = previous states, zero controls
@@ -116,7 +120,7 @@ int main(int argc, char **argv) {
     for (int64_t i = 0; i < I; i++) std::memcpy(&plan[(size_t)(i * n)], &prev[(size_t)(i * N * 8)], 8 * 8 * N);
     CK(impc_replan_set_state(rp, plan.data(), first.data()));
 
-    Dev d_pos, d_vel, d_xref, d_dcur, d_pred, d_psize, d_prob, d_csize, d_ccount, d_hp, d_np;
+    Dev d_pos, d_vel, d_xref, d_dcur, d_pred, d_psize, d_prob, d_csize, d_ccount, d_hp, d_np, d_scen, d_ssize, d_syaw;
     CK(d_pos.upload(ctx, pos));
     CK(d_vel.upload(ctx, vel));
     CK(d_xref.upload(ctx, xref));
@@ -124,6 +128,11 @@ int main(int argc, char **argv) {
     CK(d_prob.upload(ctx, prob));
     CK(d_csize.upload(ctx, csize));
     CK(d_ccount.upload(ctx, ccount));
+    if (S) {
+        CK(d_scen.upload(ctx, scen));
+        CK(d_ssize.upload(ctx, ssize));
+        CK(d_syaw.upload(ctx, syaw));
+    }
     FILE *o = std::fopen(argv[2], "wb");
     if (!o) return 2;
     double call_s = 0.0;
@@ -146,6 +155,7 @@ int main(int argc, char **argv) {
         in.prob = d_prob.as<double>(), in.has_pred = d_hp.as<int8_t>();
         in.cur_size = d_csize.as<double>(), in.cur_count = d_ccount.as<int32_t>();
         in.num_pred = P ? d_np.as<int32_t>() : nullptr;
+        if (S) in.st_centroid = d_scen.as<double>(), in.st_size = d_ssize.as<double>(), in.st_yaw = d_syaw.as<double>();
         in.solver_time_limit = 0.0;
         CK(impc_ctx_synchronize(ctx));
         const auto t0 = std::chrono::steady_clock::now();
@@ -167,7 +177,9 @@ int main(int argc, char **argv) {
         put<int8_t>(o, v.valid, I, ctx);
         put<int32_t>(o, v.num_obs, I, ctx);
         put<int32_t>(o, v.slot_row, 6 * I, ctx);
-        for (int32_t s = 0; s < (int32_t)K + 2; s++) {  // shape s: the QPs with s obstacle rows per stage
+        put<int32_t>(o, v.shape, I, ctx);
+        // shape s: the QPs with s dynamic-obstacle rows per stage; K + 2: the first plans with statics
+        for (int32_t s = 0; s < (int32_t)K + 2 + (S ? 1 : 0); s++) {
             impc_batch b = nullptr;
             int64_t cnt = 0;
             const int32_t *rinst = nullptr;

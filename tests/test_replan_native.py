@@ -18,7 +18,7 @@ import impc
 from impc import scenarios
 from impc.replan import FANOUT, SINGLE_CURRENT, SINGLE_FIRST, assemble
 
-from test_replan_branches import I, K, N, _check_replan, _scenario
+from test_replan_branches import I, K, N, _check_replan, _scenario, _statics
 
 EXE = os.path.join(os.path.dirname(__file__), "native", "build", "replan_example")
 
@@ -28,7 +28,7 @@ def _read(raw, off, dtype, count):
     return a, off + a.nbytes
 
 
-def parse(raw, R, K):
+def parse(raw, R, K, S=0):
     n = 13 * N - 5
     outs, off = [], 0
     for _ in range(R):
@@ -47,8 +47,9 @@ def parse(raw, R, K):
         o["num_obs"], off = _read(raw, off, np.int32, I)
         sr, off = _read(raw, off, np.int32, 6 * I)
         o["slot_row"] = sr.reshape(I, 6)
+        o["shape"], off = _read(raw, off, np.int32, I)
         shapes = {}
-        for k in range(K + 2):
+        for k in range(K + 2 + (1 if S else 0)):
             cnt, off = _read(raw, off, np.int64, 1)
             cnt = int(cnt[0])
             if not cnt:
@@ -75,11 +76,12 @@ def parse(raw, R, K):
     return outs
 
 
-def _run(tmp_path, p, s, inst, pred_size, first, has_pred, cur_count, cur_size, num_pred=None):
+def _run(tmp_path, p, s, inst, pred_size, first, has_pred, cur_count, cur_size, num_pred=None, static=None):
     R, K, L = has_pred.shape[0], inst["pred"].shape[1], inst["pred"].shape[3]
     fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
     with open(fin, "wb") as f:
-        f.write(np.array([I, K, L, N, R, 0 if num_pred is None else 1], np.int32).tobytes())
+        S = 0 if static is None else static[2].shape[1]
+        f.write(np.array([I, K, L, N, R, 0 if num_pred is None else 1, S], np.int32).tobytes())
         f.write(bytes(p))
         f.write(bytes(s))
         for a, dt in ((inst["pos"], np.float64), (inst["vel"], np.float64), (inst["xref"], np.float64),
@@ -89,12 +91,15 @@ def _run(tmp_path, p, s, inst, pred_size, first, has_pred, cur_count, cur_size, 
             f.write(np.ascontiguousarray(a, dt).tobytes())
         if num_pred is not None:
             f.write(np.ascontiguousarray(num_pred, np.int32).tobytes())
+        if S:
+            for a in static:
+                f.write(np.ascontiguousarray(a, np.float64).tobytes())
     r = subprocess.run([EXE, str(fin), str(fout)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
-    return parse(open(fout, "rb").read(), R, K), r.stdout.strip()
+    return parse(open(fout, "rb").read(), R, K, S), r.stdout.strip()
 
 
-def _replay(outs, pd, s, inst, pred_size, first, has_pred, cur_count, cur_size, num_pred=None):
+def _replay(outs, pd, s, inst, pred_size, first, has_pred, cur_count, cur_size, num_pred=None, static=None):
     """The host replays the chain the program ran: start state, x0 / predictions after each replan."""
     plan_x = np.zeros((I, 13 * N - 5))
     plan_x[:, : 8 * N] = inst["prev"].reshape(I, -1)
@@ -106,7 +111,7 @@ def _replay(outs, pd, s, inst, pred_size, first, has_pred, cur_count, cur_size, 
         before = (plan_x, ft, None, None)
         expect, expect_first = _check_replan(out, before, pos, vel, inst["xref"], dyn_cur, pred, pred_size,
                                              inst["prob_all"], has_pred[step], cur_size, cur_count, pd, s,
-                                             num_pred=None if num_pred is None else num_pred[step])
+                                             num_pred=None if num_pred is None else num_pred[step], static=static)
         np.testing.assert_array_equal(out["plan_x"], expect)
         np.testing.assert_array_equal(out["first_time"], expect_first)
         np.testing.assert_array_equal(out["prev_count"], np.where(expect_first == 0, N, 0))
@@ -156,4 +161,31 @@ def test_cpp_per_instance_obstacle_counts(tmp_path):
     seen, _ = _replay(outs, pd, s, inst, pred_size, first, has_pred, cur_count, cur_size, num_pred)
     assert seen == {FANOUT, SINGLE_FIRST, SINGLE_CURRENT}
     assert len(set().union(*[o["shapes"] for o in outs])) >= 10
+    print(msg)
+
+
+@pytest.mark.gpu
+def test_cpp_static_obstacles(tmp_path):
+    """The same program with every instance's static obstacles (impc_replan_config.num_static = 3,
+    random yaw; obclustering_->getStaticObstacles(), mpcPlanner.cpp:594) and obstacle counts 0..6:
+    the statics enter every QP but the first plans' (shape K + 2) and the selection, checked
+    instance by instance against the restatement."""
+    Kmax, S = 6, 3
+    buckets = scenarios.intent_config(N=N, K=Kmax, instances=I, hyps=6, seed=4747)
+    inst = next(iter(buckets.values()))["instances"]
+    p, pd = impc.mpc_params(horizon=N)
+    pred_size = np.broadcast_to(inst["size"], inst["pred"].shape).copy()
+    s = impc.default_settings(verbose=0)
+    rng = np.random.default_rng(48)
+    idx = np.arange(I)
+    first = (idx % 4 == 1).astype(np.int8)
+    has_pred = np.ones((3, I), np.int8)
+    num_pred = rng.integers(0, Kmax + 1, (3, I)).astype(np.int32)
+    cur_count = rng.integers(0, Kmax + 1, I).astype(np.int32)
+    cur_size = np.broadcast_to(inst["size"], (I, Kmax, 3)).copy()
+    static = _statics(inst, S, 49, True)
+    outs, msg = _run(tmp_path, p, s, inst, pred_size, first, has_pred, cur_count, cur_size, num_pred, static)
+    seen, _ = _replay(outs, pd, s, inst, pred_size, first, has_pred, cur_count, cur_size, num_pred, static)
+    assert seen == {FANOUT, SINGLE_FIRST, SINGLE_CURRENT}
+    assert Kmax + 2 in outs[0]["shapes"]
     print(msg)
