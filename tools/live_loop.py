@@ -11,6 +11,11 @@ replan is timed from its first call to the end of its device work.  Prints one J
 synthetic stand-in for the detector keeping the obstacles in range and view, fakeDetector.cpp:493 ->
 updatePredObstacles predPos.size(), mpcPlanner.cpp:343-373; K_i = 0 replans without predictions).
 
+--statics S: every instance also carries S static obstacles (obclustering_->getStaticObstacles(),
+mpcPlanner.cpp:594; impc_replan_config.num_static) -- boxes of 0.6-1.2 m beside its own reference
+path, 0.8-1.6 m off it, at random yaw (seeded; the live planner has clustering off, :191-193, so this
+is the dormant path at scale).
+
 --gpus N: one process per GPU (started here with torch.distributed.run before anything touches a
 GPU, or under the caller's torchrun); the instances are split in contiguous ranges, every rank
 replans its own (the selection is per instance: no exchange inside a replan), a barrier and the
@@ -49,6 +54,7 @@ def main():
     ap.add_argument("--replans", type=int, default=30)
     ap.add_argument("--horizon", type=int, default=30)
     ap.add_argument("--mixed-k", action="store_true", help="per-instance obstacle counts K_i in 0..K per replan")
+    ap.add_argument("--statics", type=int, default=0, help="static obstacles per instance (num_static)")
     ap.add_argument("--gpus", type=int, default=1)
     a = ap.parse_args()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -70,11 +76,22 @@ def main():
     num_pred = None
     if a.mixed_k:
         num_pred = np.random.default_rng(4101).integers(0, K + 1, (R, Iall)).astype(np.int32)[:, lo:hi]
+    static = None
+    if a.statics:
+        rs = np.random.default_rng(4102)
+        S = a.statics
+        cen = np.empty((I, S, 3))
+        for i in range(I):
+            path = np.asarray(sc["paths"][lo + i], np.float64).reshape(-1, 3)
+            at = path[np.linspace(1, min(len(path) - 1, 6), S).astype(int)]
+            off = rs.uniform(0.8, 1.6, (S, 2)) * rs.choice([-1.0, 1.0], (S, 2))
+            cen[i] = at + np.concatenate([off, np.zeros((S, 1))], axis=1)
+        static = (cen, rs.uniform(0.6, 1.2, (I, S, 3)), rs.uniform(-np.pi, np.pi, (I, S)))
     gen_s = time.time() - t0
     p, pd, L = sc["params"], sc["pd"], sc["L"]
     # IMPC_RANK_DEVICE: every rank on that device (a rehearsal of the rank path on a one-GPU box)
     ctx = impc.Context(int(os.environ.get("IMPC_RANK_DEVICE", local_rank)))
-    rp = DeviceReplan(ctx, p, pd, I, K, L, impc.default_settings(verbose=0))
+    rp = DeviceReplan(ctx, p, pd, I, K, L, impc.default_settings(verbose=0), num_static=a.statics)
     paths = impc.ReferencePaths(ctx, list(sc["paths"][lo:hi]), pd["ts"], N)
     Dv = impc.DeviceArray
     c = np.ascontiguousarray
@@ -82,6 +99,8 @@ def main():
     psize_d, prob_d = Dv(ctx, c(sc["pred_size"][lo:hi])), Dv(ctx, c(sc["prob"][lo:hi]))
     pred_d, cur_d = Dv(ctx, c(sc["pred_pos"][:, lo:hi])), Dv(ctx, c(sc["dyn_cur"][:, lo:hi]))
     np_d = Dv(ctx, c(num_pred)) if num_pred is not None else None
+    st_d = [Dv(ctx, c(x)) for x in static] if static is not None else []
+    st_ptr = dict(zip(("st_centroid", "st_size", "st_yaw"), (d.ptr for d in st_d)))
     step_pred, step_cur = pred_d.nbytes // R, cur_d.nbytes // R
     walls, stats = [], []
     for r in range(R):
@@ -91,7 +110,7 @@ def main():
         t = time.perf_counter()
         paths.xref_device(pos_d.ptr, xref_d.ptr)
         rp.run_device(pos_d.ptr, vel_d.ptr, xref_d.ptr, cur_d.ptr + r * step_cur, pred_d.ptr + r * step_pred,
-                      psize_d.ptr, prob_d.ptr, num_pred=None if np_d is None else np_d.ptr + r * 4 * I)
+                      psize_d.ptr, prob_d.ptr, num_pred=None if np_d is None else np_d.ptr + r * 4 * I, **st_ptr)
         rp.advance_device(pd["ts"], pos_d.ptr, vel_d.ptr)
         ctx.synchronize()
         if dist is not None:
@@ -113,7 +132,8 @@ def main():
         print(json.dumps({
             "workload": f"live loop: {Iall} instances on ref_trajectory_dynus_benchmark.txt, N={N}, "
                         f"{'K_i in 0..' + str(K) + ' per instance and replan' if a.mixed_k else 'K=' + str(K)} dynamic "
-                        f"obstacles, {R} chained replans (getXRef + makePlanWithPred + follow plan 0.1 s per replan)",
+                        f"obstacles{', ' + str(a.statics) + ' static obstacles' if a.statics else ''}, {R} chained "
+                        f"replans (getXRef + makePlanWithPred + follow plan 0.1 s per replan)",
             "instances": Iall, "replans": R, "n_gpus": world, "first_replan_s": float(w[0]),
             "fanout_replan_s": fan.tolist(), "fanout_replan_s_median": float(np.median(fan)),
             "replans_per_s": float(Iall / np.median(fan)), "branches_last": st_all.astype(int).sum(axis=0).tolist(),
@@ -125,7 +145,7 @@ def main():
             "valid_plans": int(allrec[:, 4].sum()), "records_gathered": int(allrec.shape[0]),
             "ref_start_idx_mean": float(paths.last_idx().mean()), "gen_s": gen_s,
             "build_id": impc.lib.impc_build_id().decode()}), flush=True)
-    for d in (pos_d, vel_d, xref_d, psize_d, prob_d, pred_d, cur_d) + ((np_d,) if np_d is not None else ()):
+    for d in (pos_d, vel_d, xref_d, psize_d, prob_d, pred_d, cur_d) + ((np_d,) if np_d is not None else ()) + tuple(st_d):
         d.free()
     paths.close()
     rp.close()
